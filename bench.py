@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""Benchmark: fused queries/sec of the fusion + QPP hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): BEIR-NQ-shaped batches of 3,452
+queries per GPU x 5 retrievers x top-1000, synthetic lists generated on device
+(DESIGN.md "Synthetic runs"); one step = the whole path for the batch, with the
+inputs already resident in HBM:
+  1. per-query min-max of every list -> the .norm.res values (micro-units)
+  2. 13 QPP predictors per (query, retriever) list (top_k = 100, k = 50)
+  3. per-column min/max of the predictors (+ RCCL MIN all-reduce when N > 1)
+  4. normalise + "%.6f" + RSD weight per (query, retriever)
+  5. all six fusions (CombSUM, CombMNZ, RRF, W-CombSUM, W-CombMNZ, W-RRF) of
+     every query, full fused lists sorted (what write_runfile needs).
+Queries shard across ranks (weak scaling); the only collective is the 1 KB
+all-reduce of step 3.  Rank 0 prints ONE JSON line.
+
+python bench.py [--gpus N] [--steps K] [--warmup W]
+(for N > 1 launched by torch.distributed.run, one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (ROOT, ROOT / "qpp-fusion-rag_amd"):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METHODS = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md), 6.3 TB/s measured copy
+SEED = 20251212
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--queries", type=int, default=3452, help="queries per GPU")
+    ap.add_argument("--retrievers", type=int, default=5)
+    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--qpp-top-k", type=int, default=100)
+    ap.add_argument("--qpp-index", type=int, default=5)
+    ap.add_argument("--cpu-sample", type=int, default=12,
+                    help="queries timed through the Python port of the reference (0 = skip)")
+    ap.add_argument("--native-sample", type=int, default=400,
+                    help="queries timed through the C oracle (0 = skip)")
+    ap.add_argument("--check", type=int, default=8, help="queries checked bit-exact vs oracle")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def text_inputs(q_begin, Q):
+    """Deterministic per-query numTerms and text-feature columns (host, tiny)."""
+    rng = np.random.default_rng([SEED, 99, q_begin])
+    nt = rng.integers(2, 15, Q).astype(np.int32)
+    tf = np.stack([np.log1p(nt) + 0.5 * np.log1p(rng.integers(3, 14, Q)),
+                   np.log1p(rng.uniform(3, 9, Q)) * rng.uniform(0.6, 1.0, Q)], 1)
+    return nt, tf
+
+
+class Pipeline:
+    def __init__(self, args, world, rank, dev):
+        from qppfuse import engine
+        self.engine = engine
+        self.args, self.world, self.rank, self.dev = args, world, rank, dev
+        Q, R, K = args.queries, args.retrievers, args.k
+        self.Q, self.R, self.K = Q, R, K
+        self.q_begin = rank * Q
+        self.off, self.docid, self.raw = engine.synth_runs(self.q_begin, Q, R, K, seed=SEED)
+        nt, tf = text_inputs(self.q_begin, Q)
+        self.nt = torch.from_numpy(nt).to(dev)
+        self.tf = torch.from_numpy(tf).to(dev)
+        E = Q * R * K
+        self.micro = torch.empty(E, dtype=torch.int32, device=dev)
+        self.qraw = torch.empty((Q * R, 13), dtype=torch.float64, device=dev)
+        self.mm = torch.empty(2 * R * 13, dtype=torch.float64, device=dev)
+        self.out = engine.alloc_fuse_out(Q, E, engine.methods_mask(METHODS), dev)
+        self.ev = []
+        torch.cuda.synchronize()
+
+    def step(self, timed=False):
+        from qppfuse import _lib
+        e, a = self.engine, self.args
+        s = torch.cuda.current_stream().cuda_stream
+        _lib.call("qf_minmax_per_query", self.raw.data_ptr(), self.off.data_ptr(),
+                  self.Q * self.R, None, self.micro.data_ptr(), s)
+        e.qpp_raw(self.raw, self.off, self.R, a.qpp_top_k, self.nt, self.tf, out=self.qraw)
+        e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.mm, op=dist.ReduceOp.MIN)
+        w = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
+                            want_micro=False)["weights"]
+        if timed:
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+        e.fuse(self.off, self.docid, self.micro, self.R, METHODS, 60, weights=w,
+               max_entries=self.R * self.K, out=self.out)
+        if timed:
+            t1.record()
+            self.ev.append((t0, t1))
+        self.w = w
+
+    def fuse_kernel_ms(self):
+        return float(np.mean([a.elapsed_time(b) for a, b in self.ev]))
+
+    def fuse_bytes(self):
+        """Algorithmic HBM bytes of one qf_fuse launch."""
+        uc = self.out.union_count.cpu().numpy()[:self.Q].astype(np.int64)
+        N = self.Q * self.R * self.K
+        M = len(METHODS)
+        reads = N * (4 + 4) + self.Q * self.R * 8 + (self.Q * self.R + 1) * 8
+        writes = int(uc.sum()) * (4 + M * (2 + 8)) + self.Q * 4
+        return reads + writes, float(uc.mean())
+
+
+def host_sample(p: Pipeline, nq: int):
+    """Copy the first nq queries' inputs + device outputs to host numpy."""
+    R, K = p.R, p.K
+    n = nq * R * K
+    off = p.off[: nq * R + 1].cpu().numpy()
+    return dict(off=off, docid=p.docid[:n].cpu().numpy().view(np.uint32),
+                raw=p.raw[:n].cpu().numpy(), micro=p.micro[:n].cpu().numpy(),
+                w=p.w[: nq * R].cpu().numpy(), nt=p.nt[:nq].cpu().numpy(),
+                tf=p.tf[:nq].cpu().numpy(), qraw=p.qraw[: nq * R].cpu().numpy())
+
+
+def check_parity(p: Pipeline, nq: int):
+    from oracle import _loader as coracle
+    h = host_sample(p, nq)
+    sc = h["micro"].astype(np.float64) / 1e6
+    uc = p.out.union_count[:nq].cpu().numpy()
+    ok = True
+    for m, name in enumerate(METHODS):
+        _, o_uc, o_perm, o_fused = coracle.fuse(h["off"], h["docid"], sc, p.R, name, 60,
+                                                weights=h["w"])
+        f = p.out.fused[m, : nq * p.R * p.K].cpu().numpy()
+        pm = p.out.perm[m, : nq * p.R * p.K].cpu().numpy().view(np.uint16)
+        ok &= bool(np.array_equal(uc, o_uc))
+        for q in range(nq):
+            b, n = h["off"][q * p.R], uc[q]
+            ok &= f[b:b + n].tobytes() == o_fused[b:b + n].tobytes()
+            ok &= bool(np.array_equal(pm[b:b + n], o_perm[b:b + n]))
+    return ok
+
+
+def cpu_baseline_port(p: Pipeline, nq: int):
+    """The reference's per-row CPU algorithm (oracle/ref_port.py) on nq queries, 1 thread."""
+    import pandas as pd
+
+    from oracle import ref_port
+    h = host_sample(p, nq)
+    R, K = p.R, p.K
+    names = ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade", "R5", "R6", "R7"][:R]
+    qids = [f"test{p.q_begin + q}" for q in range(nq)]
+    frames, raw_lists = {}, {}
+    for r, name in enumerate(names):
+        rows_q, rows_d, rows_r, rows_s = [], [], [], []
+        for q in range(nq):
+            a, b = h["off"][q * R + r], h["off"][q * R + r + 1]
+            rows_q += [qids[q]] * (b - a)
+            rows_d += [f"doc{d}" for d in h["docid"][a:b]]
+            rows_r += list(range(1, b - a + 1))
+            rows_s += (h["micro"][a:b] / 1e6).tolist()
+            raw_lists[(qids[q], name)] = h["raw"][a:b].tolist()
+        frames[name] = pd.DataFrame({"qid": rows_q, "iter": "Q0", "docno": rows_d,
+                                     "rank": rows_r, "score": rows_s, "runid": name})
+    t0 = time.perf_counter()
+    # QPP: per (query, retriever) list, Java restated in Python (QPPBridge.java:134-453)
+    qpp = {q: {} for q in qids}
+    for (qid, name), scores in raw_lists.items():
+        qi = qids.index(qid)
+        d = ref_port.java_qpp(int(h["nt"][qi]), float(h["tf"][qi][0]), float(h["tf"][qi][1]),
+                              sorted(scores, reverse=True)[:100])
+        qpp[qid][name] = [d[n] for n in ref_port.QPP_NAMES]
+    for m in METHODS:
+        ref_port.fuse(frames, m, qpp, p.args.qpp_index, 60)
+    dt = time.perf_counter() - t0
+    return nq / dt, dt
+
+
+def cpu_baseline_native(p: Pipeline, nq: int):
+    from oracle import _loader as coracle
+    h = host_sample(p, nq)
+    sc = h["micro"].astype(np.float64) / 1e6
+    t0 = time.perf_counter()
+    for m in METHODS:
+        coracle.fuse(h["off"], h["docid"], sc, p.R, m, 60, weights=h["w"])
+    coracle.qpp_raw(h["raw"], h["off"], np.repeat(h["nt"], p.R), np.repeat(h["tf"][:, 0], p.R),
+                    np.repeat(h["tf"][:, 1], p.R))
+    dt = time.perf_counter() - t0
+    return nq / dt
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    from qppfuse import _lib
+    _lib.lib()
+    p = Pipeline(args, world, rank, dev)
+    for _ in range(args.warmup):
+        p.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        p.step(timed=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_q = args.queries * world * args.steps
+    value = total_q / elapsed
+    fuse_ms = p.fuse_kernel_ms()
+    fbytes, mean_u = p.fuse_bytes()
+    achieved = fbytes / (fuse_ms * 1e-3) / 1e9
+    parity = check_parity(p, min(args.check, args.queries)) if args.check > 0 else None
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_sample > 0:
+            v, dt = cpu_baseline_port(p, min(args.cpu_sample, args.queries))
+            cpu = {"value": round(v, 4), "unit": "fused queries/s", "cores": 1, "kind": "port",
+                   "sample": f"{min(args.cpu_sample, args.queries)} queries x {args.retrievers} "
+                             f"x top-{args.k}: 13 QPP predictors + 6 fusions through "
+                             f"oracle/ref_port.py (pandas groupby/iterrows, the reference's "
+                             f"per-row algorithm), 1 thread, {dt:.1f} s"}
+            if args.native_sample > 0:
+                cpu["native_c_oracle_value"] = round(
+                    cpu_baseline_native(p, min(args.native_sample, args.queries)), 2)
+        result = {
+            "metric": "fused queries/sec (5 retrievers x top-1000), all 6 fusions + 13 QPP",
+            "value": round(value, 2), "unit": "fused queries/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (on-device counter-based generator, DESIGN.md)",
+            "config": {"workload": "C2: BEIR-NQ-shaped, 3452 queries/GPU x 5 retrievers x "
+                                   "top-1000; min-max + QPP(13) + 6 fusions, full sorted lists",
+                       "queries_per_gpu": args.queries, "retrievers": args.retrievers,
+                       "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": METHODS,
+                       "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1)},
+            "roofline": {"bound": "hbm", "kernel": "qf_fuse", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "algorithmic_bytes_per_launch": fbytes,
+                         "kernel_ms": round(fuse_ms, 4)},
+            "cpu_baseline": cpu,
+            "parity_vs_oracle": {"queries": min(args.check, args.queries), "bit_exact": parity},
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

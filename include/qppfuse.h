@@ -1,0 +1,158 @@
+/*
+ * qppfuse.h — C-ABI of the MI355X-native fusion + QPP engine (libqppfuse.so).
+ *
+ * This is the drop-in boundary for the hot path of PoisedDok/QPP-Fusion-RAG:
+ *   src/fusion.py   (combsum/combmnz/rrf :170-230, weighted_* :237-380)
+ *   src/qpp.py      (compute_qpp_for_res_file :245-337, _normalize_qpp :340-374)
+ *   src/qpp/java/qpp/QPPBridge.java (computeQPPScores :134-191, predictors :202-453)
+ *   src/retrievers/base.py (normalize_scores :60-73)
+ * The reference has no FFI of its own (Python + a JVM subprocess speaking JSON,
+ * src/qpp.py:140-147); every entry point below replaces one of those functions and
+ * names it.  The Python mirror of the reference API (qppfuse.fusion / qppfuse.qpp)
+ * binds these symbols with ctypes — see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer (HBM) unless stated otherwise;
+ *    the library never allocates or frees caller memory.
+ *  - `stream` is a hipStream_t passed as void*; all work is stream-ordered and
+ *    asynchronous.  Functions are re-entrant; they use the current HIP device.
+ *  - Return value: QF_OK or an error code; qf_last_error() (thread-local) says why.
+ *  - Run lists are stored query-major in CSR form: list (q, r) of query q and
+ *    retriever r occupies entries [list_off[q*R + r], list_off[q*R + r + 1]).
+ */
+#ifndef QPPFUSE_H
+#define QPPFUSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------- */
+#define QF_OK       0
+#define QF_EINVAL   1 /* bad argument (null pointer, bad size, unknown method)   */
+#define QF_ETOOBIG  2 /* a query has more entries than the fusion kernel holds   */
+#define QF_EHIP     3 /* HIP runtime error (launch / device)                     */
+
+/* Per-query status written to union_count[q] by qf_fuse when it is negative. */
+#define QF_QSTATUS_TOOBIG    (-1) /* query exceeds qf_max_entries_per_query()   */
+#define QF_QSTATUS_UNSORTED  (-2) /* a list is not sorted by score, descending  */
+#define QF_QSTATUS_RANKORDER (-3) /* rank column not non-decreasing in a list   */
+#define QF_QSTATUS_BADDOC    (-4) /* docid 0xFFFFFFFF (reserved) seen           */
+#define QF_QSTATUS_DUPDOC    (-5) /* a docid repeats inside one (q, r) list     */
+
+/* ---- fusion methods (bit mask; output slot m = m-th set bit, ascending) -- */
+#define QF_COMBSUM  (1 << 0) /* ranx fuse(method="sum")   src/fusion.py:170-186 */
+#define QF_COMBMNZ  (1 << 1) /* ranx fuse(method="mnz")   src/fusion.py:189-205 */
+#define QF_RRF      (1 << 2) /* ranx fuse(method="rrf")   src/fusion.py:208-230 */
+#define QF_WCOMBSUM (1 << 3) /* weighted_combsum          src/fusion.py:237-281 */
+#define QF_WCOMBMNZ (1 << 4) /* weighted_combmnz          src/fusion.py:284-330 */
+#define QF_WRRF     (1 << 5) /* weighted_rrf              src/fusion.py:333-380 */
+#define QF_ALL_METHODS 0x3F
+
+/* ---- score column encodings --------------------------------------------- */
+#define QF_SCORE_F64   0 /* double                                              */
+#define QF_SCORE_MICRO 1 /* int32 micro-units, value = m / 1e6 (exact %.6f text) */
+
+/* ---- QPP normalisation modes (src/qpp.py:340-374) ----------------------- */
+#define QF_NORM_NONE   0
+#define QF_NORM_MINMAX 1
+
+#define QF_QPP_COLS 13 /* Java column order: nqc smv wig SigmaMax SigmaX RSD UEF
+                          MaxIDF avgidf cumnqc snqc dense-qpp dense-qpp-m
+                          (QPPBridge.java:148-188, config/defaults.yaml:164-177) */
+
+const char* qf_version(void);
+const char* qf_last_error(void);
+/* Largest Σ_r |list(q,r)| one query may have for qf_fuse. */
+int qf_max_entries_per_query(void);
+
+/*
+ * Per-query min-max normalisation of every list (BaseRetriever.normalize_scores,
+ * src/retrievers/base.py:60-73): (s - min) / (max - min), range -> 1.0 when
+ * max == min.  out_norm (nullable) gets the double; out_micro (nullable) gets
+ * the value rounded exactly as Python's f"{x:.6f}" (scripts/02_retrieve.py:80),
+ * in micro-units — i.e. exactly what the .norm.res text holds.
+ */
+int qf_minmax_per_query(const double* score, const int64_t* list_off, int64_t n_lists,
+                        double* out_norm, int32_t* out_micro, void* stream);
+
+/*
+ * Raw QPP predictors, one row of QF_QPP_COLS doubles per list
+ * (QPPBridge.computeQPPScores, QPPBridge.java:134-191, after the driver's
+ * sort-desc + [:top_k] truncation, src/qpp.py:304-305).  Lists must be sorted
+ * by score, descending.  Scores are rounded to float32 as Java's
+ * JsonElement.getAsFloat() does (QPPBridge.java:67-70), then the first
+ * k = min(50, n) are used.  num_terms[q] = max(1, |lower(text).split("\\s+")|),
+ * text_feat[2q], text_feat[2q+1] = MaxIDF / avgidf proxies (host string work,
+ * QPPBridge.java:368-393).  Empty lists get an all-zero row (Java returns an
+ * empty map; src/qpp.py:321 maps missing names to 0.0).
+ */
+int qf_qpp_raw(const double* score, const int64_t* list_off, int64_t n_queries,
+               int32_t n_retrievers, int32_t top_k, const int32_t* num_terms,
+               const double* text_feat, double* raw_out, void* stream);
+
+/*
+ * Column minima / maxima of the raw predictors over the queries of each
+ * retriever that have a non-empty list (src/qpp.py:347-358).  mm_out holds
+ * 2*R*13 doubles: [0, R*13) = min, [R*13, 2*R*13) = -max, so that a single
+ * element-wise MIN all-reduce (RCCL) combines query shards.
+ */
+int qf_qpp_colminmax(const double* raw, const int64_t* list_off, int64_t n_queries,
+                     int32_t n_retrievers, double* mm_out, void* stream);
+
+/*
+ * Normalise raw predictors with mm (src/qpp.py:362-372) and round each value
+ * as the .qpp writer's f"{s:.6f}" does (src/qpp.py:333): micro_out (nullable,
+ * int64 micro-units) and norm_out (nullable, the unrounded double).  Then, if
+ * w_out is non-null, the fusion weight of every (q, r) as
+ * get_qpp_weight (src/fusion.py:116-158) reads it back from the .qpp text:
+ * column qpp_index, or the mean of the 13 columns when qpp_index == -1.
+ */
+int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_off,
+                     int64_t n_queries, int32_t n_retrievers, int32_t mode,
+                     int32_t qpp_index, double* norm_out, int64_t* micro_out,
+                     double* w_out, void* stream);
+
+/*
+ * Multi-method rank fusion of every query in one launch (one workgroup per
+ * query; LDS hash-join over docids, deterministic ordered reductions,
+ * stable LDS radix sort by fused score).
+ *
+ * Inputs (device): list_off[Q*R+1] (int64), docid[E] (uint32, interned
+ * docnos, 0xFFFFFFFF reserved), score[E] (score_kind), rank[E] (nullable
+ * int32 file rank column for W-RRF, src/fusion.py:372-374; NULL = position+1),
+ * weights[Q*R] (nullable unless a weighted method is requested).
+ * Preconditions per list: scores non-increasing; no docid repeated.
+ *
+ * Outputs (device), query q owns slots [list_off[q*R], list_off[q*R+R]):
+ *   union_docid  — the query's distinct docids in first-seen order
+ *                  (retriever order, then list position), u = 0..U_q-1
+ *   union_count[q] = U_q (or a negative QF_QSTATUS_* code)
+ *   for the m-th requested method (ascending bit order), at offset m*out_stride:
+ *     perm[...]  — u of the i-th fused document (uint16)
+ *     fused[...] — its fused score (double), sorted descending; ties keep
+ *                  first-seen order (Python's stable sort, src/fusion.py:475,488)
+ */
+int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+            const uint32_t* docid, const void* score, int32_t score_kind,
+            const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
+            int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
+            uint16_t* perm, double* fused, int64_t out_stride, void* stream);
+
+/*
+ * Benchmark / test support: generate Q*R synthetic lists of K entries
+ * (docid, raw score sorted descending) on device, deterministic in seed.
+ * list_off[Q*R+1] is written too.  See DESIGN.md "Synthetic runs".
+ */
+int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
+                  uint64_t seed, double p_shared, int64_t* list_off, uint32_t* docid,
+                  double* score, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QPPFUSE_H */

@@ -1,0 +1,124 @@
+// qf_capi.hip — the C-ABI of libqppfuse.so (declared in include/qppfuse.h).
+// Argument validation, kernel selection, thread-local error strings.  No entry
+// point allocates, frees or synchronises: everything is stream-ordered on the
+// caller's stream, so a caller may capture the whole pipeline in a hipGraph.
+#include <cstdio>
+#include <string>
+
+#include "../../include/qppfuse.h"
+#include "qf_internal.h"
+#include <cstdarg>
+
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int check(hipError_t e, const char* what) {
+  if (e != hipSuccess) return fail(QF_EHIP, "%s: %s", what, hipGetErrorString(e));
+  g_err.clear();
+  return QF_OK;
+}
+
+constexpr int kMaxR = 16;
+}  // namespace
+
+extern "C" {
+
+const char* qf_version(void) { return "qppfuse 0.1.0 gfx950"; }
+const char* qf_last_error(void) { return g_err.c_str(); }
+int qf_max_entries_per_query(void) { return qf::fuse_max_entries(); }
+
+int qf_minmax_per_query(const double* score, const int64_t* list_off, int64_t n_lists,
+                        double* out_norm, int32_t* out_micro, void* stream) {
+  if (n_lists < 0 || (n_lists > 0 && (!score || !list_off)))
+    return fail(QF_EINVAL, "qf_minmax_per_query: bad arguments");
+  if (!out_norm && !out_micro) return fail(QF_EINVAL, "qf_minmax_per_query: no output");
+  return check(qf::minmax_launch(score, list_off, n_lists, out_norm, out_micro,
+                                 (hipStream_t)stream),
+               "qf_minmax_per_query");
+}
+
+int qf_qpp_raw(const double* score, const int64_t* list_off, int64_t n_queries,
+               int32_t n_retrievers, int32_t top_k, const int32_t* num_terms,
+               const double* text_feat, double* raw_out, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || !list_off || !num_terms || !text_feat || !raw_out ||
+      (!score && n_queries > 0))
+    return fail(QF_EINVAL, "qf_qpp_raw: bad arguments");
+  return check(qf::qpp_raw_launch(score, list_off, n_queries, n_retrievers, top_k, num_terms,
+                                  text_feat, raw_out, (hipStream_t)stream),
+               "qf_qpp_raw");
+}
+
+int qf_qpp_colminmax(const double* raw, const int64_t* list_off, int64_t n_queries,
+                     int32_t n_retrievers, double* mm_out, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off || !mm_out)
+    return fail(QF_EINVAL, "qf_qpp_colminmax: bad arguments");
+  return check(qf::qpp_colminmax_launch(raw, list_off, n_queries, n_retrievers, mm_out,
+                                        (hipStream_t)stream),
+               "qf_qpp_colminmax");
+}
+
+int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_off,
+                     int64_t n_queries, int32_t n_retrievers, int32_t mode, int32_t qpp_index,
+                     double* norm_out, int64_t* micro_out, double* w_out, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off || (mode == QF_NORM_MINMAX && !mm))
+    return fail(QF_EINVAL, "qf_qpp_normalize: bad arguments");
+  if (mode != QF_NORM_NONE && mode != QF_NORM_MINMAX)
+    return fail(QF_EINVAL, "qf_qpp_normalize: unsupported mode %d", mode);
+  if (qpp_index < -1 || qpp_index >= QF_QPP_COLS)
+    return fail(QF_EINVAL, "qf_qpp_normalize: qpp_index %d out of range", qpp_index);
+  return check(qf::qpp_normalize_launch(raw, mm, list_off, n_queries, n_retrievers, mode,
+                                        qpp_index, norm_out, micro_out, w_out,
+                                        (hipStream_t)stream),
+               "qf_qpp_normalize");
+}
+
+int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+            const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
+            const double* weights, int32_t methods, int32_t rrf_k, int32_t max_entries,
+            uint32_t* union_docid, int32_t* union_count, uint16_t* perm, double* fused,
+            int64_t out_stride, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
+    return fail(QF_EINVAL, "qf_fuse: n_retrievers must be in [1, %d]", kMaxR);
+  if (methods <= 0 || (methods & ~QF_ALL_METHODS))
+    return fail(QF_EINVAL, "qf_fuse: bad method mask 0x%x", methods);
+  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF)) && !weights)
+    return fail(QF_EINVAL, "qf_fuse: weighted method requested without weights");
+  if (score_kind != QF_SCORE_F64 && score_kind != QF_SCORE_MICRO)
+    return fail(QF_EINVAL, "qf_fuse: bad score_kind %d", score_kind);
+  if (max_entries > qf::fuse_max_entries())
+    return fail(QF_ETOOBIG, "qf_fuse: %d entries in one query exceed the kernel limit %d",
+                max_entries, qf::fuse_max_entries());
+  if (n_queries == 0) return QF_OK;
+  if (!list_off || !docid || !score || !union_docid || !union_count || !perm || !fused ||
+      out_stride < 0)
+    return fail(QF_EINVAL, "qf_fuse: null buffer");
+  qf::FuseParams p{n_queries, n_retrievers, list_off, docid, score, rank, weights, methods,
+                   rrf_k, union_docid, union_count, perm, fused, out_stride};
+  return check(qf::fuse_launch(p, score_kind, max_entries < 1 ? 1 : max_entries,
+                               (hipStream_t)stream),
+               "qf_fuse");
+}
+
+int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
+                  uint64_t seed, double p_shared, int64_t* list_off, uint32_t* docid,
+                  double* score, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || k <= 0 || !list_off || !docid || !score)
+    return fail(QF_EINVAL, "qf_synth_runs: bad arguments");
+  return check(qf::synth_launch(q_begin, n_queries, n_retrievers, k, seed, p_shared, list_off,
+                                docid, score, (hipStream_t)stream),
+               "qf_synth_runs");
+}
+
+}  // extern "C"

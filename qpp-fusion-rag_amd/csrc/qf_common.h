@@ -1,0 +1,111 @@
+// qf_common.h — device helpers shared by the qppfuse HIP kernels (gfx950 / CDNA4).
+//
+// Everything here is written for a 64-lane wavefront.  The library is compiled
+// with -ffp-contract=off: the reference's arithmetic is sequential IEEE double
+// (Python floats, Java doubles) and an FMA contraction would change results.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qf {
+
+constexpr int kWave = 64;
+constexpr int kQppCols = 13;
+
+// ---- wave-level primitives ------------------------------------------------
+
+// Number of set bits of `mask` below this lane (v_mbcnt_lo/hi).
+__device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Inclusive prefix sum across the 64 lanes of a wave.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = fmin(v, __shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v |= __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_and(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v &= __shfl_xor(v, d, 64);
+  return v;
+}
+
+// ---- numerics ---------------------------------------------------------------
+
+// Exact Python f"{x:.6f}" rounding, returned in micro-units: the integer m with
+// m = round-half-even(x * 10^6) computed on the EXACT binary value of x (what
+// CPython's correctly rounded formatting does).  fma() gives the exact sign of
+// x*1e6 - c because it rounds only once.
+__host__ __device__ __forceinline__ long long round6(double x) {
+  double f = floor(x * 1e6);
+  if (fma(x, 1e6, -f) < 0.0) f -= 1.0;
+  else if (fma(x, 1e6, -(f + 1.0)) >= 0.0) f += 1.0;
+  const double r = fma(x, 1e6, -(f + 0.5));
+  long long m = (long long)f;
+  if (r > 0.0 || (r == 0.0 && (m & 1))) m += 1;
+  return m;
+}
+
+// Java's compensated summation as used by DoubleStream.sum()/average()
+// (java.util.stream.Collectors.sumWithCompensation / computeFinalSum, JDK 11-17).
+// QPPBridge.java calls Arrays.stream(rsvs).average() and list.stream().average().
+struct Kahan {
+  double s, c, simple;
+};
+__host__ __device__ __forceinline__ void kahan_init(Kahan& k) { k.s = 0.0; k.c = 0.0; k.simple = 0.0; }
+__host__ __device__ __forceinline__ void kahan_add(Kahan& k, double v) {
+  const double tmp = v - k.c;
+  const double sum = k.s;
+  const double velvel = sum + tmp;
+  k.c = (velvel - sum) - tmp;
+  k.s = velvel;
+  k.simple += v;
+}
+__host__ __device__ __forceinline__ double kahan_final(const Kahan& k) {
+#ifdef QF_JDK18_FINAL_SUM
+  const double tmp = k.s - k.c;  // JDK >= 18 (JDK-8214761)
+#else
+  const double tmp = k.s + k.c;  // JDK 11..17
+#endif
+  if (isnan(tmp) && isinf(k.simple)) return k.simple;
+  return tmp;
+}
+
+// Order-preserving map of a double to uint64 (ascending), with -0.0 folded
+// onto +0.0 so that the two compare equal, as Python's sort sees them.
+__device__ __forceinline__ uint64_t f64_asc_key(double v) {
+  if (v == 0.0) v = 0.0;
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double f64_from_asc_key(uint64_t k) {
+  const uint64_t b = (k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __longlong_as_double((long long)b);
+}
+
+}  // namespace qf

@@ -1,0 +1,43 @@
+// qf_internal.h — launcher declarations shared by the kernel files and the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qf {
+
+struct FuseParams {
+  int64_t n_queries;
+  int32_t R;
+  const int64_t* list_off;
+  const uint32_t* docid;
+  const void* score;
+  const int32_t* rank;
+  const double* weights;
+  int32_t methods;
+  int32_t rrf_k;
+  uint32_t* union_docid;
+  int32_t* union_count;
+  uint16_t* perm;
+  double* fused;
+  int64_t out_stride;
+};
+
+int fuse_max_entries();
+hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);
+hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t Q, int32_t R,
+                          int32_t top_k, const int32_t* nt, const double* tf, double* out,
+                          hipStream_t st);
+hipError_t qpp_colminmax_launch(const double* raw, const int64_t* list_off, int64_t Q, int32_t R,
+                                double* mm, hipStream_t st);
+hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64_t* list_off,
+                                int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
+                                double* norm_out, int64_t* micro_out, double* w_out,
+                                hipStream_t st);
+hipError_t minmax_launch(const double* score, const int64_t* list_off, int64_t n_lists,
+                         double* out_norm, int32_t* out_micro, hipStream_t st);
+hipError_t synth_launch(int64_t q_begin, int64_t n_queries, int32_t R, int32_t K, uint64_t seed,
+                        double p_shared, int64_t* list_off, uint32_t* docid, double* score,
+                        hipStream_t st);
+
+}  // namespace qf

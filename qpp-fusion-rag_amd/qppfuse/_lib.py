@@ -1,0 +1,85 @@
+"""ctypes binding of libqppfuse.so (C-ABI declared in include/qppfuse.h).
+
+There is deliberately no fallback: if the HIP library is missing or fails to
+load, every entry point of qppfuse raises.  See INTEGRATION.md.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+from ._build import LIB_PATH
+
+QF_OK, QF_EINVAL, QF_ETOOBIG, QF_EHIP = 0, 1, 2, 3
+QF_QSTATUS = {-1: "query exceeds the fusion kernel's entry limit",
+              -2: "run list not sorted by score descending",
+              -3: "rank column not non-decreasing within a run list",
+              -4: "reserved docid 0xFFFFFFFF",
+              -5: "a docno repeats within one run list (unsupported)"}
+
+COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF = (1 << i for i in range(6))
+METHOD_BITS = {"combsum": COMBSUM, "combmnz": COMBMNZ, "rrf": RRF,
+               "wcombsum": WCOMBSUM, "wcombmnz": WCOMBMNZ, "wrrf": WRRF}
+SCORE_F64, SCORE_MICRO = 0, 1
+NORM_NONE, NORM_MINMAX = 0, 1
+QPP_COLS = 13
+
+# name -> (restype, argtypes); must match include/qppfuse.h
+_vp, _i32, _i64, _u64, _f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
+SIGNATURES = {
+    "qf_version": (C.c_char_p, []),
+    "qf_last_error": (C.c_char_p, []),
+    "qf_max_entries_per_query": (C.c_int, []),
+    "qf_minmax_per_query": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "qf_qpp_raw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
+                          _vp, _vp, _vp, _vp, _i64, _vp]),
+    "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
+}
+
+
+class QPPFuseError(RuntimeError):
+    """A libqppfuse call failed (maps the C status code and qf_last_error())."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"qppfuse error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load libqppfuse.so once; raise loudly when it is absent."""
+    global _LIB
+    if _LIB is None:
+        path = Path(LIB_PATH)
+        if not path.exists():
+            raise ImportError(
+                f"libqppfuse.so not built at {path}. Run `python __graft_entry__.py build` "
+                "(hipcc --offload-arch=gfx950). qppfuse has no CPU fallback.")
+        handle = C.CDLL(str(path))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype, fn.argtypes = res, args
+        _LIB = handle
+    return _LIB
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != QF_OK:
+        msg = lib().qf_last_error().decode(errors="replace")
+        if rc == QF_EINVAL:
+            raise ValueError(f"{name}: {msg}")
+        raise QPPFuseError(rc, f"{name}: {msg}")
+
+
+def version() -> str:
+    return lib().qf_version().decode()
+
+
+def max_entries_per_query() -> int:
+    return int(lib().qf_max_entries_per_query())

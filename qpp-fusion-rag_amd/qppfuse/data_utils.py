@@ -1,0 +1,66 @@
+"""File loaders of the path (boundary only): .qpp scores, TREC runs, qrels.
+
+Same results and errors as the reference's src/data_utils.py loaders
+(load_qrels :175-197, load_run_file :204-231, load_run_as_dict :234-255,
+load_qpp_scores :262-293).  Host text parsing — no compute to accelerate.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from pathlib import Path
+from typing import Dict, List, Tuple, Union
+
+PathLike = Union[str, Path]
+
+
+def load_qrels(qrels_path: PathLike) -> Dict[str, Dict[str, int]]:
+    """BEIR qrels TSV (header line skipped) -> {qid: {docid: rel}}."""
+    out: Dict[str, Dict[str, int]] = defaultdict(dict)
+    with open(qrels_path, "r") as fh:
+        next(fh, None)
+        for line in fh:
+            f = line.strip().split("\t")
+            if len(f) >= 3:
+                out[f[0]][f[1]] = int(f[2])
+    return dict(out)
+
+
+def load_run_file(run_path: PathLike) -> Dict[str, List[Tuple[str, float, int]]]:
+    """TREC run -> {qid: [(docid, score, rank)]} sorted by rank (stable)."""
+    out: Dict[str, list] = defaultdict(list)
+    with open(run_path, "r") as fh:
+        for line in fh:
+            f = line.strip().split()
+            if len(f) >= 6:
+                out[f[0]].append((f[2], float(f[4]), int(f[3])))
+    for qid in out:
+        out[qid].sort(key=lambda x: x[2])
+    return dict(out)
+
+
+def load_run_as_dict(run_path: PathLike) -> Dict[str, Dict[str, float]]:
+    out: Dict[str, Dict[str, float]] = defaultdict(dict)
+    with open(run_path, "r") as fh:
+        for line in fh:
+            f = line.strip().split()
+            if len(f) >= 5:
+                out[f[0]][f[2]] = float(f[4])
+    return dict(out)
+
+
+def load_qpp_scores(qpp_path: PathLike) -> Dict[str, Dict[str, List[float]]]:
+    """Directory of <Retriever>.res.mmnorm.qpp -> {qid: {retriever: [13 floats]}}."""
+    qpp_path = Path(qpp_path)
+    files = list(qpp_path.glob("*.mmnorm.qpp"))
+    if not files:
+        raise FileNotFoundError(f"No .mmnorm.qpp files in {qpp_path}")
+    out: Dict[str, Dict[str, List[float]]] = defaultdict(dict)
+    for fp in files:
+        retriever = fp.stem.replace(".res.mmnorm", "")
+        with open(fp, "r") as fh:
+            for line in fh:
+                f = line.strip().split("\t")
+                if len(f) < 2:
+                    continue
+                out[f[0]][retriever] = [float(x) for x in f[1:]]
+    return dict(out)

@@ -1,0 +1,165 @@
+"""Device-level entry points: torch tensors (HBM buffers) in, torch tensors out.
+
+PyTorch is only the allocator / stream owner here; all compute is the HIP code
+in libqppfuse.so, launched on torch's current stream so that RCCL collectives
+(torch.distributed, backend "nccl") order correctly with the kernels.
+Every function raises if no ROCm device or no library is present — there is no
+CPU path.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+
+_MNAMES = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+
+
+def require_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("qppfuse needs a ROCm GPU (gfx950 / MI355X); it has no CPU fallback")
+    _lib.lib()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError("qppfuse expects contiguous device tensors")
+    return t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def methods_mask(methods) -> int:
+    if isinstance(methods, int):
+        return methods
+    mask = 0
+    for m in methods:
+        mask |= _lib.METHOD_BITS[m]
+    return mask
+
+
+def method_names(mask: int):
+    return [n for i, n in enumerate(_MNAMES) if (mask >> i) & 1]
+
+
+@dataclass
+class FuseOut:
+    """Device outputs of qf_fuse for one launch."""
+    union_docid: torch.Tensor  # int32 view of uint32 [E]
+    union_count: torch.Tensor  # int32 [Q]
+    perm: torch.Tensor         # int16 view of uint16 [M, E]
+    fused: torch.Tensor        # float64 [M, E]
+    methods: list
+
+
+def alloc_fuse_out(n_queries: int, n_entries: int, mask: int, device) -> FuseOut:
+    M = bin(mask).count("1")
+    E = max(int(n_entries), 1)
+    return FuseOut(torch.empty(E, dtype=torch.int32, device=device),
+                   torch.empty(max(n_queries, 1), dtype=torch.int32, device=device),
+                   torch.empty((M, E), dtype=torch.int16, device=device),
+                   torch.empty((M, E), dtype=torch.float64, device=device),
+                   method_names(mask))
+
+
+def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_retrievers: int,
+         methods, rrf_k: int = 60, weights: Optional[torch.Tensor] = None,
+         rank: Optional[torch.Tensor] = None, max_entries: Optional[int] = None,
+         out: Optional[FuseOut] = None) -> FuseOut:
+    """qf_fuse over every query of a packed run set (see include/qppfuse.h)."""
+    dev = require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    E = docid.numel()
+    mask = methods_mask(methods)
+    if score.dtype == torch.int32:
+        kind = _lib.SCORE_MICRO
+    elif score.dtype == torch.float64:
+        kind = _lib.SCORE_F64
+    else:
+        raise TypeError("score must be float64 or int32 micro-units")
+    if max_entries is None:
+        raise ValueError("max_entries (largest per-query entry count) is required")
+    if out is None:
+        out = alloc_fuse_out(Q, E, mask, dev)
+    _lib.call("qf_fuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
+              _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
+              _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused), out.fused.shape[1],
+              _stream())
+    return out
+
+
+def minmax_per_query(score: torch.Tensor, list_off: torch.Tensor, want_norm=True,
+                     want_micro=True):
+    require_device()
+    n_lists = list_off.numel() - 1
+    norm = torch.empty_like(score) if want_norm else None
+    micro = torch.empty(score.shape, dtype=torch.int32, device=score.device) if want_micro else None
+    _lib.call("qf_minmax_per_query", _ptr(score), _ptr(list_off), n_lists, _ptr(norm),
+              _ptr(micro), _stream())
+    return norm, micro
+
+
+def qpp_raw(score: torch.Tensor, list_off: torch.Tensor, n_retrievers: int, top_k: int,
+            num_terms: torch.Tensor, text_feat: torch.Tensor,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    if out is None:
+        out = torch.empty((Q * R, _lib.QPP_COLS), dtype=torch.float64, device=list_off.device)
+    _lib.call("qf_qpp_raw", _ptr(score), _ptr(list_off), Q, R, int(top_k), _ptr(num_terms),
+              _ptr(text_feat), _ptr(out), _stream())
+    return out
+
+
+def qpp_colminmax(raw: torch.Tensor, list_off: torch.Tensor, n_retrievers: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[2*R*13]: column minima then negated maxima (MIN all-reduce combines shards)."""
+    require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    if out is None:
+        out = torch.empty(2 * R * _lib.QPP_COLS, dtype=torch.float64, device=raw.device)
+    _lib.call("qf_qpp_colminmax", _ptr(raw), _ptr(list_off), Q, R, _ptr(out), _stream())
+    return out
+
+
+def qpp_normalize(raw: torch.Tensor, mm: Optional[torch.Tensor], list_off: torch.Tensor,
+                  n_retrievers: int, mode: str = "minmax", qpp_index: int = 5,
+                  want_norm=False, want_micro=True, want_weights=True) -> Dict[str, torch.Tensor]:
+    require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    dev = raw.device
+    mode_id = {"none": _lib.NORM_NONE, "minmax": _lib.NORM_MINMAX}.get(mode)
+    if mode_id is None:
+        raise NotImplementedError(f"QPP normalisation '{mode}' is not implemented on device")
+    norm = torch.empty_like(raw) if want_norm else None
+    micro = torch.empty(raw.shape, dtype=torch.int64, device=dev) if want_micro else None
+    w = torch.empty(Q * R, dtype=torch.float64, device=dev) if want_weights else None
+    _lib.call("qf_qpp_normalize", _ptr(raw), _ptr(mm), _ptr(list_off), Q, R, mode_id,
+              int(qpp_index), _ptr(norm), _ptr(micro), _ptr(w), _stream())
+    return {"norm": norm, "micro": micro, "weights": w}
+
+
+def synth_runs(q_begin: int, n_queries: int, n_retrievers: int, k: int, seed: int = 20251212,
+               p_shared: float = 0.7, device=None):
+    """Synthetic (list_off, docid, raw score) on device; see DESIGN.md."""
+    dev = device or require_device()
+    E = n_queries * n_retrievers * k
+    list_off = torch.empty(n_queries * n_retrievers + 1, dtype=torch.int64, device=dev)
+    docid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+    score = torch.empty(max(E, 1), dtype=torch.float64, device=dev)
+    _lib.call("qf_synth_runs", int(q_begin), int(n_queries), int(n_retrievers), int(k),
+              int(seed) & (2**64 - 1), float(p_shared), _ptr(list_off), _ptr(docid), _ptr(score),
+              _stream())
+    return list_off, docid[:E], score[:E]

@@ -1,0 +1,311 @@
+"""Drop-in replacement for the reference's src/fusion.py, computed on MI355X.
+
+Same public names, signatures, return shapes and exceptions as
+PoisedDok/QPP-Fusion-RAG src/fusion.py (imported by scripts/05_fusion.py:40-53):
+load_runs, load_qpp_scores, get_qpp_weight, get_qpp_index, combsum, combmnz,
+rrf, weighted_combsum, weighted_combmnz, weighted_rrf, learned_fusion,
+write_runfile, run_fusion.
+
+What changes is where the work happens: the runs are packed once into CSR
+columns (qppfuse.runset), uploaded to HBM, and every requested method is
+computed for every query by one launch of the HIP kernel qf_fuse
+(csrc/qf_fuse.hip).  Results come back as a FusedRun — a read-only Mapping
+{qid: [(docno, score), ...]} that materialises lists on access — in the order
+the reference returns them: score-descending for combsum/combmnz/rrf (ranx +
+_ranx_to_dict, src/fusion.py:469-477), first-seen order for the weighted
+methods (src/fusion.py:278-279).
+"""
+from __future__ import annotations
+
+import os
+import weakref
+from collections.abc import Mapping
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pandas as pd
+
+from . import engine
+from .config import ConfigError, config
+from .config import get_qpp_index as _cfg_qpp_index
+from .data_utils import load_qpp_scores as _load_qpp
+from .runset import RunSet, pack_frames, reorder
+
+__all__ = ["load_runs", "load_qpp_scores", "get_qpp_weight", "get_qpp_index", "combsum",
+           "combmnz", "rrf", "weighted_combsum", "weighted_combmnz", "weighted_rrf",
+           "learned_fusion", "write_runfile", "run_fusion", "fuse_many", "FusedRun",
+           "ConfigError"]
+
+UNWEIGHTED = ("combsum", "combmnz", "rrf")
+WEIGHTED = ("wcombsum", "wcombmnz", "wrrf")
+
+
+# ------------------------------------------------------------------ loading --
+
+def load_runs(res_path: str, use_normalized: bool = True) -> Dict[str, pd.DataFrame]:
+    """{ranker: DataFrame[qid, iter, docno, rank, score, runid]} in os.listdir order."""
+    suffix = ".norm.res" if use_normalized else ".res"
+    files = [f for f in os.listdir(res_path) if f.endswith(suffix)]
+    if not files:
+        raise FileNotFoundError(f"No {suffix} files found in {res_path}")
+    runs = {}
+    for f in files:
+        df = pd.read_csv(os.path.join(res_path, f), sep=r"\s+",
+                         names=["qid", "iter", "docno", "rank", "score", "runid"],
+                         dtype={"qid": str, "docno": str})
+        df["qid"] = df["qid"].astype(str)
+        runs[f.replace(suffix, "")] = df
+    return runs
+
+
+def load_qpp_scores(qpp_path: str) -> Dict[str, Dict[str, List[float]]]:
+    return _load_qpp(qpp_path)
+
+
+def get_qpp_weight(qid: str, ranker: str, qpp_data, qpp_index: int = None,
+                   fusion_mode: bool = False) -> float:
+    """Weight of (query, ranker); KeyError / IndexError exactly where the reference raises."""
+    if qpp_index is None:
+        qpp_index = config.qpp.default_index
+    if qid not in qpp_data:
+        raise KeyError(f"QPP data missing for query '{qid}'. Run QPP computation first.")
+    if ranker not in qpp_data[qid]:
+        raise KeyError(f"QPP data missing for ranker '{ranker}' on query '{qid}'. "
+                       f"Available: {list(qpp_data[qid].keys())}")
+    vals = qpp_data[qid][ranker]
+    if fusion_mode or qpp_index == -1:
+        return sum(vals) / len(vals)
+    if qpp_index >= len(vals):
+        raise IndexError(f"QPP index {qpp_index} out of range. Available: 0-{len(vals)-1}")
+    return vals[qpp_index]
+
+
+def get_qpp_index(model_name: str) -> int:
+    return _cfg_qpp_index(model_name)
+
+
+# --------------------------------------------------------------- results -----
+
+def qid_sort_key(x: str):
+    """write_runfile's qid order (src/fusion.py:487); mixed kinds raise TypeError."""
+    return int(x.replace("test", "")) if x.startswith("test") else x
+
+
+class FusedRun(Mapping):
+    """{qid: [(docno, score)]} backed by the kernel's packed output arrays."""
+
+    def __init__(self, qids, docnos, qbase, counts, union_docid, perm, fused, order: str):
+        self._qids = list(qids)
+        self._index = {q: i for i, q in enumerate(self._qids)}
+        self._docnos = docnos
+        self._qbase = qbase
+        self._counts = counts
+        self._udoc = union_docid
+        self._perm = perm
+        self._fused = fused
+        self.order = order  # "sorted" or "first_seen"
+
+    def __len__(self):
+        return len(self._qids)
+
+    def __iter__(self):
+        return iter(self._qids)
+
+    def __contains__(self, qid):
+        return qid in self._index
+
+    def arrays(self, qid) -> Tuple[np.ndarray, np.ndarray]:
+        """(docno ids, scores) of one query in score-descending order."""
+        i = self._index[qid]
+        b, n = int(self._qbase[i]), int(self._counts[i])
+        p = self._perm[b:b + n].astype(np.int64)
+        return self._udoc[b + p], self._fused[b:b + n]
+
+    def __getitem__(self, qid) -> List[Tuple[str, float]]:
+        i = self._index[qid]
+        b, n = int(self._qbase[i]), int(self._counts[i])
+        p = self._perm[b:b + n].astype(np.int64)
+        s = self._fused[b:b + n]
+        if self.order == "sorted":
+            docs = self._docnos[self._udoc[b + p]]
+            return list(zip(docs.tolist(), s.tolist()))
+        by_u = np.empty(n, dtype=np.float64)
+        by_u[p] = s
+        docs = self._docnos[self._udoc[b:b + n]]
+        return list(zip(docs.tolist(), by_u.tolist()))
+
+    def to_dict(self) -> Dict[str, List[Tuple[str, float]]]:
+        return {q: self[q] for q in self._qids}
+
+
+# ---------------------------------------------------------------- packing ----
+
+_PACK_CACHE: Dict[tuple, RunSet] = {}
+
+
+def _pack(runs: Dict[str, pd.DataFrame]) -> RunSet:
+    """Pack once per runs dict (cached on the frames' identity while they live)."""
+    key = tuple((name, id(df), len(df)) for name, df in runs.items())
+    rs = _PACK_CACHE.get(key)
+    if rs is None:
+        rs = pack_frames(runs)
+        _PACK_CACHE.clear()
+        _PACK_CACHE[key] = rs
+        for df in runs.values():
+            weakref.finalize(df, _PACK_CACHE.pop, key, None)
+    return rs
+
+
+def _weights(rs: RunSet, qpp_data, qpp_index: int) -> np.ndarray:
+    """[Q*R] weights in the reference's visiting order, raising as it does."""
+    fusion_mode = qpp_index == -1
+    w = np.empty(rs.n_queries * rs.n_rankers, dtype=np.float64)
+    k = 0
+    for qid in rs.qids:
+        for ranker in rs.rankers:
+            w[k] = get_qpp_weight(qid, ranker, qpp_data, qpp_index, fusion_mode)
+            k += 1
+    return w
+
+
+def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np.ndarray]):
+    import torch
+    engine.require_device()
+    d = rs.to_device()
+    wd = None if weights is None else torch.from_numpy(weights).to(d["list_off"].device)
+    out = engine.fuse(d["list_off"], d["docid"], d["score"], rs.n_rankers, list(methods),
+                      rrf_k=rrf_k, weights=wd, rank=d["rank"], max_entries=rs.max_entries())
+    counts = out.union_count.cpu().numpy()[:rs.n_queries]
+    bad = np.nonzero(counts < 0)[0]
+    if bad.size:
+        from ._lib import QF_QSTATUS
+        code = int(counts[bad[0]])
+        raise ValueError(f"query '{rs.qids[bad[0]]}': {QF_QSTATUS.get(code, code)}")
+    E = rs.n_entries
+    udoc = out.union_docid.cpu().numpy()[:E].view(np.uint32)
+    perm = out.perm.cpu().numpy()[:, :E].view(np.uint16)
+    fused = out.fused.cpu().numpy()[:, :E]
+    res = {}
+    for m, name in enumerate(out.methods):
+        order = "sorted" if name in UNWEIGHTED else "first_seen"
+        res[name] = FusedRun(rs.qids, rs.docnos, rs.query_base(), counts, udoc, perm[m],
+                             fused[m], order)
+    return res
+
+
+def fuse_many(runs: Dict[str, pd.DataFrame], methods: Sequence[str], qpp_data=None,
+              qpp_index: Optional[int] = None, k: Optional[int] = None) -> Dict[str, FusedRun]:
+    """Several methods from one packed upload (one launch when the lists are canonical)."""
+    methods = [m.lower() for m in methods]
+    k = k if k is not None else config.fusion.rrf_k
+    qpp_index = qpp_index if qpp_index is not None else config.qpp.default_index
+    rs = _pack(runs)
+    weighted = [m for m in methods if m in WEIGHTED]
+    weights = _weights(rs, qpp_data, qpp_index) if weighted else None
+    if rs.canonical:
+        return _launch(rs, methods, k, weights)
+    # Lists whose file order is not score order: each family gets the order the
+    # reference iterates in (ranx: score-sorted; W-CombSUM/MNZ: file rows;
+    # W-RRF: rank-sorted, src/fusion.py:372).
+    res = {}
+    un = [m for m in methods if m in UNWEIGHTED]
+    if un:
+        res.update(_launch(reorder(rs, "score"), un, k, None))
+    ws = [m for m in methods if m in ("wcombsum", "wcombmnz")]
+    if ws:
+        res.update(_launch(rs, ws, k, weights))
+    if "wrrf" in methods:
+        res.update(_launch(reorder(rs, "rank"), ["wrrf"], k, weights))
+    return {m: res[m] for m in methods}
+
+
+# ------------------------------------------------------- public fusions ------
+
+def combsum(runs: Dict[str, pd.DataFrame]) -> FusedRun:
+    """CombSUM(d,q) = Σ_i S_i(d,q) over min-max normalised runs (ranx "sum")."""
+    return fuse_many(runs, ["combsum"])["combsum"]
+
+
+def combmnz(runs: Dict[str, pd.DataFrame]) -> FusedRun:
+    """CombMNZ(d,q) = |{i: d ∈ R_i}| · Σ_i S_i(d,q) (ranx "mnz")."""
+    return fuse_many(runs, ["combmnz"])["combmnz"]
+
+
+def rrf(runs: Dict[str, pd.DataFrame], k: int = None) -> FusedRun:
+    """RRF(d,q) = Σ_i 1/(k + rank_i(d,q)) (ranx "rrf"), k from config when None."""
+    return fuse_many(runs, ["rrf"], k=k)["rrf"]
+
+
+def weighted_combsum(runs, qpp_data, qpp_index: int = None) -> FusedRun:
+    """W-CombSUM(d,q) = Σ_i w_i(q) · S_i(d,q); qpp_index -1 = mean of the 13 columns."""
+    return fuse_many(runs, ["wcombsum"], qpp_data, qpp_index)["wcombsum"]
+
+
+def weighted_combmnz(runs, qpp_data, qpp_index: int = None) -> FusedRun:
+    """W-CombMNZ(d,q) = |{i}| · Σ_i w_i(q) · S_i(d,q)."""
+    return fuse_many(runs, ["wcombmnz"], qpp_data, qpp_index)["wcombmnz"]
+
+
+def weighted_rrf(runs, qpp_data, qpp_index: int = None, k: int = None) -> FusedRun:
+    """W-RRF(d,q) = Σ_i w_i(q) / (k + rank_i(d,q)) with the file's rank column."""
+    return fuse_many(runs, ["wrrf"], qpp_data, qpp_index, k)["wrrf"]
+
+
+def learned_fusion(runs, qpp_data, model_path: str, retrievers: Optional[List[str]] = None):
+    """Learned (LightGBM / MLP) weights — SURVEY §8(f) "next", not in this build."""
+    raise NotImplementedError(
+        "learned_fusion (LightGBM inference on the QPP features) is the next row of the build "
+        "plan (SURVEY.md §8(f) #1); it is not implemented on MI355X yet")
+
+
+# ------------------------------------------------------------------ output ---
+
+def write_runfile(fused: Mapping, output_path: str, tag: str = "fusion") -> None:
+    """TREC run file: qids by qid_sort_key, docs by score desc (stable), '%.6f' scores."""
+    with open(output_path, "w") as fout:
+        for qid in sorted(fused.keys(), key=qid_sort_key):
+            if isinstance(fused, FusedRun):
+                ids, scores = fused.arrays(qid)
+                docs = fused._docnos[ids].tolist()
+                scores = scores.tolist()
+                fout.write("".join(f"{qid} Q0 {d} {i} {s:.6f} {tag}\n"
+                                   for i, (d, s) in enumerate(zip(docs, scores), start=1)))
+            else:
+                ranked = sorted(fused[qid], key=lambda x: x[1], reverse=True)
+                fout.write("".join(f"{qid} Q0 {d} {i} {s:.6f} {tag}\n"
+                                   for i, (d, s) in enumerate(ranked, start=1)))
+    print(f"Wrote fused run to {output_path}")
+
+
+def run_fusion(method: str, runs_dir: str, qpp_dir: Optional[str] = None, qpp_model: str = None,
+               model_path: Optional[str] = None, output_path: Optional[str] = None,
+               rrf_k: int = None):
+    """Load, fuse with one method, optionally write — same dispatch and tags as the reference."""
+    qpp_model = qpp_model or config.qpp.default_method
+    rrf_k = rrf_k if rrf_k is not None else config.fusion.rrf_k
+    runs = load_runs(runs_dir, use_normalized=True)
+    print(f"Loaded {len(runs)} rankers: {list(runs.keys())}")
+    method = method.lower()
+    if method in ("combsum", "combmnz"):
+        fused, tag = fuse_many(runs, [method])[method], method
+    elif method == "rrf":
+        fused, tag = rrf(runs, k=rrf_k), f"rrf-k{rrf_k}"
+    elif method in ("wcombsum", "w-combsum", "wcombmnz", "w-combmnz", "wrrf", "w-rrf"):
+        if not qpp_dir:
+            raise ValueError("--qpp_dir required for weighted methods")
+        name = method.replace("-", "")
+        qpp_data = load_qpp_scores(qpp_dir)
+        qpp_index = get_qpp_index(qpp_model)
+        fused = fuse_many(runs, [name], qpp_data, qpp_index, rrf_k)[name]
+        tag = f"{name}-{qpp_model.lower()}"
+    elif method == "learned":
+        if not model_path:
+            raise ValueError("--model_path required for learned fusion")
+        if not qpp_dir:
+            raise ValueError("--qpp_dir required for learned fusion")
+        fused, tag = learned_fusion(runs, load_qpp_scores(qpp_dir), model_path), "learned"
+    else:
+        raise ValueError(f"Unknown method '{method}'. Valid: {config.fusion.methods}")
+    if output_path:
+        write_runfile(fused, output_path, tag)
+    return fused

@@ -1,0 +1,154 @@
+"""Drop-in replacement for the reference's src/qpp.py, computed on MI355X.
+
+The reference computes the 13 QPP predictors in a JVM subprocess
+(QPPBridge.java, fed JSON over stdin, src/qpp.py:117-171).  Here the same
+predictors are a HIP kernel (csrc/qf_qpp.hip, one wavefront per ranked list);
+the per-column min-max normalisation and the "%.6f" write-back are kernels too.
+Public surface kept: QPPResult, QPPBridge (compute_batch / compute),
+compute_qpp_for_res_file, _normalize_qpp — same arguments, return values,
+output files and exception types (RuntimeError when the engine is unavailable,
+FileNotFoundError / ValueError on bad inputs).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from collections import defaultdict
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from . import _lib, engine, textfeat
+from .config import config
+
+QPP_METHODS = list(config.qpp.methods)
+
+
+@dataclass
+class QPPResult:
+    query: str
+    retriever_name: str
+    qpp_scores: Dict[str, float]
+    methods_used: List[str]
+    processing_time_ms: float
+    predictions: Dict[str, Any]
+    error: Optional[str] = None
+
+
+def _device_qpp(lists: List[List[float]], texts: List[str], top_k: int = 0) -> np.ndarray:
+    """Raw predictors [L, 13] for L score lists (each used in the given order)."""
+    import torch
+    dev = engine.require_device()
+    lens = np.fromiter((len(s) for s in lists), dtype=np.int64, count=len(lists))
+    off = np.zeros(len(lists) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    flat = np.fromiter((float(x) for s in lists for x in s), dtype=np.float64, count=int(off[-1]))
+    nt, tf = textfeat.feature_arrays(texts)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    raw = engine.qpp_raw(t(flat) if flat.size else torch.zeros(1, dtype=torch.float64, device=dev),
+                         t(off), 1, top_k, t(nt), t(tf))
+    return raw.cpu().numpy()
+
+
+class QPPBridge:
+    """Same interface as the reference's Java bridge; the arithmetic runs on the GPU."""
+
+    def __init__(self, java_dir: Optional[str] = None, persistent: bool = True):
+        self.persistent = persistent
+        self.qpp_method_names = list(config.qpp.methods)
+        try:
+            engine.require_device()
+        except (RuntimeError, ImportError) as exc:  # the reference raises RuntimeError too
+            raise RuntimeError(f"QPP engine unavailable: {exc}") from exc
+        print("[QPP] MI355X QPP kernels ready", file=sys.stderr)
+
+    def compute_batch(self, queries_scores: List[tuple]) -> List[QPPResult]:
+        """[(query_text, scores)] -> one QPPResult per list, in input order."""
+        if not queries_scores:
+            return []
+        texts = [str(q) for q, _ in queries_scores]
+        lists = [list(s) for _, s in queries_scores]
+        raw = _device_qpp(lists, texts)
+        out = []
+        for text, scores, row in zip(texts, lists, raw):
+            vals = {} if len(scores) == 0 else dict(zip(QPP_METHODS, row.tolist()))
+            out.append(QPPResult(query=text, retriever_name="batch", qpp_scores=vals,
+                                 methods_used=self.qpp_method_names, processing_time_ms=0,
+                                 predictions={}))
+        return out
+
+    def compute(self, query: str, scores: List[float], retriever_name: str = "unknown",
+                methods: Optional[List[str]] = None) -> QPPResult:
+        t0 = time.time()
+        raw = _device_qpp([list(scores)], [query])[0]
+        vals = {} if len(scores) == 0 else dict(zip(QPP_METHODS, raw.tolist()))
+        return QPPResult(query=query, retriever_name=retriever_name, qpp_scores=vals,
+                         methods_used=list(vals.keys()),
+                         processing_time_ms=(time.time() - t0) * 1000, predictions={})
+
+
+def _read_scores(res_path: str):
+    """qid -> [scores] in file order, for lines with >= 5 fields (src/qpp.py:292-298)."""
+    runs = defaultdict(list)
+    with open(res_path, "r") as fh:
+        for line in fh:
+            f = line.strip().split()
+            if len(f) >= 5:
+                runs[f[0]].append(float(f[4]))
+    return runs
+
+
+def compute_qpp_for_res_file(res_path: str, output_path: Optional[str] = None,
+                             top_k: int = None, normalize: str = None,
+                             queries_path: Optional[str] = None) -> Dict[str, List[float]]:
+    """QPP of every query in a raw TREC .res file; writes <out>.qpp if asked."""
+    top_k = top_k or config.processing.retrieval.top_k
+    normalize = normalize or config.qpp.normalization
+    if not os.path.exists(res_path):
+        raise FileNotFoundError(f"Run file not found: {res_path}")
+    texts = {}
+    if queries_path and os.path.exists(queries_path):
+        with open(queries_path, "r") as fh:
+            for line in fh:
+                q = json.loads(line)
+                texts[q["_id"]] = q["text"]
+    runs = _read_scores(res_path)
+    if not runs:
+        raise ValueError(f"No valid entries in run file: {res_path}")
+    qids = list(runs.keys())
+    # sorted(scores, reverse=True)[:top_k] per query (src/qpp.py:304-305)
+    lists = [sorted(runs[q], reverse=True)[:top_k] for q in qids]
+    QPPBridge()
+    raw = _device_qpp(lists, [texts.get(q, q) for q in qids])
+    results = {q: raw[i].tolist() for i, q in enumerate(qids)}
+    if normalize != "none" and results:
+        results = _normalize_qpp(results, normalize)
+    if output_path:
+        with open(output_path, "w") as fh:
+            for qid in sorted(results.keys(), key=lambda x: int(x) if x.isdigit() else x):
+                fh.write(f"{qid}\t" + "\t".join(f"{s:.6f}" for s in results[qid]) + "\n")
+        print(f"Wrote QPP scores to {output_path}")
+    return results
+
+
+def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, List[float]]:
+    """Per-column normalisation across queries (src/qpp.py:340-374), on device for minmax."""
+    qids = list(results.keys())
+    arr = np.asarray([results[q] for q in qids], dtype=np.float64).reshape(len(qids), -1)
+    if method == "minmax" and arr.shape[1] == _lib.QPP_COLS:
+        import torch
+        dev = engine.require_device()
+        raw = torch.from_numpy(arr).to(dev)
+        off = torch.arange(len(qids) + 1, dtype=torch.int64, device=dev)  # every list present
+        mm = engine.qpp_colminmax(raw, off, 1)
+        norm = engine.qpp_normalize(raw, mm, off, 1, "minmax", qpp_index=0, want_norm=True,
+                                    want_micro=False, want_weights=False)["norm"]
+        vals = norm.cpu().numpy()
+    else:
+        raise NotImplementedError(
+            f"QPP normalisation '{method}' is not implemented on device (minmax, the default "
+            "of config/defaults.yaml:200, is)")
+    return {q: [float(v) for v in vals[i]] for i, q in enumerate(qids)}

@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Run in the build container only (the GPU box has no /root/reference):
+    python tests/golden/make_golden.py
+It imports the reference's own src/fusion.py, src/qpp.py, src/data_utils.py,
+src/config.py and src/retrievers/base.py by file path — with a bare `src`
+package (src/__init__.py:33 pulls ir_measures, not installed) and a stub `ranx`
+module (not installed; only its three names are bound at import) — runs them on
+small synthetic inputs, and writes inputs + outputs as JSON / text.  Nothing of
+the reference's source is copied: the fixtures are data.  Floats are stored
+with float.hex() so the comparison can be bit-exact.
+
+What is pinned here (see DESIGN.md "Parity"):
+  weighted_combsum / weighted_combmnz / weighted_rrf (incl. ties, missing
+  rankers, qpp_index=-1, unsorted rows), write_runfile bytes, get_qpp_index,
+  get_qpp_weight errors, _normalize_qpp, normalize_scores, load_qpp_scores,
+  load_runs, and the committed .qpp text columns 7-8 with their query texts.
+"""
+from __future__ import annotations
+
+import importlib.util
+import io
+import json
+import os
+import random
+import shutil
+import sys
+import tempfile
+import types
+from contextlib import redirect_stdout
+from pathlib import Path
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+
+
+def load_reference():
+    tmp = tempfile.mkdtemp(prefix="qppfuse_ref_")
+    os.environ["PROJECT_ROOT"] = tmp  # src/config.py:202-203 mkdirs cache_root
+    src = types.ModuleType("src")
+    src.__path__ = [str(REF / "src")]
+    sys.modules["src"] = src
+    ranx = types.ModuleType("ranx")
+    ranx.Run = ranx.fuse = ranx.Qrels = None
+    sys.modules["ranx"] = ranx
+
+    def load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+        return mod
+
+    mods = {}
+    mods["config"] = load("src.config", REF / "src/config.py")
+    mods["data_utils"] = load("src.data_utils", REF / "src/data_utils.py")
+    mods["fusion"] = load("src.fusion", REF / "src/fusion.py")
+    mods["qpp"] = load("src.qpp", REF / "src/qpp.py")
+    mods["base"] = load("src.retrievers.base", REF / "src/retrievers/base.py")
+    return mods
+
+
+def hx(x: float) -> str:
+    return float(x).hex()
+
+
+def make_case(rng, n_q, rankers, k_range, pool, p_skip=0.0, ties=False, unsorted=False,
+              neg=False, rank_shift=False, normed=False):
+    """Synthetic .norm.res-like runs: {ranker: rows}; rows = [qid, docno, rank, score]."""
+    runs = {}
+    qids = [f"test{i}" for i in rng.sample(range(1000), n_q)]
+    for r in rankers:
+        rows = []
+        for qid in qids:
+            if rng.random() < p_skip:
+                continue
+            k = rng.randint(*k_range)
+            docs = rng.sample(pool, k)
+            if ties:
+                vals = sorted((rng.randint(0, 4) / 4 for _ in range(k)), reverse=True)
+            else:
+                vals = sorted((rng.randint(0, 10**6) / 1e6 for _ in range(k)), reverse=True)
+                vals = [float(f"{v:.6f}") for v in vals]
+            if neg:
+                vals = [v - 0.5 for v in vals]
+            if normed and len(vals) > 1 and vals[0] > vals[-1]:
+                # a .norm.res list: per-query min-max, written "%.6f"
+                lo, hi = vals[-1], vals[0]
+                vals = [float(f"{(v - lo) / (hi - lo):.6f}") for v in vals]
+            items = [[qid, d, i + 1 + (3 if rank_shift else 0), v]
+                     for i, (d, v) in enumerate(zip(docs, vals))]
+            if unsorted:
+                rng.shuffle(items)
+            rows.extend(items)
+        runs[r] = rows
+    return qids, runs
+
+
+def to_frames(runs):
+    import pandas as pd
+    out = {}
+    for r, rows in runs.items():
+        df = pd.DataFrame(rows, columns=["qid", "docno", "rank", "score"])
+        df.insert(1, "iter", "Q0")
+        df["runid"] = r
+        df["qid"] = df["qid"].astype(str)
+        out[r] = df
+    return out
+
+
+def make_qpp(rng, qids, rankers, const=None, missing=None):
+    data = {}
+    for q in qids:
+        data[q] = {}
+        for r in rankers:
+            if missing and (q, r) == missing:
+                continue
+            if const is not None:
+                data[q][r] = [const] * 13
+            else:
+                data[q][r] = [float(f"{rng.random():.6f}") for _ in range(13)]
+    return data
+
+
+def enc_fused(fused):
+    return {q: [[d, hx(s)] for d, s in lst] for q, lst in fused.items()}
+
+
+def main():
+    mods = load_reference()
+    fu, qp, du, base = mods["fusion"], mods["qpp"], mods["data_utils"], mods["base"]
+    rng = random.Random(20251212)
+    pool = [f"doc{i}" for i in range(60)]
+    rankers = ["BGE", "BM25", "Splade"]
+
+    cases = []
+    specs = [
+        ("basic", dict(n_q=6, rankers=rankers, k_range=(5, 12), pool=pool), dict(), 5),
+        ("fusion_mode", dict(n_q=5, rankers=rankers, k_range=(4, 10), pool=pool), dict(), -1),
+        ("ties", dict(n_q=5, rankers=rankers, k_range=(6, 14), pool=pool[:20], ties=True),
+         dict(), 3),
+        ("missing_rows", dict(n_q=7, rankers=rankers, k_range=(3, 9), pool=pool, p_skip=0.3),
+         dict(), 5),
+        ("unsorted_rankshift", dict(n_q=4, rankers=rankers, k_range=(5, 9), pool=pool,
+                                    unsorted=True, rank_shift=True), dict(), 5),
+        ("negative_zero_weight", dict(n_q=4, rankers=rankers, k_range=(5, 9), pool=pool,
+                                      neg=True), dict(const=0.0), 5),
+        ("unit_weights", dict(n_q=6, rankers=rankers + ["BM25_TCT", "BM25_MonoT5"],
+                              k_range=(8, 20), pool=pool, normed=True), dict(const=1.0), 5),
+        ("five_rankers", dict(n_q=8, rankers=["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade"],
+                              k_range=(15, 40), pool=[f"d{i}" for i in range(120)], normed=True),
+         dict(), 5),
+    ]
+    for name, cspec, qspec, qidx in specs:
+        qids, runs = make_case(rng, **cspec)
+        qpp = make_qpp(rng, qids, cspec["rankers"], **qspec)
+        frames = to_frames(runs)
+        case = {"name": name, "rankers": cspec["rankers"], "runs": runs, "qpp": qpp,
+                "qpp_index": qidx, "rrf_k": 60, "outputs": {}, "runfiles": {}}
+        with redirect_stdout(io.StringIO()):
+            outs = {
+                "wcombsum": fu.weighted_combsum(frames, qpp, qidx),
+                "wcombmnz": fu.weighted_combmnz(frames, qpp, qidx),
+                "wrrf": fu.weighted_rrf(frames, qpp, qidx, k=60),
+            }
+            for m, fused in outs.items():
+                case["outputs"][m] = enc_fused(fused)
+                with tempfile.NamedTemporaryFile("r", suffix=".res", delete=False) as tf:
+                    path = tf.name
+                fu.write_runfile(fused, path, f"{m}-tag")
+                case["runfiles"][m] = Path(path).read_text()
+                os.unlink(path)
+        cases.append(case)
+
+    # errors of get_qpp_weight (missing qid / ranker even without rows, bad index)
+    qids, runs = make_case(rng, n_q=3, rankers=rankers, k_range=(3, 5), pool=pool)
+    frames = to_frames(runs)
+    errors = []
+    for label, qpp, qidx in [
+        ("missing_ranker", make_qpp(rng, qids, rankers, missing=(sorted(qids)[1], "BM25")), 5),
+        ("missing_qid", {q: v for q, v in make_qpp(rng, qids, rankers).items()
+                         if q != sorted(qids)[2]}, 5),
+        ("bad_index", make_qpp(rng, qids, rankers), 13),
+    ]:
+        try:
+            with redirect_stdout(io.StringIO()):
+                fu.weighted_combsum(frames, qpp, qidx)
+            err = None
+        except Exception as exc:  # noqa: BLE001
+            err = [type(exc).__name__, str(exc)]
+        errors.append({"label": label, "runs": runs, "qpp": qpp, "qpp_index": qidx,
+                       "error": err})
+
+    # qid sort key of write_runfile with mixed qids
+    mixed = {}
+    try:
+        with redirect_stdout(io.StringIO()):
+            fu.write_runfile({"test3": [("a", 1.0)], "5ae7": [("b", 1.0)]}, os.devnull, "t")
+        mixed["error"] = None
+    except Exception as exc:  # noqa: BLE001
+        mixed["error"] = [type(exc).__name__, str(exc)]
+
+    # get_qpp_index
+    names = ["RSD", "rsd", "NQC", "nqc", "Sigma(%)", "sigma_max", "QPP-PRP", "WIG", "SCNQC",
+             "QV-NQC", "DM", "NQA-QPP", "BERTQPP", "SMV", "UEF", "fusion", "FUSION", "bogus"]
+    idx = {}
+    for n in names:
+        try:
+            idx[n] = fu.get_qpp_index(n)
+        except Exception as exc:  # noqa: BLE001
+            idx[n] = [type(exc).__name__]
+
+    # _normalize_qpp (minmax) on raw predictor rows, incl. a constant column
+    raw = {}
+    for i in range(25):
+        row = [rng.uniform(-3, 5) for _ in range(13)]
+        row[12] = 0.25  # constant column -> scale 1.0 -> zeros
+        raw[str(i) if i % 2 else f"q{i}"] = row
+    norm = qp._normalize_qpp(raw, "minmax")
+    normq = {"raw": {q: [hx(v) for v in r] for q, r in raw.items()},
+             "norm": {q: [hx(float(v)) for v in r] for q, r in norm.items()}}
+
+    # normalize_scores
+    lists = [[(f"d{i}", rng.uniform(-20, 40), i + 1) for i in range(n)] for n in (1, 2, 7, 30)]
+    lists.append([("a", 3.5, 1), ("b", 3.5, 2), ("c", 3.5, 3)])
+    lists.append([])
+    ns = [{"in": [[d, hx(s), r] for d, s, r in L],
+           "out": [[d, hx(s), r] for d, s, r in base.BaseRetriever.normalize_scores(L)]}
+          for L in lists]
+
+    # loaders on files written here
+    tmp = Path(tempfile.mkdtemp(prefix="qppfuse_files_"))
+    (tmp / "runs").mkdir()
+    (tmp / "qpp").mkdir()
+    for r, rows in cases[0]["runs"].items():
+        with open(tmp / "runs" / f"{r}.norm.res", "w") as fh:
+            for qid, d, rk, s in rows:
+                fh.write(f"{qid} Q0 {d} {rk} {s:.6f} {r}\n")
+        with open(tmp / "qpp" / f"{r}.res.mmnorm.qpp", "w") as fh:
+            for qid, vals in cases[0]["qpp"].items():
+                fh.write(qid + "\t" + "\t".join(f"{v:.6f}" for v in vals[r]) + "\n")
+    files = {"runs": {f"{r}.norm.res": (tmp / "runs" / f"{r}.norm.res").read_text()
+                      for r in cases[0]["runs"]},
+             "qpp": {f"{r}.res.mmnorm.qpp": (tmp / "qpp" / f"{r}.res.mmnorm.qpp").read_text()
+                     for r in cases[0]["runs"]}}
+    loaded_qpp = du.load_qpp_scores(tmp / "qpp")
+    loaded_runs = fu.load_runs(str(tmp / "runs"))
+    files["load_qpp_scores"] = {q: {r: [hx(v) for v in vals] for r, vals in d.items()}
+                                for q, d in loaded_qpp.items()}
+    files["load_runs"] = {r: {"qid": df["qid"].tolist(), "docno": df["docno"].tolist(),
+                              "rank": [int(x) for x in df["rank"]],
+                              "score": [hx(x) for x in df["score"]]}
+                          for r, df in loaded_runs.items()}
+    with redirect_stdout(io.StringIO()):
+        fused = fu.run_fusion("wcombsum", str(tmp / "runs"), str(tmp / "qpp"), "RSD", None,
+                              str(tmp / "wcs.res"), 60)
+    files["run_fusion_wcombsum_rsd"] = (tmp / "wcs.res").read_text()
+    shutil.rmtree(tmp)
+
+    golden = {"cases": cases, "errors": errors, "mixed_qids": mixed, "qpp_index": idx,
+              "normalize_qpp": normq, "normalize_scores": ns, "files": files}
+    (OUT / "reference_fusion.json").write_text(json.dumps(golden, indent=1, sort_keys=True))
+
+    # committed .qpp text columns 7-8 (MaxIDF / avgidf proxies) + their query texts
+    for ds, qdir in [("scifact", "BEIR-scifact"), ("nq", "BEIR-nq")]:
+        texts = {}
+        with open(REF / "data" / ds / qdir / "queries.jsonl") as fh:
+            for line in fh:
+                q = json.loads(line)
+                texts[q["_id"]] = q["text"]
+        cols = {}
+        for line in open(REF / "data" / ds / "qpp" / "BGE.res.mmnorm.qpp"):
+            f = line.rstrip("\n").split("\t")
+            cols[f[0]] = [f[8], f[9], f[12], f[13]]  # cols 7, 8, 11, 12 as written
+        fixture = {"qids": list(cols.keys()), "text": [texts.get(q, q) for q in cols],
+                   "col7": [cols[q][0] for q in cols], "col8": [cols[q][1] for q in cols],
+                   "col11": [cols[q][2] for q in cols], "col12": [cols[q][3] for q in cols]}
+        (OUT / f"qpp_textcols_{ds}.json").write_text(json.dumps(fixture))
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

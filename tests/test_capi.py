@@ -1,0 +1,71 @@
+"""The C-ABI library loads and exports every symbol include/qppfuse.h declares (CPU)."""
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "qppfuse.h"
+
+
+def header_functions():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(qf_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ["qf_fuse", "qf_minmax_per_query", "qf_qpp_raw", "qf_qpp_colminmax",
+                 "qf_qpp_normalize", "qf_last_error", "qf_version", "qf_max_entries_per_query",
+                 "qf_synth_runs"]:
+        assert name in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from qppfuse import _lib
+    lib = _lib.lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(header_functions())
+
+
+def test_version_and_limits():
+    from qppfuse import _lib
+    assert "gfx950" in _lib.version()
+    assert _lib.max_entries_per_query() >= 5000  # 5 retrievers x top-1000 in one workgroup
+
+
+def test_argument_validation_without_device():
+    """Validation happens before any HIP call: bad arguments fail with EINVAL."""
+    from qppfuse import _lib
+    with pytest.raises(ValueError, match="n_retrievers"):
+        _lib.call("qf_fuse", 1, 0, None, None, None, 0, None, None, 1, 60, 10, None, None,
+                  None, None, 0, None)
+    with pytest.raises(ValueError, match="method mask"):
+        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, 0x40, 60, 10, None, None,
+                  None, None, 0, None)
+    with pytest.raises(ValueError, match="without weights"):
+        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, _lib.WRRF, 60, 10, None,
+                  None, None, None, 0, None)
+    with pytest.raises(_lib.QPPFuseError, match="exceed"):
+        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, _lib.RRF, 60, 10**6, None,
+                  None, None, None, 0, None)
+    with pytest.raises(ValueError, match="qpp_index"):
+        _lib.call("qf_qpp_normalize", 1, 1, 1, 1, 1, 1, 13, None, None, None, None)
+
+
+def test_product_has_no_cpu_fallback(monkeypatch):
+    """Without a device the product raises instead of computing on the CPU."""
+    import torch
+    from qppfuse import engine
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        engine.require_device()
+
+
+def test_product_never_imports_oracle():
+    pkg = ROOT / "qpp-fusion-rag_amd"
+    for f in pkg.rglob("*.py"):
+        assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", f.read_text(), re.M), f

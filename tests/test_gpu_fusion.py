@@ -1,0 +1,189 @@
+"""Parity of the HIP fusion kernel (qf_fuse) with the oracle — needs an MI355X.
+
+Bit-exact is the bar: fused scores are compared as IEEE doubles, orders and
+document ids exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import _loader as coracle
+from oracle import ref_port
+from tests.helpers import decode_fused, frames_from_rows, sorted_lists, first_seen_lists
+
+pytestmark = pytest.mark.gpu
+
+ALL = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+
+
+def _api():
+    from qppfuse import fusion
+    return fusion
+
+
+@pytest.mark.parametrize("method", ["wcombsum", "wcombmnz", "wrrf"])
+def test_weighted_api_matches_reference_golden(gpu, golden, method):
+    fusion = _api()
+    for case in golden["cases"]:
+        frames = frames_from_rows(case["runs"], case["rankers"])
+        fn = {"wcombsum": fusion.weighted_combsum, "wcombmnz": fusion.weighted_combmnz}.get(method)
+        if fn is None:
+            got = fusion.weighted_rrf(frames, case["qpp"], case["qpp_index"], k=case["rrf_k"])
+        else:
+            got = fn(frames, case["qpp"], case["qpp_index"])
+        want = decode_fused(case["outputs"][method])
+        assert sorted(got.keys()) == sorted(want.keys())
+        for q in want:
+            assert got[q] == want[q], (case["name"], method, q)
+
+
+@pytest.mark.parametrize("method", ["combsum", "combmnz", "rrf"])
+def test_unweighted_api_matches_port(gpu, golden, method):
+    fusion = _api()
+    for case in golden["cases"]:
+        frames = frames_from_rows(case["runs"], case["rankers"])
+        if case["name"] in ("unsorted_rankshift",):
+            continue
+        got = getattr(fusion, method)(frames)
+        want = ref_port.ranx_fusion(frames, method, 60)
+        for q in want:
+            assert got[q] == want[q], (case["name"], method, q)
+
+
+def test_write_runfile_bytes_match_reference(gpu, golden, tmp_path):
+    fusion = _api()
+    for case in golden["cases"]:
+        frames = frames_from_rows(case["runs"], case["rankers"])
+        res = fusion.fuse_many(frames, ["wcombsum", "wcombmnz", "wrrf"], case["qpp"],
+                               case["qpp_index"], case["rrf_k"])
+        for m, fused in res.items():
+            p = tmp_path / f"{case['name']}_{m}.res"
+            fusion.write_runfile(fused, str(p), f"{m}-tag")
+            assert p.read_text() == case["runfiles"][m], (case["name"], m)
+
+
+def _synthetic(Q, R, K, seed=11, p_shared=0.7):
+    from qppfuse import engine
+    off, docid, raw = engine.synth_runs(0, Q, R, K, seed=seed, p_shared=p_shared)
+    norm, micro = engine.minmax_per_query(raw, off)
+    return off, docid, raw, norm, micro
+
+
+@pytest.mark.parametrize("shape", [(64, 3, 100), (200, 5, 1000), (40, 7, 1000), (300, 2, 37)])
+def test_fuse_all_methods_bit_exact_vs_c_oracle(gpu, shape):
+    from qppfuse import engine
+    Q, R, K = shape
+    off, docid, raw, norm, micro = _synthetic(Q, R, K)
+    rng = np.random.default_rng(Q + R + K)
+    w = torch.from_numpy(rng.random(Q * R).round(6)).to(gpu)
+    out = engine.fuse(off, docid, micro, R, ALL, rrf_k=60, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    w_h = w.cpu().numpy()
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    uc = out.union_count.cpu().numpy()
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fused = out.fused.cpu().numpy()
+    assert (uc > 0).all()
+    for m, name in enumerate(ALL):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60, weights=w_h)
+        np.testing.assert_array_equal(uc, o_uc)
+        for q in range(Q):
+            b, n = off_h[q * R], uc[q]
+            np.testing.assert_array_equal(ud[b:b + n], o_ud[b:b + n])
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=f"{name} q{q}")
+            assert fused[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
+def test_fuse_f64_scores_bit_exact(gpu):
+    from qppfuse import engine
+    Q, R, K = 50, 4, 250
+    off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=5)
+    out = engine.fuse(off, docid, raw, R, ["combsum", "rrf", "combmnz"], max_entries=R * K)
+    off_h, doc_h, raw_h = off.cpu().numpy(), docid.cpu().numpy().view(np.uint32), raw.cpu().numpy()
+    uc = out.union_count.cpu().numpy()
+    for m, name in enumerate(["combsum", "combmnz", "rrf"]):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, raw_h, R, name)
+        f = out.fused.cpu().numpy()[m]
+        p = out.perm.cpu().numpy().view(np.uint16)[m]
+        for q in range(Q):
+            b, n = off_h[q * R], uc[q]
+            assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+            np.testing.assert_array_equal(p[b:b + n], o_perm[b:b + n])
+
+
+def _csr(lists, device):
+    off = np.cumsum([0] + [len(l[0]) for l in lists]).astype(np.int64)
+    doc = np.concatenate([np.asarray(l[0], np.uint32) for l in lists] or [np.zeros(0, np.uint32)])
+    sc = np.concatenate([np.asarray(l[1], np.float64) for l in lists] or [np.zeros(0)])
+    t = lambda a: torch.from_numpy(a).to(device)
+    return off, doc, sc, t(off), t(doc.view(np.int32)), t(sc)
+
+
+def test_edge_cases_empty_lists_ties_single(gpu):
+    from qppfuse import engine
+    R = 3
+    lists = [  # q0: one retriever empty, ties everywhere
+        ([1, 2, 3], [0.5, 0.5, 0.5]), ([], []), ([3, 2, 9], [1.0, 0.25, 0.25]),
+        # q1: single entry
+        ([7], [0.0]), ([], []), ([], []),
+        # q2: identical lists in all retrievers
+        ([4, 5, 6], [1.0, 0.5, 0.0]), ([4, 5, 6], [1.0, 0.5, 0.0]), ([4, 5, 6], [1.0, 0.5, 0.0]),
+    ]
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    w = torch.tensor([0.3, 0.5, 0.2] * 3, dtype=torch.float64, device=gpu)
+    out = engine.fuse(doff, ddoc, dsc, R, ALL, weights=w, max_entries=9)
+    uc = out.union_count.cpu().numpy()
+    for m, name in enumerate(ALL):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, weights=w.cpu().numpy())
+        np.testing.assert_array_equal(uc, o_uc)
+        np.testing.assert_array_equal(out.perm.cpu().numpy().view(np.uint16)[m][:off[-1]][
+            np.concatenate([np.arange(off[q * R], off[q * R] + uc[q]) for q in range(3)])],
+            o_perm[np.concatenate([np.arange(off[q * R], off[q * R] + uc[q]) for q in range(3)])])
+        f = out.fused.cpu().numpy()[m]
+        for q in range(3):
+            b, n = off[q * R], uc[q]
+            assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
+@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680])
+def test_kernel_capacity_boundaries(gpu, n_entries):
+    """Queries exactly at / just past each kernel configuration's capacity."""
+    from qppfuse import engine
+    R = 2
+    rng = np.random.default_rng(n_entries)
+    a = n_entries // 2
+    docs = rng.choice(50_000, size=n_entries, replace=False).astype(np.uint32)
+    docs[a:a + a // 3] = docs[: a // 3]  # overlap between the two lists
+    s1 = np.sort(rng.integers(0, 10**6, a))[::-1] / 1e6
+    s2 = np.sort(rng.integers(0, 10**6, n_entries - a))[::-1] / 1e6
+    lists = [(docs[:a], s1), (docs[a:], s2)]
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    out = engine.fuse(doff, ddoc, dsc, R, ["combsum", "rrf"], max_entries=n_entries)
+    uc = out.union_count.cpu().numpy()
+    for m, name in enumerate(["combsum", "rrf"]):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name)
+        assert uc[0] == o_uc[0]
+        n = uc[0]
+        assert out.fused.cpu().numpy()[m][:n].tobytes() == o_fused[:n].tobytes()
+        np.testing.assert_array_equal(out.perm.cpu().numpy().view(np.uint16)[m][:n], o_perm[:n])
+
+
+def test_too_big_and_unsorted_are_reported(gpu):
+    from qppfuse import engine, _lib
+    R = 1
+    off, doc, sc, doff, ddoc, dsc = _csr([([1, 2, 3], [0.1, 0.9, 0.5])], gpu)
+    out = engine.fuse(doff, ddoc, dsc, R, ["rrf"], max_entries=3)
+    assert out.union_count.cpu().numpy()[0] == -2
+    out = engine.fuse(doff, ddoc, dsc, R, ["wcombsum"], max_entries=3,
+                      weights=torch.ones(1, dtype=torch.float64, device=gpu))
+    assert out.union_count.cpu().numpy()[0] == 3  # weighted methods need no order
+    with pytest.raises(_lib.QPPFuseError):
+        engine.fuse(doff, ddoc, dsc, R, ["rrf"], max_entries=_lib.max_entries_per_query() + 1)
+    with pytest.raises(ValueError):
+        engine.fuse(doff, ddoc, dsc, R, ["wrrf"], max_entries=3)  # no weights
+    off, doc, sc, doff, ddoc, dsc = _csr([([1, 2, 1], [0.9, 0.5, 0.1]), ([4], [1.0])], gpu)
+    out = engine.fuse(doff, ddoc, dsc, 2, ["combsum"], max_entries=4)
+    assert out.union_count.cpu().numpy()[0] == -5  # duplicate docid inside one list

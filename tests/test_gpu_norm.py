@@ -1,0 +1,72 @@
+"""Per-query min-max normalisation kernel vs the oracle — needs an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import _loader as coracle
+from tests.helpers import unhex
+
+pytestmark = pytest.mark.gpu
+
+
+def test_minmax_bit_exact_and_micro_is_python_format(gpu):
+    from qppfuse import engine
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 1500, 400)
+    lens[:3] = [1, 2, 0]
+    lists = [np.sort(rng.normal(0, 10, n))[::-1] for n in lens]
+    lists[10] = np.full(17, 4.25)  # constant list -> all zeros
+    off = np.cumsum([0] + [len(l) for l in lists]).astype(np.int64)
+    flat = np.concatenate(lists)
+    norm, micro = engine.minmax_per_query(torch.from_numpy(flat).to(gpu),
+                                          torch.from_numpy(off).to(gpu))
+    norm, micro = norm.cpu().numpy(), micro.cpu().numpy()
+    want = coracle.minmax_per_query(flat, off)
+    assert norm.tobytes() == want.tobytes()
+    fmt = [f"{v:.6f}" for v in want]
+    got = [f"{m // 10**6}.{m % 10**6:06d}" for m in micro]
+    assert got == fmt
+
+
+def test_round6_half_even_and_hard_cases(gpu):
+    """Values next to 6th-decimal ties: the exact binary value decides (CPython)."""
+    from qppfuse import engine
+    base = np.array([0.0000005, 0.0000015, 0.0000025, 0.1234565, 0.9999995, 0.5, 1.0,
+                     0.3333335, 0.0000004999999, 0.7654325])
+    vals = np.concatenate([base, np.nextafter(base, 2), np.nextafter(base, -1)])
+    vals = np.clip(vals, 0, 1)
+    rng = np.random.default_rng(5)
+    vals = np.concatenate([vals, rng.random(100_000),
+                           np.round(rng.random(20_000), 7)])
+    # one list [1, vals..., 0] so min-max is the identity
+    flat = np.concatenate([[1.0], np.sort(vals)[::-1], [0.0]])
+    off = np.array([0, len(flat)], np.int64)
+    _, micro = engine.minmax_per_query(torch.from_numpy(flat).to(gpu),
+                                       torch.from_numpy(off).to(gpu))
+    micro = micro.cpu().numpy()
+    got = [f"{m // 10**6}.{m % 10**6:06d}" for m in micro]
+    assert got == [f"{v:.6f}" for v in flat]
+
+
+def test_normalize_scores_matches_reference_golden(gpu, golden):
+    from qppfuse.retrieval import normalize_scores
+    for case in golden["normalize_scores"]:
+        src = [(d, unhex(s), r) for d, s, r in case["in"]]
+        want = [(d, unhex(s), r) for d, s, r in case["out"]]
+        assert normalize_scores(src) == want
+
+
+def test_write_run_normalized_text(gpu, tmp_path):
+    from qppfuse.retrieval import write_run
+    rng = np.random.default_rng(2)
+    results = {f"test{i}": [(f"d{j}", float(s), j + 1) for j, s in
+                            enumerate(sorted(rng.gamma(2, 6, 20), reverse=True))]
+               for i in range(12)}
+    p = tmp_path / "X.norm.res"
+    write_run(results, str(p), "X", normalize=True)
+    from oracle import ref_port
+    want = []
+    for qid in sorted(results, key=ref_port.qid_sort_key):
+        for d, s, r in ref_port.normalize_scores(results[qid]):
+            want.append(f"{qid} Q0 {d} {r} {s:.6f} X\n")
+    assert p.read_text() == "".join(want)
