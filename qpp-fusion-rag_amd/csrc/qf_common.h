@@ -34,6 +34,24 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// Same, with DPP (no LDS round trips), the GFX9 wave64 sequence: each lane adds
+// the 3 lanes before it (row_shr:1,2,3 of the ORIGINAL value), then row_shr:4
+// (bank_mask 0xe) and row_shr:8 (bank_mask 0xc) finish 16-lane rows, then
+// row_bcast:15 (row_mask 0xa) and row_bcast:31 (row_mask 0xc) carry across rows.
+// Out-of-row sources and masked lanes contribute `old` = 0.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+  const int x0 = (int)v;
+  int x = x0;
+  x += __builtin_amdgcn_update_dpp(0, x0, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x0, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x0, 0x113, 0xf, 0xf, false);  // row_shr:3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xe, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xc, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return (uint32_t)x;
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));

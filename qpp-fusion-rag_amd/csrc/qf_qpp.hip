@@ -18,15 +18,28 @@ namespace qf {
 
 constexpr int kQppBlock = 256;  // 4 lists per workgroup
 
+// v of lane l (l wave-uniform) as a scalar: two v_readlane_b32.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Java's left-to-right sum of t[0..k) (t held one per lane): a serial chain of
+// scalar-broadcast adds, exactly the reference's order.
+__device__ __forceinline__ double ordered_sum(double t, int k) {
+  double acc = 0.0;
+  for (int j = 0; j < k; ++j) acc += readlane_f64(t, j);
+  return acc;
+}
+
 __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     int32_t R, int32_t top_k, const int32_t* __restrict__ num_terms,
     const double* __restrict__ text_feat, double* __restrict__ out) {
-  __shared__ double xs_all[kQppBlock];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t l = (int64_t)blockIdx.x * (kQppBlock / 64) + wid;
   if (l >= n_lists) return;  // wave-uniform; no block barrier below
-  double* xs = xs_all + wid * 64;
   const int64_t a = list_off[l], b = list_off[l + 1];
   int64_t n64 = b - a;
   if (top_k > 0 && n64 > top_k) n64 = top_k;  // sorted(...)[:top_k], src/qpp.py:305
@@ -38,101 +51,97 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     return;
   }
   const int64_t q = l / R;
+  const bool act = lane < k;
   // float32 rounding of the JSON value (Gson getAsFloat), then widened.
-  const double x = lane < k ? (double)(float)score[a + lane] : 0.0;
-  xs[lane] = x;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const double x = act ? (double)(float)score[a + lane] : 0.0;
   const int nt_raw = num_terms[q];
   const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
 
-  // prefix Kahan means: lane i -> mean of rsv[0..i]
+  // prefix Kahan means (DoubleStream.average): lane i -> mean of rsv[0..i]
   Kahan kp;
   kahan_init(kp);
   for (int j = 0; j < k; ++j) {
-    const double xj = xs[j];
+    const double xj = readlane_f64(x, j);
     if (j <= lane) kahan_add(kp, xj);
   }
   const double mean_i = kahan_final(kp) / (double)(lane + 1);
-  const double mu = __shfl(mean_i, k - 1, 64);  // Arrays.stream(rsvs).average()
+  const double mu = readlane_f64(mean_i, k - 1);  // Arrays.stream(rsvs).average()
 
-  // prefix sums of squared deviations around each prefix mean:
-  //   simple sum -> NQC of prefix (CumNQC, NQC), Kahan average -> SigmaMax
+  // squared deviations around each prefix mean: simple sum -> NQC of the prefix
+  // (NQC, CumNQC), compensated average -> population variance (SigmaMax, RSD)
   Kahan kv;
   kahan_init(kv);
   double sq = 0.0;
   for (int j = 0; j < k; ++j) {
-    const double xj = xs[j];
+    const double del = readlane_f64(x, j) - mean_i;
+    const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
     if (j <= lane) {
-      const double del = xj - mean_i;
-      const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
       sq += d2;
       kahan_add(kv, d2);
     }
   }
-  const double nqc_i = sq / (double)(lane + 1);                    // computeNQC(prefix)
-  const double sigma_i = sqrt(kahan_final(kv) / (double)(lane + 1));  // SigmaMax window std
-  const double var_full = __shfl(kahan_final(kv) / (double)(lane + 1), k - 1, 64);
-
-  // ---- col 0: NQC (QPPBridge.java:202-216)
-  const double nqc = __shfl(nqc_i, k - 1, 64);
-  // ---- col 3: SigmaMax (QPPBridge.java:269-293)
-  double sm = (lane >= 1 && lane < k) ? sigma_i : 0.0;
+  const double nqc_i = sq / (double)(lane + 1);
+  const double var_i = kahan_final(kv) / (double)(lane + 1);
+  const double sigma_i = sqrt(var_i);
+  const double nqc = readlane_f64(nqc_i, k - 1);          // col 0: NQC (:202-216)
+  const double var_full = readlane_f64(var_i, k - 1);
+  double sm = (lane >= 1 && act) ? sigma_i : 0.0;          // col 3: SigmaMax (:269-293)
   sm = wave_max(sm);
   const double sigmamax = k < 2 ? 0.0 : sm / sqrt((double)numTerms);
-  // ---- col 9: CumNQC (QPPBridge.java:400-410): sequential over k = 2..n
-  double cum = 0.0;
-  for (int j = 1; j < k; ++j) cum += __shfl(nqc_i, j, 64);
+  // col 9: CumNQC (:400-410), sum over prefix sizes 2..n in order
+  const double cum = ordered_sum((lane >= 1 && act) ? nqc_i : 0.0, k);
   const double cumnqc = k < 2 ? 0.0 : cum / (double)(k - 1);
 
-  // ---- sequential single-accumulator loops (uniform across lanes)
-  const double muhat = mu <= 0.0 ? 1.0 : mu;                         // SMV
-  const double baseline = 1.0 / (0.01 > mu ? 0.01 : mu);             // WIG
-  const double std_full = sqrt(var_full);                            // RSD
-  const double thr = xs[0] * 0.5;                                    // SigmaX
-  double smv = 0.0, wig = 0.0, skew = 0.0, snqc = 0.0, mx = xs[0], mn = xs[0];
-  Kahan kf;
-  kahan_init(kf);
-  int nf = 0;
-  for (int j = 0; j < k; ++j) {
-    const double xj = xs[j];
-    if (xj > 0.0) smv += xj * fabs(log(xj / muhat));
-    wig += (xj - baseline);
-    skew += pow((xj - mu) / std_full, 3.0);
-    if (xj > 0.0) {
-      const double del = xj - mu;
-      const double f2 = (del * del) / xj;
-      const double prod = pow(1.0, 0.33) * pow(f2, 0.33);
-      snqc += pow(prod, 0.33);
+  // per-element terms, one element per lane (transcendentals run once each)
+  const double muhat = mu <= 0.0 ? 1.0 : mu;                  // SMV
+  const double baseline = 1.0 / (0.01 > mu ? 0.01 : mu);      // WIG
+  const double std_full = sqrt(var_full);                     // RSD
+  const double x0 = readlane_f64(x, 0);
+  const double thr = x0 * 0.5;                                // SigmaX
+  double t_smv = 0.0, t_snqc = 0.0, t_skew = 0.0, t_wig = 0.0, t_uw = 0.0, t_w = 0.0;
+  if (act) {
+    if (x > 0.0) {
+      t_smv = x * fabs(log(x / muhat));
+      const double del = x - mu;
+      const double prod = pow(1.0, 0.33) * pow((del * del) / x, 0.33);
+      t_snqc = pow(prod, 0.33);
     }
-    if (xj >= thr) { kahan_add(kf, xj); ++nf; }
-    mx = fmax(mx, xj);
-    mn = fmin(mn, xj);
+    t_skew = pow((x - mu) / std_full, 3.0);
+    t_wig = x - baseline;
+    if (lane < 20) {  // UEF DCG weights (:349-363)
+      t_w = 1.0 / (log((double)(lane + 2)) / log(2.0));
+      t_uw = x * t_w;
+    }
   }
-  // ---- col 4: SigmaX (QPPBridge.java:299-319)
+  // Java adds the x <= 0 terms of SMV / SNQC as "skip": adding +0.0 is the same.
+  const double smv = ordered_sum(t_smv, k);
+  const double wig = ordered_sum(t_wig, k);
+  const double skew = ordered_sum(t_skew, k);
+  const double snqc = ordered_sum(t_snqc, k);
+  const int ku = k < 20 ? k : 20;
+  const double util = ordered_sum(t_uw, ku);
+  const double wsum = ordered_sum(t_w, ku);
+  // col 4: SigmaX (:299-319): compensated mean / variance of {x >= thr} in order
+  const bool inF = act && x >= thr;
+  const uint64_t fmask = ballot(inF);
+  const int nf = __popcll(fmask);
   double sigmax = 0.0;
   if (k >= 2 && nf >= 2) {
+    Kahan kf;
+    kahan_init(kf);
+    for (int j = 0; j < k; ++j)
+      if ((fmask >> j) & 1ull) kahan_add(kf, readlane_f64(x, j));
     const double mf = kahan_final(kf) / (double)nf;
+    const double dv = x - mf;
+    const double t = dv * dv;
     Kahan kfv;
     kahan_init(kfv);
-    for (int j = 0; j < k; ++j) {
-      const double xj = xs[j];
-      if (xj >= thr) {
-        const double del = xj - mf;
-        kahan_add(kfv, del * del);
-      }
-    }
+    for (int j = 0; j < k; ++j)
+      if ((fmask >> j) & 1ull) kahan_add(kfv, readlane_f64(t, j));
     sigmax = sqrt(kahan_final(kfv) / (double)nf);
   }
-  // ---- col 6: UEF (QPPBridge.java:349-363)
-  double util = 0.0, wsum = 0.0;
-  const int ku = k < 20 ? k : 20;
-  const double ln2 = log(2.0);
-  for (int i = 0; i < ku; ++i) {
-    const double wgt = 1.0 / (log((double)(i + 2)) / ln2);
-    util += xs[i] * wgt;
-    wsum += wgt;
-  }
+  const double mx = wave_max(act ? x : -INFINITY);
+  const double mn = wave_min(act ? x : INFINITY);
   double res[kQppCols];
   res[0] = nqc;
   res[1] = smv / (double)k;

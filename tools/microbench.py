@@ -1,7 +1,7 @@
 """Per-kernel timing of the C2 pipeline (development tool, not the bench)."""
 import sys, json
 from pathlib import Path
-ROOT = Path(__file__).resolve().parent
+ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
 import numpy as np, torch
 from qppfuse import engine, _lib

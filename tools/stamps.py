@@ -1,0 +1,43 @@
+"""Phase breakdown of qf_fuse from the QF_STAMPS diagnostic build (development tool).
+
+Reads per-block s_memtime deltas (shader cycles) of thread 0 at phase
+boundaries; shares matter, not absolute length (stamps add fences).
+"""
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
+import numpy as np
+import torch
+from qppfuse import _lib
+
+_lib.LIB_PATH = ROOT / "qpp-fusion-rag_amd" / "qppfuse" / "libqppfuse_stamps.so"
+from qppfuse import engine
+
+lib = _lib.lib()
+lib.qf_debug_stamps.restype = C.c_int
+lib.qf_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
+NB, NS = 4096, 16
+names = ["load+insert", "compact+umap", "zero(acc)", "rounds", "keys", "sort", "output", "-", "cs:count", "cs:bar1", "cs:scan+bar", "cs:scatter", "cs:bar3", "cs:readback"]
+Q, R, K = 3452, 5, 1000
+dev = torch.device("cuda", 0)
+off, docid, raw = engine.synth_runs(0, Q, R, K)
+_, micro = engine.minmax_per_query(raw, off, want_norm=False)
+w = torch.rand(Q * R, dtype=torch.float64, device=dev)
+buf = np.zeros(NB * NS, np.uint64)
+out = {}
+for ms in (["rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]):
+    engine.fuse(off, docid, micro, R, ms, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    lib.qf_debug_stamps(buf.ctypes.data_as(C.c_void_p), NB * NS, 1)
+    engine.fuse(off, docid, micro, R, ms, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    lib.qf_debug_stamps(buf.ctypes.data_as(C.c_void_p), NB * NS, 1)
+    st = buf.reshape(NB, NS)[:Q, :14].astype(np.float64)
+    tot = st[:, :7].sum(1).mean()
+    out["+".join(ms)] = {"cycles_per_block": round(tot),
+                         **{n: round(float(st[:, i].mean())) for i, n in enumerate(names)}}
+print(json.dumps(out, indent=1))
