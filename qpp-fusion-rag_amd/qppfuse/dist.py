@@ -1,0 +1,40 @@
+"""Query sharding across GPUs (one process per GPU) and the one collective of the path.
+
+Fusion is independent per query; QPP normalisation couples the queries of each
+retriever through per-column min / max (src/qpp.py:347-361).  Each rank reduces
+its shard to [min, -max] per (retriever, column) (qf_qpp_colminmax) and one
+element-wise MIN all-reduce (RCCL over xGMI with backend "nccl"; gloo in the CPU
+tests) combines them.  Fused lists stay on the rank that produced them.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+
+def shard_range(n_queries: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, balanced [begin, end) of `n_queries` for `rank` of `world`."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    base, extra = divmod(n_queries, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def shard_by_entries(list_off: np.ndarray, n_retrievers: int, world: int) -> np.ndarray:
+    """Query boundaries [world+1] balancing Σ entries (ragged lists) across ranks."""
+    qoff = np.asarray(list_off)[:: n_retrievers]
+    total = int(qoff[-1])
+    targets = [total * r // world for r in range(world + 1)]
+    b = np.searchsorted(qoff, targets, side="left")
+    b[0], b[-1] = 0, len(qoff) - 1
+    return np.maximum.accumulate(b)
+
+
+def allreduce_minmax(mm, group=None):
+    """In-place element-wise MIN over ranks of the [min, -max] buffer (a torch tensor)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
+    return mm

@@ -1,0 +1,75 @@
+"""Multi-rank host logic on CPU: sharding and the QPP min/max all-reduce (gloo, world 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ref_port
+
+
+def test_shard_range_covers_everything():
+    from qppfuse.dist import shard_range
+    for n in (0, 1, 7, 3452, 1_000_000):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(n, w, r) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            sizes = [e - b for b, e in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_by_entries_balances_ragged_lists():
+    from qppfuse.dist import shard_by_entries
+    rng = np.random.default_rng(0)
+    R, Q = 5, 1000
+    lens = rng.integers(0, 2000, Q * R)
+    off = np.concatenate([[0], np.cumsum(lens)])
+    for w in (2, 4, 8):
+        b = shard_by_entries(off, R, w)
+        assert b[0] == 0 and b[-1] == Q and np.all(np.diff(b) >= 0)
+        per = [off[b[i + 1] * R] - off[b[i] * R] for i in range(w)]
+        assert max(per) - min(per) <= 2 * 2000 * R
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, raw, Q, R, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qppfuse.dist import allreduce_minmax, shard_range
+    b, e = shard_range(Q, world, rank)
+    mine = raw[b * R:e * R].reshape(e - b, R, 13)
+    mm = torch.from_numpy(np.concatenate([mine.min(axis=0).ravel(),
+                                          (-mine.max(axis=0)).ravel()]).copy())
+    allreduce_minmax(mm)
+    out[rank] = mm.numpy().copy()
+    dist.destroy_process_group()
+
+
+def test_sharded_qpp_normalisation_equals_global():
+    """[min, -max] per shard + MIN all-reduce == the reference's global min-max."""
+    rng = np.random.default_rng(1)
+    Q, R, world = 37, 3, 2
+    raw = rng.normal(0, 5, (Q * R, 13))
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, raw, Q, R, out), nprocs=world, join=True)
+    assert np.array_equal(out[0], out[1])
+    mm = out[0]
+    lo, hi = mm[:R * 13].reshape(R, 13), -mm[R * 13:].reshape(R, 13)
+    for r in range(R):
+        res = {str(q): raw[q * R + r].tolist() for q in range(Q)}
+        want = ref_port.normalize_qpp(res, "minmax")
+        scale = np.where(hi[r] > lo[r], hi[r] - lo[r], 1.0)
+        got = (raw[r::R] - lo[r]) / scale
+        for q in range(Q):
+            assert got[q].tolist() == [float(v) for v in want[str(q)]]

@@ -1,0 +1,38 @@
+"""Turn a tools/profile.sh output directory into committed summaries under profiles/.
+
+python tools/summarize_profile.py gpurun_out/prof r01
+ -> profiles/r01_kernel_stats.csv  (rocprofv3 --kernel-trace --stats, verbatim)
+    profiles/r01_pmc.json          (per-kernel mean FETCH_SIZE / WRITE_SIZE per launch,
+                                    bytes = counter x 1024; no gfx950 x2 correction is
+                                    applied: calibrated on this pattern)
+"""
+import collections
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+src, tag = Path(sys.argv[1]), sys.argv[2]
+out = Path(__file__).resolve().parents[1] / "profiles"
+out.mkdir(exist_ok=True)
+shutil.copy(src / "trace" / "run_kernel_stats.csv", out / f"{tag}_kernel_stats.csv")
+pmc = collections.defaultdict(dict)
+for name in ("fetch", "write"):
+    rows = list(csv.DictReader(open(src / name / "run_counter_collection.csv")))
+    agg = collections.defaultdict(list)
+    for r in rows:
+        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (k, c), v in agg.items():
+        pmc[k][c] = {"mean_kb_per_launch": sum(v) / len(v), "launches": len(v)}
+stats = {r["Name"]: float(r["AverageNs"]) for r in csv.DictReader(open(src / "trace" / "run_kernel_stats.csv"))}
+summary = {}
+for k, d in pmc.items():
+    f = d.get("FETCH_SIZE", {}).get("mean_kb_per_launch")
+    w = d.get("WRITE_SIZE", {}).get("mean_kb_per_launch")
+    summary[k] = {"fetch_bytes": None if f is None else f * 1024,
+                  "write_bytes": None if w is None else w * 1024,
+                  "hbm_bytes": None if f is None or w is None else (f + w) * 1024,
+                  "avg_ns": stats.get(k)}
+(out / f"{tag}_pmc.json").write_text(json.dumps(summary, indent=1))
+print(json.dumps(summary, indent=1))
