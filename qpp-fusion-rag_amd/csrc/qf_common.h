@@ -23,6 +23,10 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
 // Inclusive prefix sum across the 64 lanes of a wave.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;

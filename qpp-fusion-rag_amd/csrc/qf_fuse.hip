@@ -1,40 +1,41 @@
-// qf_fuse.hip — multi-method rank fusion, one workgroup per query (gfx950).
+// qf_fuse.hip — multi-method rank fusion on gfx950: a join kernel + a fuse kernel.
 //
 // Replaces the per-row Python loops of src/fusion.py:
 //   combsum / combmnz / rrf      (ranx fuse, src/fusion.py:170-230, 455-477)
 //   weighted_combsum / _combmnz / weighted_rrf (src/fusion.py:237-380)
 // and the per-query sort of write_runfile (src/fusion.py:480-492).
 //
-// Per query q (N = Σ_r |list(q,r)| entries, N <= NMAX = BLOCK*ITEMS):
-//  1. Entries are loaded striped (entry e = j*BLOCK + tid), coalesced, and kept
-//     in registers for the whole kernel (docid is only needed for the join).
-//  2. LDS hash-join: open addressing on docid (atomicCAS), first-seen entry
-//     index per slot via atomicMin.  Entry index e is retriever-major, so the
-//     smallest e of a document is exactly the reference's first-seen order
-//     (dict insertion order over rankers in runs order, rows in file order).
-//  3. Distinct documents are compacted in first-seen order (ballot + scan):
-//     u = 0..U-1, and union_docid[u] is written.
-//  4. For each requested method, fused scores are accumulated in LDS in R
-//     rounds, one retriever per round, separated by barriers: within a round
-//     every u receives at most one contribution, so each document's sum is
-//     formed in exactly the reference's order (retriever order) — bit-exact
-//     IEEE double, no atomics on floats.
-//  5. A stable LSD radix sort (8-bit digits, wave ballot-match ranking, one
-//     LDS scatter per pass, passes over constant digits skipped) orders the
-//     documents by fused score descending with ties in first-seen order —
-//     Python's stable sorted(key=-score) of _ranx_to_dict / write_runfile.
-//  6. perm (u of each rank) and the fused score are written, coalesced.
+// join_kernel — one workgroup per query (N = Σ_r |list(q,r)| entries):
+//   docids are inserted into an LDS hash table (open addressing, ds_cmpst); each
+//   slot ORs in a retriever bit.  Lists are retriever-major with rows in file
+//   order, so a document's first-seen entry (the reference's defaultdict
+//   insertion order, src/fusion.py:264-279) is its entry in the lowest
+//   retriever holding it.  Distinct documents are numbered u = 0..U-1 in
+//   first-seen order (ballot + scan), and every entry is placed into its
+//   document's contribution group, groups in u order, entries inside a group in
+//   retriever order: goff[u] / grp[k] (workspace).  A retriever bit already set
+//   means a docid repeats inside one list -> per-query error.
+// fuse_kernel — one workgroup per (query, method), the methods of a query on
+//   one XCD (blockIdx % 8) so the workspace is re-read from that XCD's L2:
+//   every document's fused score is its group's contributions added in
+//   retriever order — the reference's left-to-right sum, bit for bit, no
+//   atomics, no barriers — kept in registers in the sort's layout, then a
+//   stable sort by score descending, ties in first-seen order (Python's stable
+//   sorted(), src/fusion.py:475,488), then perm / fused are written coalesced.
+#include <cstdlib>
+
+#include "../../include/qppfuse.h"
 #include "qf_common.h"
 #include "qf_internal.h"
-#include "../../include/qppfuse.h"
 
 namespace qf {
 
 constexpr int kRMax = 16;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 #ifdef QF_STAMPS
 // Diagnostic build only (tools/): per-block phase cycle counts of block 0..kStampBlocks-1.
-constexpr int kStampBlocks = 4096, kStampSlots = 16;
+constexpr int kStampBlocks = 32768, kStampSlots = 16;
 __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 #define QF_STAMP_INIT() unsigned long long _st_prev = __builtin_amdgcn_s_memtime()
 #define QF_STAMP(slot)                                                          \
@@ -48,34 +49,6 @@ __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 #define QF_STAMP_INIT()
 #define QF_STAMP(slot)
 #endif
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-
-
-template <int BLOCK, int ITEMS, int TB, int MINW>
-struct FuseCfg {
-  static constexpr int kBlock = BLOCK;
-  static constexpr int kItems = ITEMS;
-  static constexpr int kWaves = BLOCK / 64;
-  static constexpr int kNMax = BLOCK * ITEMS;
-  static constexpr int kTS = 1 << TB;
-  static constexpr int kTB = TB;
-  static constexpr int kMinWaves = MINW;
-  // LDS: [umap u16 NMAX] then either the hash table (phase 1-2) or the
-  // accumulate/sort image (phase 3), which alias.
-  static constexpr int kUmapBytes = (2 * kNMax + 15) & ~15;
-  static constexpr int kTableBytes = 8 * kTS;
-  static constexpr int kAccOff = 0;                                // f64 / u64 [NMAX]
-  static constexpr int kPayOff = kAccOff + 8 * kNMax;              // u16 [NMAX]
-  static constexpr int kCntOff = kPayOff + 2 * kNMax;              // u8  [NMAX]
-  static constexpr int kNegOff = (kCntOff + kNMax + 15) & ~15;     // u32 [NMAX/32]
-  static constexpr int kHistOff = (kNegOff + 4 * ((kNMax + 31) / 32) + 15) & ~15;  // u32 [W][256]
-  static constexpr int kPostBytes = kHistOff + 4 * 256 * kWaves;
-  static constexpr int kSmem =
-      kUmapBytes + (kTableBytes > kPostBytes ? kTableBytes : kPostBytes);
-  static_assert(kTS >= kNMax, "hash table must hold every entry");
-  static_assert(kNMax <= 65535, "perm / umap are uint16");
-  static_assert(kSmem <= 160 * 1024, "LDS budget");
-};
 
 // Score as stored: int32 micro-units (exact "%.6f" text) or double.
 template <int KIND>
@@ -91,7 +64,6 @@ struct ScoreIn<1> {
     return (double)((const int32_t*)p)[i] / 1e6;
   }
 };
-
 
 // ---- block-level helpers ------------------------------------------------------
 
@@ -113,11 +85,11 @@ __device__ __forceinline__ void block_min_max(uint64_t kmn, uint64_t kmx,
 
 template <int ITEMS, int WAVES>
 struct SortCtx {
-  uint32_t* hist;    // [WAVES][256]
-  uint64_t* skey;    // [NMAX]
-  uint16_t* spay;    // [NMAX]
-  uint32_t* bstart;  // [257] bucket starts of the last counting pass
-  int* flag;         // largest bucket of the last counting pass
+  uint32_t* hist;    // [256][WAVES]
+  uint64_t* skey;    // [UMAX]
+  uint16_t* spay;    // [UMAX]
+  uint32_t* wtot;    // [WAVES] scan carries
+  int* flag;         // fix-up status
   int U, rows, lane, wid, tid;
 };
 
@@ -125,20 +97,23 @@ struct SortCtx {
 // in registers, wave-major: item i = (wid*rows + j)*64 + lane.  Within a wave a
 // row's items are ranked by a ballot match of their digits; the row's leader
 // lane claims a run of slots with one LDS atomicAdd (LDS ops of a wave execute
-// in program order, so rows stay ordered without a read->write chain); digit
-// offsets are an exclusive scan, digits ascending and waves ascending within a
-// digit.  Leaves the scattered sequence in skey/spay, bucket starts in bstart
-// and the largest bucket in *flag.  `readback` reloads the registers.
+// in program order, so rows stay ordered without a read->write chain); the
+// (digit, wave) offsets are one block-wide exclusive scan of the [digit][wave]
+// counters.  Leaves the scattered sequence in skey/spay; `readback` reloads
+// the registers.
 template <int ITEMS, int WAVES, class Digit>
 __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
                                               uint64_t (&key)[ITEMS], uint32_t (&pay)[ITEMS],
                                               Digit digit, bool readback) {
+  static_assert(WAVES % 4 == 0 || WAVES == 1 || WAVES == 2, "4 counters per thread");
   const int lane = sx.lane, wid = sx.wid;
   int rp = sx.rows;
   asm volatile("" : "+s"(rp));
-  uint32_t* h = sx.hist + wid * 256;
+  // hist is [digit][wave]: in that flat order an exclusive scan IS the scatter
+  // offset of (wave, digit) — digits ascending, waves ascending within a digit.
+  uint32_t* hist = sx.hist;
   QF_STAMP_INIT();
-  for (int k = lane; k < 256; k += 64) h[k] = 0u;
+  for (int k = lane; k < 256; k += 64) hist[k * WAVES + wid] = 0u;
   uint32_t rank_in[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -156,7 +131,7 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
       const uint32_t before = mbcnt(peers);
       const int leader = __ffsll((unsigned long long)peers) - 1;
       uint32_t old = 0u;
-      if (valid && before == 0) old = atomicAdd(&h[d], (uint32_t)__popcll(peers));
+      if (valid && before == 0) old = atomicAdd(&hist[d * WAVES + wid], (uint32_t)__popcll(peers));
       old = (uint32_t)__shfl((int)old, leader < 0 ? 0 : leader, 64);
       rank_in[j] = old + before;
     }
@@ -164,31 +139,21 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   QF_STAMP(8);
   __syncthreads();
   QF_STAMP(9);
-  if (wid == 0) {
-    uint32_t run0 = 0, run1 = 0, run2 = 0, run3 = 0;
+  // block-wide exclusive scan of the 256*WAVES counters, 4 per thread
+  {
+    constexpr int PER = 256 * WAVES / (64 * WAVES);  // == 4
+    static_assert(PER == 4, "");
+    uint4 v = *(uint4*)&hist[4 * sx.tid];
+    const uint32_t t = v.x + v.y + v.z + v.w;
+    const uint32_t incl = wave_incl_scan_dpp(t);
+    if (lane == 63) sx.wtot[wid] = incl;
+    __syncthreads();
+    uint32_t pre = 0u;
 #pragma unroll
-    for (int ww = 0; ww < WAVES; ++ww) {
-      uint4* row = (uint4*)&sx.hist[ww * 256 + 4 * lane];
-      const uint4 c = *row;
-      *row = make_uint4(run0, run1, run2, run3);
-      run0 += c.x; run1 += c.y; run2 += c.z; run3 += c.w;
-    }
-    const uint32_t tot = run0 + run1 + run2 + run3;
-    const uint32_t lb = wave_incl_scan_dpp(tot) - tot;
-    const uint32_t b0 = lb, b1 = lb + run0, b2 = b1 + run1, b3 = b2 + run2;
-#pragma unroll
-    for (int ww = 0; ww < WAVES; ++ww) {
-      uint4* row = (uint4*)&sx.hist[ww * 256 + 4 * lane];
-      uint4 c = *row;
-      c.x += b0; c.y += b1; c.z += b2; c.w += b3;
-      *row = c;
-    }
-    *(uint4*)&sx.bstart[4 * lane] = make_uint4(b0, b1, b2, b3);
-    if (lane == 63) sx.bstart[256] = lb + tot;
-    uint32_t mx = max(max(run0, run1), max(run2, run3));
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
-    if (lane == 0) *sx.flag = (int)mx;
+    for (int w = 0; w < WAVES; ++w)
+      if (w < wid) pre += sx.wtot[w];
+    const uint32_t ex = pre + incl - t;
+    *(uint4*)&hist[4 * sx.tid] = make_uint4(ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z);
   }
   __syncthreads();
   QF_STAMP(10);
@@ -197,7 +162,7 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rp + j) * 64 + lane;
     if (j < rp && i < sx.U) {
-      const uint32_t dst = h[digit(key[j])] + rank_in[j];
+      const uint32_t dst = hist[digit(key[j]) * WAVES + wid] + rank_in[j];
       sx.skey[dst] = key[j];
       sx.spay[dst] = (uint16_t)pay[j];
     }
@@ -230,21 +195,22 @@ struct Digit {
 
 // Stable sort of the items by key ascending (keys are ~orderable(score): scores
 // descending; ties keep input = first-seen order).  kmin / kmax: extreme keys.
-//  1. LSD counting passes on the 32 most significant bits of (key - kmin);
+//  1. LSD counting passes on the kWindow most significant bits of (key - kmin);
 //  2. runs of items that agree on those 32 bits (contiguous, first-seen order,
 //     almost always of length 1 or 2) are put in full-key order by a stable
 //     insertion sort run by the thread at the run's start.
 // A run longer than kRunMax sends the block on with LSD passes over every bit
 // from bit 0: started from the order of step 1 (equal keys still first-seen)
 // they give the same stable result.
-constexpr int kRunMax = 64;
+constexpr int kRunMax = 48;
+constexpr int kWindow = 24;  // bits sorted by LSD passes (3 passes of 8)
 
 template <int ITEMS, int WAVES>
 __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&key)[ITEMS],
                           uint32_t (&pay)[ITEMS], uint64_t kmin, uint64_t kmax) {
   if (kmin >= kmax) return;  // all keys equal (or no items): first-seen order stands
   const int hb = 64 - __clzll((long long)(kmax - kmin));
-  const int lo = hb > 32 ? hb - 32 : 0;
+  const int lo = hb > kWindow ? hb - kWindow : 0;
   int sh = lo;
   bool fallback = false;
 #pragma unroll 1
@@ -305,12 +271,16 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&key)[ITEMS
   }
 }
 
-// Sorted items -> perm (u of rank i) and the fused score, coalesced.
+// Sorted items -> perm (u of rank i) and the fused score, coalesced.  Payload
+// bit 15 marks a -0.0 score (the key folds -0.0 onto +0.0 so they tie, as in
+// Python's sort; the value written keeps its sign, as "%.6f" prints it).
+constexpr uint32_t kNegZero = 0x8000u;
+
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
                                           const uint64_t (&key)[ITEMS],
-                                          const uint32_t (&pay)[ITEMS], const uint32_t* negz,
-                                          uint16_t* operm, double* ofused) {
+                                          const uint32_t (&pay)[ITEMS], uint16_t* operm,
+                                          double* ofused) {
   int ro = sx.rows;
   asm volatile("" : "+s"(ro));
 #pragma unroll
@@ -318,60 +288,50 @@ __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
     const int i = (sx.wid * ro + j) * 64 + sx.lane;
     if (j < ro && i < sx.U) {
       double v = f64_from_asc_key(~key[j]);
-      if (v == 0.0 && ((negz[pay[j] >> 5] >> (pay[j] & 31)) & 1u)) v = -0.0;
-      operm[i] = (uint16_t)pay[j];
+      if (v == 0.0 && (pay[j] & kNegZero)) v = -0.0;
+      operm[i] = (uint16_t)(pay[j] & ~kNegZero);
       ofused[i] = v;
     }
   }
 }
 
+
+// ============================================================================
+// join_kernel
+// ============================================================================
+template <int BLOCK, int ITEMS, int TB>
+struct JoinCfg {
+  static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64;
+  static constexpr int kNMax = BLOCK * ITEMS, kTS = 1 << TB, kTB = TB;
+  static_assert(kTS >= kNMax, "hash table must hold every entry");
+  static_assert(kNMax <= 65535, "u / group offsets are uint16");
+  static_assert(8 * kTS <= 160 * 1024, "LDS budget");
+};
+
 template <class C, int KIND>
-__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParams p) {
+__global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   constexpr int BLOCK = C::kBlock, ITEMS = C::kItems, WAVES = C::kWaves;
   constexpr int NMAX = C::kNMax, TS = C::kTS;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
+  __shared__ __attribute__((aligned(16))) uint32_t tkey[TS];
+  __shared__ __attribute__((aligned(16))) uint32_t tmask[TS];
   __shared__ int64_t s_off[kRMax + 1];
-  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax];
-  __shared__ int s_chunk[ITEMS * WAVES];
-  __shared__ int s_U, s_status, s_flag;
-  __shared__ __attribute__((aligned(16))) uint32_t s_bstart[260];
-  __shared__ unsigned long long s_or[2], s_and[2];
+  __shared__ int s_cnt[ITEMS * WAVES], s_gof[ITEMS * WAVES];
+  __shared__ int s_U, s_status;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t q = blockIdx.x;
   if (q >= p.n_queries) return;
   const int R = p.R;
-  QF_STAMP_INIT();
-
   if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
   if (tid == 0) s_status = 0;
   __syncthreads();
   const int64_t base = s_off[0];
   const int64_t N64 = s_off[R] - base;
-  if (N64 > NMAX) {  // uniform: every thread sees the same offsets
+  if (N64 > NMAX) {  // uniform
     if (tid == 0) p.union_count[q] = QF_QSTATUS_TOOBIG;
     return;
   }
   const int N = (int)N64;
-  if (tid < R) {
-    const int64_t a = s_off[tid], b = s_off[tid + 1];
-    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
-    // ranx min-max (norm="min-max", the fuse() default).  Lists are sorted
-    // descending (checked below), so max / min are the end points.
-    double mx = 0.0, mn = 0.0;
-    if (b > a) {
-      mx = ScoreIn<KIND>::load(p.score, a);
-      mn = ScoreIn<KIND>::load(p.score, b - 1);
-    }
-    s_min[tid] = mn;
-    s_den[tid] = mx - mn;
-  }
-
-  uint16_t* umap = (uint16_t*)smem;                      // entry e -> u
-  unsigned char* img = smem + C::kUmapBytes;
-  // ---- phase 1: LDS hash insert -------------------------------------------
-  uint32_t* tkey = (uint32_t*)img;
-  uint32_t* tmask = tkey + TS;  // retrievers holding the slot's docid; later slot -> u
   for (int i = tid * 4; i < TS; i += BLOCK * 4) {
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
     *(uint4*)&tmask[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -383,10 +343,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
     dk[j] = e < N ? p.docid[base + e] : kEmpty;
   }
   __syncthreads();
-  // Entry e = j*BLOCK + tid belongs to list r(e); lists are retriever-major, so
-  // a document's first-seen entry is its entry in the lowest retriever holding
-  // it: the lowest bit of the slot's retriever mask.  A bit already set when an
-  // entry ORs it in means the docid repeats inside one list (unsupported).
+  // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
   int status = 0;
   uint32_t rj[ITEMS];
 #pragma unroll
@@ -408,227 +365,287 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
       const uint32_t old = atomicOr(&tmask[h], 1u << r);
       if ((old >> r) & 1u) status = QF_QSTATUS_DUPDOC;
       dk[j] = h;  // keep the slot
+      // preconditions of the ranx methods / W-RRF (checked once, here)
+      const int64_t g = base + e;
+      if (g + 1 < s_off[r + 1]) {
+        if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
+            ScoreIn<KIND>::load(p.score, g + 1) > ScoreIn<KIND>::load(p.score, g))
+          status = QF_QSTATUS_UNSORTED;
+        if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
+          status = QF_QSTATUS_RANKORDER;
+      }
     }
   }
   if (status) atomicMin(&s_status, status);
   __syncthreads();
-  QF_STAMP(0);
-
-  // ---- phase 2: distinct documents in first-seen order --------------------
-  uint32_t repm = 0u;  // bit j: entry j is its document's first occurrence
+  // ---- number distinct documents in first-seen order; size their groups ------
+  uint32_t repm = 0u;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
-    const bool rep = (e < N) && (uint32_t)(__ffs(tmask[dk[j]]) - 1) == rj[j];
+    uint32_t pc = 0u;
+    bool rep = false;
+    if (e < N) {
+      const uint32_t msk = tmask[dk[j]];
+      rep = (uint32_t)(__ffs(msk) - 1) == rj[j];
+      pc = rep ? (uint32_t)__popc(msk) : 0u;
+    }
     repm |= (uint32_t)rep << j;
     const uint64_t b = ballot(rep);
-    if (lane == 0) s_chunk[j * WAVES + wid] = __popcll(b);
+    const uint32_t tot = readlane_u32(wave_incl_scan_dpp(pc), 63);
+    if (lane == 0) {
+      s_cnt[j * WAVES + wid] = __popcll(b);
+      s_gof[j * WAVES + wid] = (int)tot;
+    }
   }
   __syncthreads();
-  if (wid == 0) {
-    uint32_t carry = 0;
+  if (wid == 0) {  // exclusive scans over the (row, wave) chunks, in entry order
+    uint32_t c1 = 0, c2 = 0;
     for (int c0 = 0; c0 < ITEMS * WAVES; c0 += 64) {
       const int i = c0 + lane;
-      const uint32_t v = i < ITEMS * WAVES ? (uint32_t)s_chunk[i] : 0u;
-      const uint32_t incl = wave_incl_scan(v);
-      if (i < ITEMS * WAVES) s_chunk[i] = (int)(carry + incl - v);
-      carry += __shfl(incl, 63, 64);
+      const uint32_t v1 = i < ITEMS * WAVES ? (uint32_t)s_cnt[i] : 0u;
+      const uint32_t v2 = i < ITEMS * WAVES ? (uint32_t)s_gof[i] : 0u;
+      const uint32_t i1 = wave_incl_scan_dpp(v1), i2 = wave_incl_scan_dpp(v2);
+      if (i < ITEMS * WAVES) {
+        s_cnt[i] = (int)(c1 + i1 - v1);
+        s_gof[i] = (int)(c2 + i2 - v2);
+      }
+      c1 += readlane_u32(i1, 63);
+      c2 += readlane_u32(i2, 63);
     }
-    if (lane == 0) s_U = (int)carry;
+    if (lane == 0) s_U = (int)c1;
   }
   __syncthreads();
   const int U = s_U;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
+    const int e = j * BLOCK + tid;
     const bool rep = (repm >> j) & 1u;
     const uint64_t b = ballot(rep);
+    uint32_t msk = 0u, pc = 0u;
     if (rep) {
-      const uint32_t u = (uint32_t)s_chunk[j * WAVES + wid] + mbcnt(b);
-      p.union_docid[base + u] = tkey[dk[j]];
-      tmask[dk[j]] = u;  // slot -> u (only the representative writes)
+      msk = tmask[dk[j]];
+      pc = (uint32_t)__popc(msk);
     }
+    const uint32_t gpre = wave_incl_scan_dpp(pc) - pc;
+    if (rep) {
+      const uint32_t u = (uint32_t)s_cnt[j * WAVES + wid] + mbcnt(b);
+      const uint32_t go = (uint32_t)s_gof[j * WAVES + wid] + gpre;
+      p.union_docid[base + u] = tkey[dk[j]];
+      p.goff[base + u] = (uint16_t)go;
+      tkey[dk[j]] = u;                    // slot -> u
+      tmask[dk[j]] = go | (msk << 16);    // slot -> group offset | retriever mask
+    }
+    (void)e;
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
+  for (int j = 0; j < ITEMS; ++j) {  // each entry into its group, retriever order
     const int e = j * BLOCK + tid;
-    if (e < N) umap[e] = (uint16_t)tmask[dk[j]];
+    if (e < N) {
+      const uint32_t gm = tmask[dk[j]];
+      const int r = (int)rj[j];
+      const uint32_t k = (gm & 0xFFFFu) + (uint32_t)__popc((gm >> 16) & ((1u << r) - 1u));
+      const int64_t g = base + e;
+      p.gsc[base + k] = ScoreIn<KIND>::load(p.score, g);
+      p.gpr[base + k] = (uint32_t)(g - s_off[r]) | ((uint32_t)r << 16);
+    }
   }
-  __syncthreads();  // hash table dead from here; its LDS is re-used below
-  QF_STAMP(1);
+  if (tid == 0) p.union_count[q] = s_status ? s_status : U;
+}
 
-  double* acc = (double*)(img + C::kAccOff);
-  uint64_t* skey = (uint64_t*)(img + C::kAccOff);
-  uint16_t* spay = (uint16_t*)(img + C::kPayOff);
-  uint8_t* cnt = (uint8_t*)(img + C::kCntOff);
-  uint32_t* negz = (uint32_t*)(img + C::kNegOff);
-  uint32_t* hist = (uint32_t*)(img + C::kHistOff);
-  SortCtx<ITEMS, WAVES> sx{hist, skey, spay, s_bstart, &s_flag, U,
+// ============================================================================
+// fuse_kernel
+// ============================================================================
+template <int BLOCK, int ITEMS, int MINW>
+struct SortCfg {
+  static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64, kMinWaves = MINW;
+  static constexpr int kUMax = BLOCK * ITEMS;
+  static constexpr int kKeyOff = 0;                                  // u64 [UMAX]
+  static constexpr int kPayOff = 8 * kUMax;                          // u16 [UMAX]
+  static constexpr int kHistOff = (kPayOff + 2 * kUMax + 15) & ~15;  // u32 [W][256]
+  static constexpr int kSmem = kHistOff + 4 * 256 * kWaves;
+  static_assert(kUMax < (int)kNegZero, "payload bit 15 is the -0.0 flag");
+  static_assert(kSmem <= 160 * 1024, "LDS budget");
+};
+
+template <class C, int KIND>
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParams p, int umin) {
+  constexpr int ITEMS = C::kItems, WAVES = C::kWaves, UMAX = C::kUMax;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
+  __shared__ int64_t s_off[kRMax + 1];
+  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax];
+  __shared__ int s_flag;
+  __shared__ uint32_t s_wtot[16];
+  __shared__ unsigned long long s_kmin, s_kmax;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // block -> (query, method slot); blocks b and b+8 share an XCD, so all methods
+  // of query q (slot-major groups of 8 queries) run where its workspace lives.
+  const int M = __popc(p.methods);
+  const int64_t grp8 = (int64_t)(blockIdx.x >> 3);
+  const int64_t q = (grp8 / M) * 8 + (blockIdx.x & 7);
+  const int ms = (int)(grp8 % M);
+  if (q >= p.n_queries) return;
+  const int U = p.union_count[q];
+  if (U < 0 || U > UMAX || U < umin) return;  // error / other pass
+  int m = 0;
+  for (int t = 0, c = 0; t < 6; ++t)
+    if ((p.methods >> t) & 1) { if (c == ms) m = t; ++c; }
+  const int R = p.R;
+  QF_STAMP_INIT();
+  if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
+  if (tid == 0) { s_kmin = ~0ull; s_kmax = 0ull; }
+  __syncthreads();
+  if (tid < R) {
+    const int64_t a = s_off[tid], b = s_off[tid + 1];
+    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
+    // ranx min-max (norm="min-max", the fuse() default); lists are sorted
+    // descending (checked by join_kernel), so max / min are the end points.
+    double mx = 0.0, mn = 0.0;
+    if (b > a) {
+      mx = ScoreIn<KIND>::load(p.score, a);
+      mn = ScoreIn<KIND>::load(p.score, b - 1);
+    }
+    s_min[tid] = mn;
+    s_den[tid] = mx - mn;
+  }
+  __syncthreads();
+  const int64_t base = s_off[0];
+  const int N = (int)(s_off[R] - base);
+  uint64_t* skey = (uint64_t*)(smem + C::kKeyOff);
+  uint16_t* spay = (uint16_t*)(smem + C::kPayOff);
+  uint32_t* hist = (uint32_t*)(smem + C::kHistOff);
+  SortCtx<ITEMS, WAVES> sx{hist, skey, spay, s_wtot, &s_flag, U,
                            (U + 64 * WAVES - 1) / (64 * WAVES), lane, wid, tid};
-
-  // One job per method, in method-bit order.  CombMNZ / W-CombMNZ are the SUM
-  // family's sums times the per-document count (ranx comb_mnz, src/fusion.py:327):
-  // right after their SUM job they reuse its sorted sums (no accumulation rounds).
+  // ---- fused score of every document: its group, in retriever order ---------
   uint64_t key[ITEMS];
   uint32_t pay[ITEMS];
-  bool first_family = true;
-  bool have_sorted_sum = false;
-#pragma unroll 1
-  for (int job = 0; job < 6; ++job) {
-    if (!((p.methods >> job) & 1)) { have_sorted_sum = false; continue; }
-    const bool is_mnz = job == 1 || job == 4;
-    const int fam = is_mnz ? job - 1 : job;  // 0 sum, 2 rrf, 3 wsum, 5 wrrf
-    if (tid == 0) { s_or[0] = ~0ull; s_and[0] = 0ull; }  // min / max key
-    if (!(is_mnz && have_sorted_sum)) {
-      // -- zero accumulators ----------------------------------------------------
-      for (int i = tid; i < U; i += BLOCK) acc[i] = 0.0;
-      if (first_family)
-        for (int i = tid; i < U; i += BLOCK) cnt[i] = 0;
-      for (int i = tid; i < (NMAX + 31) / 32; i += BLOCK) negz[i] = 0u;
-      __syncthreads();
-      QF_STAMP(2);
-      // -- ordered accumulation: one retriever (list) per round -----------------
-      // Scores for round r+1 are loaded before round r's barrier.
-      const bool need_score = fam == 0 || fam == 3;
-      int status2 = 0;
-      constexpr int PF = 2;  // entries per thread prefetched per round (K <= 2*BLOCK)
-      double nxt[PF];
-      auto fetch = [&](int r, double (&dst)[PF]) {
-        const int e0 = (int)(s_off[r] - base), e1 = (int)(s_off[r + 1] - base);
+  uint64_t kmn = ~0ull, kmx = 0ull;
+  const bool mnz = m == 1 || m == 4;
+  const int rrf_k = p.rrf_k;
+  // group bounds: document i's group ends where i+1's starts (next lane), the
+  // last document's at N
+  int gsr[ITEMS], ger[ITEMS];
 #pragma unroll
-        for (int t = 0; t < PF; ++t) {
-          const int e = e0 + tid + t * BLOCK;
-          dst[t] = (need_score && e < e1) ? ScoreIn<KIND>::load(p.score, base + e) : 0.0;
-        }
-      };
-      fetch(0, nxt);
-#pragma unroll 1
-      for (int r = 0; r < R; ++r) {
-        double cur[PF];
-#pragma unroll
-        for (int t = 0; t < PF; ++t) cur[t] = nxt[t];
-        if (r + 1 < R) fetch(r + 1, nxt);
-        const double w = s_w[r], mn = s_min[r], den = s_den[r];
-        const int e0 = (int)(s_off[r] - base), e1 = (int)(s_off[r + 1] - base);
-        for (int e = e0 + tid, t = 0; e < e1; e += BLOCK, ++t) {
-          const int pos = e - e0;
-          double sj = 0.0;
-          if (need_score) {
-            if (t < PF) {
-#pragma unroll
-              for (int tt = 0; tt < PF; ++tt)
-                if (tt == t) sj = cur[tt];
-            } else {
-              sj = ScoreIn<KIND>::load(p.score, base + e);
-            }
-          }
-          double c;
-          if (fam == 0) c = den > 0.0 ? (sj - mn) / den : 0.0;          // ranx min-max
-          else if (fam == 2) c = 1.0 / (double)(p.rrf_k + pos + 1);     // ranx rrf
-          else if (fam == 3) c = w * sj;                                // fusion.py:273
-          else c = w / (double)(p.rrf_k + (p.rank ? p.rank[base + e] : pos + 1));  // :374
-          const uint32_t u = umap[e];
-          acc[u] += c;
-          if (first_family) {
-            cnt[u] += 1;
-            // preconditions: scores non-increasing in a list when a ranx method
-            // (min-max end points, RRF rank = position) is requested; rank column
-            // non-decreasing when W-RRF reads it (first-seen = rank order).
-            if (e + 1 < e1) {
-              if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
-                  ScoreIn<KIND>::load(p.score, base + e + 1) >
-                      ScoreIn<KIND>::load(p.score, base + e))
-                status2 = QF_QSTATUS_UNSORTED;
-              if ((p.methods & QF_WRRF) && p.rank && p.rank[base + e + 1] < p.rank[base + e])
-                status2 = QF_QSTATUS_RANKORDER;
-            }
-          }
-        }
-        __syncthreads();
-      }
-      if (first_family) {
-        if (status2) atomicMin(&s_status, status2);
-        __syncthreads();
-        if (tid == 0) p.union_count[q] = s_status ? s_status : U;
-      }
-      first_family = false;
-      QF_STAMP(3);
-      // -- keys in first-seen order -----------------------------------------------
-      int rowsk = sx.rows;
-      asm volatile("" : "+s"(rowsk));  // keep per-item addresses out of loop-invariant code
-      uint64_t kmn = ~0ull, kmx = 0ull;
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const int i = (wid * rowsk + j) * 64 + lane;
-        key[j] = ~0ull;
-        pay[j] = (uint32_t)i;
-        if (j < rowsk && i < U) {
-          double v = acc[i];
-          if (is_mnz) v = v * (double)cnt[i];
-          if (v == 0.0 && __double_as_longlong(v) < 0) atomicOr(&negz[i >> 5], 1u << (i & 31));
-          key[j] = ~f64_asc_key(v);  // ascending sort on ~key == descending score
-          kmn = min(kmn, key[j]);
-          kmx = max(kmx, key[j]);
-        }
-      }
-      block_min_max(kmn, kmx, &s_or[0], &s_and[0], lane);
-      __syncthreads();  // acc no longer read; skey may be written
-    } else {
-      // -- MNZ from the sorted SUM items, scattered back to first-seen (u) order
-      //    so that the stable sort breaks ties by first-seen order again.
-      uint64_t kmn = ~0ull, kmx = 0ull;
-      int rp = sx.rows;
-      asm volatile("" : "+s"(rp));
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const int i = (wid * rp + j) * 64 + lane;
-        if (j < rp && i < U) {
-          double v = f64_from_asc_key(~key[j]);
-          if (v == 0.0 && ((negz[pay[j] >> 5] >> (pay[j] & 31)) & 1u)) v = -0.0;
-          v = v * (double)cnt[pay[j]];
-          const uint64_t k2 = ~f64_asc_key(v);
-          skey[pay[j]] = k2;
-          kmn = min(kmn, k2);
-          kmx = max(kmx, k2);
-        }
-      }
-      block_min_max(kmn, kmx, &s_or[0], &s_and[0], lane);
-      __syncthreads();
-      asm volatile("" : "+s"(rp));
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const int i = (wid * rp + j) * 64 + lane;
-        pay[j] = (uint32_t)i;
-        key[j] = (j < rp && i < U) ? skey[i] : ~0ull;
-      }
-      __syncthreads();
-    }
-    QF_STAMP(4);
-    sort_desc(sx, key, pay, (uint64_t)s_or[0], (uint64_t)s_and[0]);
-    QF_STAMP(5);
-    const int slot = __popc(p.methods & ((1 << job) - 1));
-    write_out(sx, key, pay, negz, p.perm + (int64_t)slot * p.out_stride + base,
-              p.fused + (int64_t)slot * p.out_stride + base);
-    have_sorted_sum = !is_mnz && (fam == 0 || fam == 3);
-    __syncthreads();  // skey / negz / acc are rewritten by the next job
-    QF_STAMP(6);
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = (wid * sx.rows + j) * 64 + lane;
+    gsr[j] = (j < sx.rows && i < U) ? (int)p.goff[base + i] : N;
   }
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = (wid * sx.rows + j) * 64 + lane;
+    int nx = __shfl_down(gsr[j], 1, 64);
+    if (lane == 63 && j < sx.rows && i + 1 < U) nx = (int)p.goff[base + i + 1];
+    ger[j] = (i + 1 < U) ? nx : N;
+  }
+  constexpr int CAP = 6;  // contributions per document prefetched as one batch
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = (wid * sx.rows + j) * 64 + lane;
+    key[j] = ~0ull;
+    pay[j] = (uint32_t)i;
+    if (j < sx.rows && i < U) {
+      const int gs = gsr[j], ge = ger[j];
+      double sc[CAP];
+      uint32_t pr[CAP];
+#pragma unroll
+      for (int t = 0; t < CAP; ++t) {
+        sc[t] = 0.0;
+        pr[t] = 0u;
+        if (gs + t < ge) {
+          sc[t] = p.gsc[base + gs + t];
+          pr[t] = p.gpr[base + gs + t];
+        }
+      }
+      double acc = 0.0;
+      for (int k = gs, t = 0; k < ge; ++k, ++t) {
+        double s;
+        uint32_t q2;
+        if (t < CAP) {
+          s = sc[0];
+          q2 = pr[0];
+#pragma unroll
+          for (int tt = 1; tt < CAP; ++tt)
+            if (tt == t) { s = sc[tt]; q2 = pr[tt]; }
+        } else {
+          s = p.gsc[base + k];
+          q2 = p.gpr[base + k];
+        }
+        const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
+        double c;
+        if (m <= 1) {  // ranx min-max normalised score
+          const double den = s_den[r];
+          c = den > 0.0 ? (s - s_min[r]) / den : 0.0;
+        } else if (m == 2) {  // ranx rrf: rank = position
+          c = 1.0 / (double)(rrf_k + pos + 1);
+        } else if (m <= 4) {  // src/fusion.py:273
+          c = s_w[r] * s;
+        } else {  // src/fusion.py:374
+          const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
+          c = s_w[r] / (double)(rrf_k + rk);
+        }
+        acc += c;
+      }
+      if (mnz) acc = acc * (double)(ge - gs);  // CombMNZ: sum x count (src/fusion.py:327)
+      if (acc == 0.0 && __double_as_longlong(acc) < 0) pay[j] |= kNegZero;
+      key[j] = ~f64_asc_key(acc);  // ascending sort on ~key == descending score
+      kmn = min(kmn, key[j]);
+      kmx = max(kmx, key[j]);
+    }
+  }
+  block_min_max(kmn, kmx, &s_kmin, &s_kmax, lane);
+  __syncthreads();
+  QF_STAMP(0);
+  sort_desc(sx, key, pay, (uint64_t)s_kmin, (uint64_t)s_kmax);
+  QF_STAMP(1);
+  write_out(sx, key, pay, p.perm + (int64_t)ms * p.out_stride + base,
+            p.fused + (int64_t)ms * p.out_stride + base);
+  QF_STAMP(2);
 }
 
 // ---- launch -----------------------------------------------------------------
-using CfgS = FuseCfg<256, 4, 11, 4>;    // N <= 1024   (e.g. 3 x top-100)
-using CfgM = FuseCfg<512, 10, 13, 4>;   // N <= 5120   (5 x top-1000)
-using CfgL = FuseCfg<768, 10, 13, 3>;   // N <= 7680   (7 x top-1000)
+using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
+using JoinM = JoinCfg<512, 10, 13>;   // N <= 5120
+using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
+using SortS = SortCfg<256, 4, 4>;     // U <= 1024
+using SortM = SortCfg<512, 6, 8>;     // U <= 3072
+using SortL = SortCfg<768, 10, 3>;    // U <= 7680
 
-template <class C>
-static hipError_t launch_cfg(const FuseParams& p, int kind, hipStream_t st) {
-  dim3 grid((unsigned)p.n_queries), block(C::kBlock);
-  if (kind == 1) hipLaunchKernelGGL((fuse_kernel<C, 1>), grid, block, 0, st, p);
-  else hipLaunchKernelGGL((fuse_kernel<C, 0>), grid, block, 0, st, p);
-  return hipGetLastError();
+int fuse_max_entries() { return JoinL::kNMax; }
+
+size_t fuse_workspace_bytes(int64_t n_entries) {
+  return (size_t)(n_entries > 0 ? n_entries : 1) * (8 + 4 + 2) + 256;
 }
 
-int fuse_max_entries() { return CfgL::kNMax; }
+template <class J>
+static void launch_join(const FuseParams& p, int kind, hipStream_t st) {
+  dim3 grid((unsigned)p.n_queries), block(J::kBlock);
+  if (kind == 1) hipLaunchKernelGGL((join_kernel<J, 1>), grid, block, 0, st, p);
+  else hipLaunchKernelGGL((join_kernel<J, 0>), grid, block, 0, st, p);
+}
+
+template <class S>
+static void launch_sort(const FuseParams& p, int kind, int umin, hipStream_t st) {
+  const int M = __builtin_popcount((unsigned)p.methods);
+  const int64_t groups = (p.n_queries + 7) / 8;
+  dim3 grid((unsigned)(groups * 8 * M)), block(S::kBlock);
+  if (kind == 1) hipLaunchKernelGGL((fuse_kernel<S, 1>), grid, block, 0, st, p, umin);
+  else hipLaunchKernelGGL((fuse_kernel<S, 0>), grid, block, 0, st, p, umin);
+}
+
+hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
+  if (max_entries <= JoinS::kNMax) {
+    launch_join<JoinS>(p, kind, st);
+    launch_sort<SortS>(p, kind, 0, st);
+  } else {
+    if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
+    else launch_join<JoinL>(p, kind, st);
+    launch_sort<SortM>(p, kind, 0, st);
+    launch_sort<SortL>(p, kind, SortM::kUMax + 1, st);  // the queries SortM left
+  }
+  return hipGetLastError();
+}
 
 #ifdef QF_STAMPS
 extern "C" int qf_debug_stamps(unsigned long long* host, int n, int clear) {
@@ -641,11 +658,5 @@ extern "C" int qf_debug_stamps(unsigned long long* host, int n, int clear) {
   return 0;
 }
 #endif
-
-hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
-  if (max_entries <= CfgS::kNMax) return launch_cfg<CfgS>(p, kind, st);
-  if (max_entries <= CfgM::kNMax) return launch_cfg<CfgM>(p, kind, st);
-  return launch_cfg<CfgL>(p, kind, st);
-}
 
 }  // namespace qf

@@ -35,7 +35,8 @@ SIGNATURES = {
     "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
-                          _vp, _vp, _vp, _vp, _i64, _vp]),
+                          _vp, _vp, _vp, _vp, _i64, _vp, C.c_size_t, _vp]),
+    "qf_fuse_workspace_bytes": (C.c_size_t, [_i64]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
 }
 
@@ -55,7 +56,8 @@ def lib() -> C.CDLL:
     """Load libqppfuse.so once; raise loudly when it is absent."""
     global _LIB
     if _LIB is None:
-        path = Path(LIB_PATH)
+        import os
+        path = Path(os.environ.get("QPPFUSE_LIB", LIB_PATH))  # dev override (variant builds)
         if not path.exists():
             raise ImportError(
                 f"libqppfuse.so not built at {path}. Run `python __graft_entry__.py build` "

@@ -20,8 +20,8 @@ from qppfuse import engine
 lib = _lib.lib()
 lib.qf_debug_stamps.restype = C.c_int
 lib.qf_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
-NB, NS = 4096, 16
-names = ["load+insert", "compact+umap", "zero(acc)", "rounds", "keys", "sort", "output", "-", "cs:count", "cs:bar1", "cs:scan+bar", "cs:scatter", "cs:bar3", "cs:readback"]
+NB, NS = 32768, 16
+names = ["gather+keys", "sort", "output", "-", "-", "-", "-", "-", "cs:count", "cs:bar1", "cs:scan+bar", "cs:scatter", "cs:bar3", "cs:readback"]
 Q, R, K = 3452, 5, 1000
 dev = torch.device("cuda", 0)
 off, docid, raw = engine.synth_runs(0, Q, R, K)
@@ -36,8 +36,10 @@ for ms in (["rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"
     engine.fuse(off, docid, micro, R, ms, weights=w, max_entries=R * K)
     torch.cuda.synchronize()
     lib.qf_debug_stamps(buf.ctypes.data_as(C.c_void_p), NB * NS, 1)
-    st = buf.reshape(NB, NS)[:Q, :14].astype(np.float64)
-    tot = st[:, :7].sum(1).mean()
+    nb = ((Q + 7) // 8) * 8 * len(ms)
+    st = buf.reshape(NB, NS)[:nb, :14].astype(np.float64)
+    st = st[st[:, 0] > 0]  # blocks that ran (not padding / other pass)
+    tot = st[:, :3].sum(1).mean()
     out["+".join(ms)] = {"cycles_per_block": round(tot),
                          **{n: round(float(st[:, i].mean())) for i, n in enumerate(names)}}
 print(json.dumps(out, indent=1))
