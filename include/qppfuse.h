@@ -118,9 +118,9 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
 
 /*
  * Multi-method rank fusion of every query: a join kernel (one workgroup per
- * query, LDS hash join over docids, contribution groups in first-seen order)
- * and a fuse kernel (one workgroup per (query, method): ordered sums, stable
- * LDS radix sort by fused score).
+ * query: LDS hash join over docids, contribution groups in first-seen order,
+ * the ordered sums of every requested method) and a sort kernel (one workgroup
+ * per (query, method): stable LDS radix sort by fused score, in place).
  *
  * Inputs (device): list_off[Q*R+1] (int64), docid[E] (uint32, interned
  * docnos, 0xFFFFFFFF reserved), score[E] (score_kind), rank[E] (nullable
@@ -141,12 +141,7 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const uint32_t* docid, const void* score, int32_t score_kind,
             const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
             int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
-            uint16_t* perm, double* fused, int64_t out_stride, void* workspace,
-            size_t workspace_bytes, void* stream);
-
-/* Device workspace qf_fuse needs for a batch of n_entries (>= the total entry
- * count E; pass the same value as out_stride): per-document contribution groups. */
-size_t qf_fuse_workspace_bytes(int64_t n_entries);
+            uint16_t* perm, double* fused, int64_t out_stride, void* stream);
 
 /*
  * Benchmark / test support: generate Q*R synthetic lists of K entries

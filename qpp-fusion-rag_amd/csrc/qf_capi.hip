@@ -38,7 +38,6 @@ extern "C" {
 const char* qf_version(void) { return "qppfuse 0.1.0 gfx950"; }
 const char* qf_last_error(void) { return g_err.c_str(); }
 int qf_max_entries_per_query(void) { return qf::fuse_max_entries(); }
-size_t qf_fuse_workspace_bytes(int64_t n_entries) { return qf::fuse_workspace_bytes(n_entries); }
 
 int qf_minmax_per_query(const double* score, const int64_t* list_off, int64_t n_lists,
                         double* out_norm, int32_t* out_micro, void* stream) {
@@ -89,7 +88,7 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
             const double* weights, int32_t methods, int32_t rrf_k, int32_t max_entries,
             uint32_t* union_docid, int32_t* union_count, uint16_t* perm, double* fused,
-            int64_t out_stride, void* workspace, size_t workspace_bytes, void* stream) {
+            int64_t out_stride, void* stream) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "qf_fuse: n_retrievers must be in [1, %d]", kMaxR);
   if (methods <= 0 || (methods & ~QF_ALL_METHODS))
@@ -103,20 +102,10 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
                 max_entries, qf::fuse_max_entries());
   if (n_queries == 0) return QF_OK;
   if (!list_off || !docid || !score || !union_docid || !union_count || !perm || !fused ||
-      out_stride < 0 || !workspace)
+      out_stride < 0)
     return fail(QF_EINVAL, "qf_fuse: null buffer");
-  // entries of the batch = the caller's out_stride lower bound; the workspace
-  // must hold two uint16 per entry
-  if (workspace_bytes < qf::fuse_workspace_bytes(out_stride))
-    return fail(QF_EINVAL, "qf_fuse: workspace of %zu bytes < %zu required", workspace_bytes,
-                qf::fuse_workspace_bytes(out_stride));
-  char* ws = (char*)workspace;  // [gsc f64 E][gpr u32 E][goff u16 E], 8-byte aligned
-  double* gsc = (double*)ws;
-  uint32_t* gpr = (uint32_t*)(ws + 8 * out_stride);
-  uint16_t* goff = (uint16_t*)(ws + 12 * out_stride);
-  qf::FuseParams p{n_queries, n_retrievers, list_off, docid,      score, rank,
-                   weights,   methods,      rrf_k,    union_docid, union_count, perm,
-                   fused,     out_stride,   goff,     gpr,         gsc};
+  qf::FuseParams p{n_queries, n_retrievers, list_off,    docid, score, rank,       weights,
+                   methods,   rrf_k,        union_docid, union_count, perm, fused, out_stride};
   return check(qf::fuse_launch(p, score_kind, max_entries < 1 ? 1 : max_entries,
                                (hipStream_t)stream),
                "qf_fuse");

@@ -5,7 +5,7 @@
 //   weighted_combsum / _combmnz / weighted_rrf (src/fusion.py:237-380)
 // and the per-query sort of write_runfile (src/fusion.py:480-492).
 //
-// join_kernel — one workgroup per query (N = Σ_r |list(q,r)| entries):
+// join_kernel — one workgroup per query (N = Σ_r |list(q,r)| entries), all in LDS:
 //   docids are inserted into an LDS hash table (open addressing, ds_cmpst); each
 //   slot ORs in a retriever bit.  Lists are retriever-major with rows in file
 //   order, so a document's first-seen entry (the reference's defaultdict
@@ -13,15 +13,15 @@
 //   retriever holding it.  Distinct documents are numbered u = 0..U-1 in
 //   first-seen order (ballot + scan), and every entry is placed into its
 //   document's contribution group, groups in u order, entries inside a group in
-//   retriever order: goff[u] / grp[k] (workspace).  A retriever bit already set
-//   means a docid repeats inside one list -> per-query error.
-// fuse_kernel — one workgroup per (query, method), the methods of a query on
-//   one XCD (blockIdx % 8) so the workspace is re-read from that XCD's L2:
-//   every document's fused score is its group's contributions added in
-//   retriever order — the reference's left-to-right sum, bit for bit, no
-//   atomics, no barriers — kept in registers in the sort's layout, then a
-//   stable sort by score descending, ties in first-seen order (Python's stable
-//   sorted(), src/fusion.py:475,488), then perm / fused are written coalesced.
+//   retriever order.  A retriever bit already set means a docid repeats inside
+//   one list -> per-query error.  Then one thread per document adds its group's
+//   contributions in retriever order — the reference's left-to-right sum, bit
+//   for bit, no atomics — for every requested method at once, and writes the
+//   unsorted fused scores to fused[slot][u].
+// fuse_kernel — one workgroup per (query, method): reads fused[slot][0..U)
+//   (coalesced) into registers in the sort's layout, stable-sorts by score
+//   descending, ties in first-seen order (Python's stable sorted(),
+//   src/fusion.py:475,488), and writes perm / fused back in place, coalesced.
 #include <cstdlib>
 
 #include "../../include/qppfuse.h"
@@ -303,20 +303,26 @@ template <int BLOCK, int ITEMS, int TB>
 struct JoinCfg {
   static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64;
   static constexpr int kNMax = BLOCK * ITEMS, kTS = 1 << TB, kTB = TB;
+  // LDS: the hash table (tkey, tmask: u32 [TS] each), later overlaid by the
+  // grouped contributions gsc f64 [NMAX], gpr u32 [NMAX] and group starts u16 [NMAX]
+  static constexpr int kGscOff = 0, kGprOff = 8 * kNMax, kGoOff = 12 * kNMax;
+  static constexpr int kSmem = (8 * kTS > 14 * kNMax ? 8 * kTS : 14 * kNMax);
   static_assert(kTS >= kNMax, "hash table must hold every entry");
   static_assert(kNMax <= 65535, "u / group offsets are uint16");
-  static_assert(8 * kTS <= 160 * 1024, "LDS budget");
+  static_assert(kSmem <= 160 * 1024, "LDS budget");
 };
 
 template <class C, int KIND>
 __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   constexpr int BLOCK = C::kBlock, ITEMS = C::kItems, WAVES = C::kWaves;
   constexpr int NMAX = C::kNMax, TS = C::kTS;
-  __shared__ __attribute__((aligned(16))) uint32_t tkey[TS];
-  __shared__ __attribute__((aligned(16))) uint32_t tmask[TS];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
   __shared__ int64_t s_off[kRMax + 1];
+  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax];
   __shared__ int s_cnt[ITEMS * WAVES], s_gof[ITEMS * WAVES];
   __shared__ int s_U, s_status;
+  uint32_t* tkey = (uint32_t*)smem;
+  uint32_t* tmask = (uint32_t*)(smem + 4 * TS);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t q = blockIdx.x;
@@ -332,15 +338,30 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     return;
   }
   const int N = (int)N64;
+  if (tid < R) {
+    const int64_t a = s_off[tid], b = s_off[tid + 1];
+    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
+    // ranx min-max (norm="min-max", the fuse() default); lists are sorted
+    // descending (checked below), so max / min are the end points.
+    double mx = 0.0, mn = 0.0;
+    if (b > a) {
+      mx = ScoreIn<KIND>::load(p.score, a);
+      mn = ScoreIn<KIND>::load(p.score, b - 1);
+    }
+    s_min[tid] = mn;
+    s_den[tid] = mx - mn;
+  }
   for (int i = tid * 4; i < TS; i += BLOCK * 4) {
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
     *(uint4*)&tmask[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   uint32_t dk[ITEMS];
+  double sc[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {  // all loads in flight before the first use
     const int e = j * BLOCK + tid;
     dk[j] = e < N ? p.docid[base + e] : kEmpty;
+    sc[j] = e < N ? ScoreIn<KIND>::load(p.score, base + e) : 0.0;
   }
   __syncthreads();
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
@@ -369,7 +390,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
       const int64_t g = base + e;
       if (g + 1 < s_off[r + 1]) {
         if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
-            ScoreIn<KIND>::load(p.score, g + 1) > ScoreIn<KIND>::load(p.score, g))
+            ScoreIn<KIND>::load(p.score, g + 1) > sc[j])
           status = QF_QSTATUS_UNSORTED;
         if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
           status = QF_QSTATUS_RANKORDER;
@@ -419,7 +440,6 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   const int U = s_U;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const int e = j * BLOCK + tid;
     const bool rep = (repm >> j) & 1u;
     const uint64_t b = ballot(rep);
     uint32_t msk = 0u, pc = 0u;
@@ -432,24 +452,73 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
       const uint32_t u = (uint32_t)s_cnt[j * WAVES + wid] + mbcnt(b);
       const uint32_t go = (uint32_t)s_gof[j * WAVES + wid] + gpre;
       p.union_docid[base + u] = tkey[dk[j]];
-      p.goff[base + u] = (uint16_t)go;
       tkey[dk[j]] = u;                    // slot -> u
       tmask[dk[j]] = go | (msk << 16);    // slot -> group offset | retriever mask
     }
-    (void)e;
   }
   __syncthreads();
+  // ---- every entry's place in its group (retriever order); a document's
+  // first-seen entry opens the group: k == go ---------------------------------
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {  // each entry into its group, retriever order
+  for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
     if (e < N) {
       const uint32_t gm = tmask[dk[j]];
-      const int r = (int)rj[j];
+      const uint32_t r = rj[j];
       const uint32_t k = (gm & 0xFFFFu) + (uint32_t)__popc((gm >> 16) & ((1u << r) - 1u));
-      const int64_t g = base + e;
-      p.gsc[base + k] = ScoreIn<KIND>::load(p.score, g);
-      p.gpr[base + k] = (uint32_t)(g - s_off[r]) | ((uint32_t)r << 16);
+      const uint32_t u = ((repm >> j) & 1u) ? tkey[dk[j]] : 0u;
+      dk[j] = k | (u << 16);
     }
+  }
+  __syncthreads();  // the hash table is dead; its LDS becomes the groups
+  double* gsc = (double*)(smem + C::kGscOff);
+  uint32_t* gpr = (uint32_t*)(smem + C::kGprOff);
+  uint16_t* ugo = (uint16_t*)(smem + C::kGoOff);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int e = j * BLOCK + tid;
+    if (e < N) {
+      const uint32_t k = dk[j] & 0xFFFFu, r = rj[j];
+      gsc[k] = sc[j];
+      gpr[k] = (uint32_t)(base + e - s_off[r]) | (r << 16);
+      if ((repm >> j) & 1u) ugo[dk[j] >> 16] = (uint16_t)k;
+    }
+  }
+  __syncthreads();
+  // ---- fused score of every document, every requested method ------------------
+  const int methods = p.methods, rrf_k = p.rrf_k;
+  int slot[6];
+  for (int t = 0, c = 0; t < 6; ++t) {
+    slot[t] = c;
+    c += (methods >> t) & 1;
+  }
+  for (int u = tid; u < U; u += BLOCK) {
+    const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0;
+    for (int k = gs; k < ge; ++k) {
+      const double s = gsc[k];
+      const uint32_t q2 = gpr[k];
+      const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
+      if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // ranx min-max normalised score
+        const double den = s_den[r];
+        a0 += den > 0.0 ? (s - s_min[r]) / den : 0.0;
+      }
+      if (methods & QF_RRF) a1 += 1.0 / (double)(rrf_k + pos + 1);  // ranx rrf: rank = position
+      if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += s_w[r] * s;  // src/fusion.py:273
+      if (methods & QF_WRRF) {                                      // src/fusion.py:374
+        const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
+        a5 += s_w[r] / (double)(rrf_k + rk);
+      }
+    }
+    const double cnt = (double)(ge - gs);  // CombMNZ: sum x count (src/fusion.py:327)
+    double* out = p.fused + base + u;
+    const int64_t st = p.out_stride;
+    if (methods & QF_COMBSUM) out[slot[0] * st] = a0;
+    if (methods & QF_COMBMNZ) out[slot[1] * st] = a0 * cnt;
+    if (methods & QF_RRF) out[slot[2] * st] = a1;
+    if (methods & QF_WCOMBSUM) out[slot[3] * st] = a2;
+    if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
+    if (methods & QF_WRRF) out[slot[5] * st] = a5;
   }
   if (tid == 0) p.union_count[q] = s_status ? s_status : U;
 }
@@ -473,15 +542,13 @@ template <class C, int KIND>
 __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParams p, int umin) {
   constexpr int ITEMS = C::kItems, WAVES = C::kWaves, UMAX = C::kUMax;
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
-  __shared__ int64_t s_off[kRMax + 1];
-  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax];
   __shared__ int s_flag;
   __shared__ uint32_t s_wtot[16];
   __shared__ unsigned long long s_kmin, s_kmax;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // block -> (query, method slot); blocks b and b+8 share an XCD, so all methods
-  // of query q (slot-major groups of 8 queries) run where its workspace lives.
+  // block -> (query, method slot): slot-major groups of 8 queries, so that the
+  // blocks resident together on an XCD (blockIdx % 8) read adjacent queries.
   const int M = __popc(p.methods);
   const int64_t grp8 = (int64_t)(blockIdx.x >> 3);
   const int64_t q = (grp8 / M) * 8 + (blockIdx.x & 7);
@@ -489,107 +556,29 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   if (q >= p.n_queries) return;
   const int U = p.union_count[q];
   if (U < 0 || U > UMAX || U < umin) return;  // error / other pass
-  int m = 0;
-  for (int t = 0, c = 0; t < 6; ++t)
-    if ((p.methods >> t) & 1) { if (c == ms) m = t; ++c; }
-  const int R = p.R;
   QF_STAMP_INIT();
-  if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
   if (tid == 0) { s_kmin = ~0ull; s_kmax = 0ull; }
   __syncthreads();
-  if (tid < R) {
-    const int64_t a = s_off[tid], b = s_off[tid + 1];
-    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
-    // ranx min-max (norm="min-max", the fuse() default); lists are sorted
-    // descending (checked by join_kernel), so max / min are the end points.
-    double mx = 0.0, mn = 0.0;
-    if (b > a) {
-      mx = ScoreIn<KIND>::load(p.score, a);
-      mn = ScoreIn<KIND>::load(p.score, b - 1);
-    }
-    s_min[tid] = mn;
-    s_den[tid] = mx - mn;
-  }
-  __syncthreads();
-  const int64_t base = s_off[0];
-  const int N = (int)(s_off[R] - base);
+  const int64_t base = p.list_off[q * p.R];
   uint64_t* skey = (uint64_t*)(smem + C::kKeyOff);
   uint16_t* spay = (uint16_t*)(smem + C::kPayOff);
   uint32_t* hist = (uint32_t*)(smem + C::kHistOff);
   SortCtx<ITEMS, WAVES> sx{hist, skey, spay, s_wtot, &s_flag, U,
                            (U + 64 * WAVES - 1) / (64 * WAVES), lane, wid, tid};
-  // ---- fused score of every document: its group, in retriever order ---------
+  // ---- the unsorted fused scores join_kernel left in fused[ms][u] --------------
+  double* io = p.fused + (int64_t)ms * p.out_stride + base;
   uint64_t key[ITEMS];
   uint32_t pay[ITEMS];
   uint64_t kmn = ~0ull, kmx = 0ull;
-  const bool mnz = m == 1 || m == 4;
-  const int rrf_k = p.rrf_k;
-  // group bounds: document i's group ends where i+1's starts (next lane), the
-  // last document's at N
-  int gsr[ITEMS], ger[ITEMS];
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const int i = (wid * sx.rows + j) * 64 + lane;
-    gsr[j] = (j < sx.rows && i < U) ? (int)p.goff[base + i] : N;
-  }
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const int i = (wid * sx.rows + j) * 64 + lane;
-    int nx = __shfl_down(gsr[j], 1, 64);
-    if (lane == 63 && j < sx.rows && i + 1 < U) nx = (int)p.goff[base + i + 1];
-    ger[j] = (i + 1 < U) ? nx : N;
-  }
-  constexpr int CAP = 6;  // contributions per document prefetched as one batch
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * sx.rows + j) * 64 + lane;
     key[j] = ~0ull;
     pay[j] = (uint32_t)i;
     if (j < sx.rows && i < U) {
-      const int gs = gsr[j], ge = ger[j];
-      double sc[CAP];
-      uint32_t pr[CAP];
-#pragma unroll
-      for (int t = 0; t < CAP; ++t) {
-        sc[t] = 0.0;
-        pr[t] = 0u;
-        if (gs + t < ge) {
-          sc[t] = p.gsc[base + gs + t];
-          pr[t] = p.gpr[base + gs + t];
-        }
-      }
-      double acc = 0.0;
-      for (int k = gs, t = 0; k < ge; ++k, ++t) {
-        double s;
-        uint32_t q2;
-        if (t < CAP) {
-          s = sc[0];
-          q2 = pr[0];
-#pragma unroll
-          for (int tt = 1; tt < CAP; ++tt)
-            if (tt == t) { s = sc[tt]; q2 = pr[tt]; }
-        } else {
-          s = p.gsc[base + k];
-          q2 = p.gpr[base + k];
-        }
-        const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
-        double c;
-        if (m <= 1) {  // ranx min-max normalised score
-          const double den = s_den[r];
-          c = den > 0.0 ? (s - s_min[r]) / den : 0.0;
-        } else if (m == 2) {  // ranx rrf: rank = position
-          c = 1.0 / (double)(rrf_k + pos + 1);
-        } else if (m <= 4) {  // src/fusion.py:273
-          c = s_w[r] * s;
-        } else {  // src/fusion.py:374
-          const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
-          c = s_w[r] / (double)(rrf_k + rk);
-        }
-        acc += c;
-      }
-      if (mnz) acc = acc * (double)(ge - gs);  // CombMNZ: sum x count (src/fusion.py:327)
-      if (acc == 0.0 && __double_as_longlong(acc) < 0) pay[j] |= kNegZero;
-      key[j] = ~f64_asc_key(acc);  // ascending sort on ~key == descending score
+      const double v = io[i];
+      if (v == 0.0 && __double_as_longlong(v) < 0) pay[j] |= kNegZero;
+      key[j] = ~f64_asc_key(v);  // ascending sort on ~key == descending score
       kmn = min(kmn, key[j]);
       kmx = max(kmx, key[j]);
     }
@@ -599,8 +588,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   QF_STAMP(0);
   sort_desc(sx, key, pay, (uint64_t)s_kmin, (uint64_t)s_kmax);
   QF_STAMP(1);
-  write_out(sx, key, pay, p.perm + (int64_t)ms * p.out_stride + base,
-            p.fused + (int64_t)ms * p.out_stride + base);
+  write_out(sx, key, pay, p.perm + (int64_t)ms * p.out_stride + base, io);
   QF_STAMP(2);
 }
 
@@ -613,10 +601,6 @@ using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
 
 int fuse_max_entries() { return JoinL::kNMax; }
-
-size_t fuse_workspace_bytes(int64_t n_entries) {
-  return (size_t)(n_entries > 0 ? n_entries : 1) * (8 + 4 + 2) + 256;
-}
 
 template <class J>
 static void launch_join(const FuseParams& p, int kind, hipStream_t st) {

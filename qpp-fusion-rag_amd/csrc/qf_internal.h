@@ -21,15 +21,9 @@ struct FuseParams {
   uint16_t* perm;
   double* fused;
   int64_t out_stride;
-  // workspace, all [E] and query-relative: group offset of document u; then, per
-  // contribution in group order (documents by u, retrievers ascending inside):
-  uint16_t* goff;  // group start of document u
-  uint32_t* gpr;   // position in its list | retriever << 16
-  double* gsc;     // score (as the methods read it: micro-units already / 1e6)
 };
 
 int fuse_max_entries();
-size_t fuse_workspace_bytes(int64_t n_entries);
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);
 hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t Q, int32_t R,
                           int32_t top_k, const int32_t* nt, const double* tf, double* out,

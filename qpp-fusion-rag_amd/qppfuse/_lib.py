@@ -35,8 +35,7 @@ SIGNATURES = {
     "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
-                          _vp, _vp, _vp, _vp, _i64, _vp, C.c_size_t, _vp]),
-    "qf_fuse_workspace_bytes": (C.c_size_t, [_i64]),
+                          _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
 }
 

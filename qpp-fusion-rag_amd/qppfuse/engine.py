@@ -52,24 +52,22 @@ def method_names(mask: int):
 
 @dataclass
 class FuseOut:
-    """Device outputs (and workspace) of qf_fuse for one launch shape."""
+    """Device outputs of qf_fuse for one launch shape."""
     union_docid: torch.Tensor  # int32 view of uint32 [E]
     union_count: torch.Tensor  # int32 [Q]
     perm: torch.Tensor         # int16 view of uint16 [M, E]
     fused: torch.Tensor        # float64 [M, E]
     methods: list
-    workspace: torch.Tensor = None  # uint8 [qf_fuse_workspace_bytes(E)]
 
 
 def alloc_fuse_out(n_queries: int, n_entries: int, mask: int, device) -> FuseOut:
     M = bin(mask).count("1")
     E = max(int(n_entries), 1)
-    ws = int(_lib.lib().qf_fuse_workspace_bytes(E))
     return FuseOut(torch.empty(E, dtype=torch.int32, device=device),
                    torch.empty(max(n_queries, 1), dtype=torch.int32, device=device),
                    torch.empty((M, E), dtype=torch.int16, device=device),
                    torch.empty((M, E), dtype=torch.float64, device=device),
-                   method_names(mask), torch.empty(ws, dtype=torch.uint8, device=device))
+                   method_names(mask))
 
 
 def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_retrievers: int,
@@ -95,7 +93,7 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
     _lib.call("qf_fuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
               _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
               _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused), out.fused.shape[1],
-              _ptr(out.workspace), out.workspace.numel(), _stream())
+              _stream())
     return out
 
 

@@ -39,7 +39,7 @@ def test_version_and_limits():
 def test_argument_validation_without_device():
     """Validation happens before any HIP call: bad arguments fail with EINVAL."""
     from qppfuse import _lib
-    tail = (None, None, None, None, 0, None, 0, None)
+    tail = (None, None, None, None, 0, None)
     with pytest.raises(ValueError, match="n_retrievers"):
         _lib.call("qf_fuse", 1, 0, None, None, None, 0, None, None, 1, 60, 10, *tail)
     with pytest.raises(ValueError, match="method mask"):
@@ -49,9 +49,8 @@ def test_argument_validation_without_device():
     with pytest.raises(_lib.QPPFuseError, match="exceed"):
         _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, _lib.RRF, 60, 10**6, *tail)
     with pytest.raises(ValueError, match="null buffer"):
-        _lib.call("qf_fuse", 1, 2, 8, 8, 8, 0, None, None, _lib.RRF, 60, 10, 8, 8, 8, 8, 16,
-                  None, 0, None)
-    assert _lib.lib().qf_fuse_workspace_bytes(1000) >= 4000
+        _lib.call("qf_fuse", 1, 2, 8, 8, 8, 0, None, None, _lib.RRF, 60, 10, 8, 8, 8, None, 16,
+                  None)
     with pytest.raises(ValueError, match="qpp_index"):
         _lib.call("qf_qpp_normalize", 1, 1, 1, 1, 1, 1, 13, None, None, None, None)
 
