@@ -83,37 +83,50 @@ __device__ __forceinline__ void block_min_max(uint64_t kmn, uint64_t kmx,
   }
 }
 
+// ---- the per-(query, method) sort -------------------------------------------
+//
+// Items are 64-bit words, held in registers wave-major (item i = (wid*rows +
+// j)*64 + lane) and scattered through LDS between passes:
+//   bits 32..55  window key: the kWindow most significant bits of (key - kmin),
+//                key = ~orderable(score) (ascending key == descending score)
+//   bits  0..15  u, the document's first-seen index
+// The full key of an item is re-derived from fused[u] (the unsorted scores in
+// HBM/L2), which only the rare fix-up and the fallback need.
 template <int ITEMS, int WAVES>
 struct SortCtx {
-  uint32_t* hist;    // [256][WAVES]
-  uint64_t* skey;    // [UMAX]
-  uint16_t* spay;    // [UMAX]
+  uint32_t* hist;    // [WAVES][256]
+  uint64_t* sitem;   // [UMAX]
   uint32_t* wtot;    // [WAVES] scan carries
-  int* flag;         // fix-up status
+  int* flag;         // [2]: fix-up status, listed runs
+  const double* io;  // fused[slot] of the query: unsorted scores by u
+  uint64_t kmin;
   int U, rows, lane, wid, tid;
 };
 
-// One stable counting-scatter pass on an 8-bit digit digit(key).  Items are held
-// in registers, wave-major: item i = (wid*rows + j)*64 + lane.  Within a wave a
-// row's items are ranked by a ballot match of their digits; the row's leader
-// lane claims a run of slots with one LDS atomicAdd (LDS ops of a wave execute
-// in program order, so rows stay ordered without a read->write chain); the
-// (digit, wave) offsets are one block-wide exclusive scan of the [digit][wave]
-// counters.  Leaves the scattered sequence in skey/spay; `readback` reloads
-// the registers.
+constexpr uint32_t kUMask = 0xFFFFu;
+
+template <int ITEMS, int WAVES>
+__device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, uint64_t item) {
+  return ~f64_asc_key(sx.io[item & kUMask]);
+}
+
+// One stable counting-scatter pass on an 8-bit digit of the items.  Within a
+// wave a row's items are ranked by a ballot match of their digits; the row's
+// leader lane claims a run of slots with one LDS atomicAdd (LDS ops of a wave
+// execute in program order, so rows stay ordered); the (wave, digit) offsets
+// are one block-wide exclusive scan in [digit][wave] order.  Leaves the
+// scattered sequence in sitem; `readback` reloads the registers.
 template <int ITEMS, int WAVES, class Digit>
 __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
-                                              uint64_t (&key)[ITEMS], uint32_t (&pay)[ITEMS],
-                                              Digit digit, bool readback) {
-  static_assert(WAVES % 4 == 0 || WAVES == 1 || WAVES == 2, "4 counters per thread");
+                                              uint64_t (&item)[ITEMS], Digit digit,
+                                              bool readback) {
   const int lane = sx.lane, wid = sx.wid;
   int rp = sx.rows;
   asm volatile("" : "+s"(rp));
-  // hist is [digit][wave]: in that flat order an exclusive scan IS the scatter
-  // offset of (wave, digit) — digits ascending, waves ascending within a digit.
+  // hist is [wave][digit] (a wave's leaders hit distinct banks)
   uint32_t* hist = sx.hist;
   QF_STAMP_INIT();
-  for (int k = lane; k < 256; k += 64) hist[k * WAVES + wid] = 0u;
+  for (int k = lane; k < 256; k += 64) hist[wid * 256 + k] = 0u;
   uint32_t rank_in[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -121,18 +134,21 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
     if (j < rp) {  // wave-uniform
       const int i = (wid * rp + j) * 64 + lane;
       const bool valid = i < sx.U;
-      const uint32_t d = digit(key[j]);
-      uint64_t peers = ballot(valid);
+      const uint32_t d = valid ? digit(item[j]) : 0u;
+      // peers = the valid lanes whose digit equals mine: no bit may mismatch
+      uint64_t mis = ~ballot(valid);
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
-        const uint64_t bb = ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bb : ~bb;
+        const int32_t m = ((int32_t)(d << (31 - b))) >> 31;  // 0 / -1
+        const uint64_t bb = ballot(m != 0);
+        mis |= bb ^ (uint64_t)(int64_t)m;
       }
+      const uint64_t peers = ~mis;
       const uint32_t before = mbcnt(peers);
       const int leader = __ffsll((unsigned long long)peers) - 1;
       uint32_t old = 0u;
-      if (valid && before == 0) old = atomicAdd(&hist[d * WAVES + wid], (uint32_t)__popcll(peers));
-      old = (uint32_t)__shfl((int)old, leader < 0 ? 0 : leader, 64);
+      if (valid && before == 0) old = atomicAdd(&hist[wid * 256 + d], (uint32_t)__popcll(peers));
+      old = (uint32_t)__builtin_amdgcn_ds_bpermute((leader & 63) << 2, (int)old);
       rank_in[j] = old + before;
     }
   }
@@ -141,19 +157,26 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   QF_STAMP(9);
   // block-wide exclusive scan of the 256*WAVES counters, 4 per thread
   {
-    constexpr int PER = 256 * WAVES / (64 * WAVES);  // == 4
-    static_assert(PER == 4, "");
-    uint4 v = *(uint4*)&hist[4 * sx.tid];
-    const uint32_t t = v.x + v.y + v.z + v.w;
+    uint32_t v[4], t = 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 4 * sx.tid + c;
+      v[c] = hist[(f % WAVES) * 256 + f / WAVES];
+      t += v[c];
+    }
     const uint32_t incl = wave_incl_scan_dpp(t);
     if (lane == 63) sx.wtot[wid] = incl;
     __syncthreads();
-    uint32_t pre = 0u;
+    uint32_t ex = incl - t;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w)
-      if (w < wid) pre += sx.wtot[w];
-    const uint32_t ex = pre + incl - t;
-    *(uint4*)&hist[4 * sx.tid] = make_uint4(ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z);
+      if (w < wid) ex += sx.wtot[w];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 4 * sx.tid + c;
+      hist[(f % WAVES) * 256 + f / WAVES] = ex;
+      ex += v[c];
+    }
   }
   __syncthreads();
   QF_STAMP(10);
@@ -161,11 +184,8 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rp + j) * 64 + lane;
-    if (j < rp && i < sx.U) {
-      const uint32_t dst = hist[digit(key[j]) * WAVES + wid] + rank_in[j];
-      sx.skey[dst] = key[j];
-      sx.spay[dst] = (uint16_t)pay[j];
-    }
+    if (j < rp && i < sx.U)
+      sx.sitem[hist[wid * 256 + digit(item[j])] + rank_in[j]] = item[j];
   }
   QF_STAMP(11);
   __syncthreads();
@@ -175,126 +195,165 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const int i = (wid * rp + j) * 64 + lane;
-      if (j < rp && i < sx.U) {
-        key[j] = sx.skey[i];
-        pay[j] = sx.spay[i];
-      }
+      if (j < rp && i < sx.U) item[j] = sx.sitem[i];
     }
   }
   QF_STAMP(13);
 }
 
-// digit(k) = ((k - kmin) >> sh) & 0xFF.
-struct Digit {
-  uint64_t base;
-  int sh;
-  __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
-    return (uint32_t)((k - base) >> sh) & 0xFFu;
-  }
-};
+// Lane l gets lane l-1's value (DPP wave_shr:1; lane 0 gets its own back).
+__device__ __forceinline__ uint32_t wave_up1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xf, 0xf, false);
+}
 
-// Stable sort of the items by key ascending (keys are ~orderable(score): scores
-// descending; ties keep input = first-seen order).  kmin / kmax: extreme keys.
-//  1. LSD counting passes on the kWindow most significant bits of (key - kmin);
-//  2. runs of items that agree on those 32 bits (contiguous, first-seen order,
-//     almost always of length 1 or 2) are put in full-key order by a stable
-//     insertion sort run by the thread at the run's start.
-// A run longer than kRunMax sends the block on with LSD passes over every bit
-// from bit 0: started from the order of step 1 (equal keys still first-seen)
-// they give the same stable result.
-constexpr int kRunMax = 48;
+// Stable sort of the items by full key ascending (scores descending; ties keep
+// input = first-seen order), given the window width nb = min(hb, kWindow):
+//  1. LSD counting passes over the window key (bits 32.. of the item);
+//  2. if the window dropped low bits (lo > 0): inside a run of items with equal
+//     window keys an item is "bad" when its predecessor has a larger full key.
+//     No bad item anywhere (the usual case; long runs of equal keys are never
+//     bad): sorted.  Otherwise the run of each first bad item is put in
+//     full-key order by a stable insertion sort run by one thread.
+// A run longer than kRunMax that needs fixing sends the block on with LSD passes
+// over every bit of (full key - kmin) from bit 0: started from the order of
+// step 1 (equal keys still first-seen) they give the same stable result.
+constexpr int kRunMax = 64;
 constexpr int kWindow = 24;  // bits sorted by LSD passes (3 passes of 8)
 
 template <int ITEMS, int WAVES>
-__device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&key)[ITEMS],
-                          uint32_t (&pay)[ITEMS], uint64_t kmin, uint64_t kmax) {
-  if (kmin >= kmax) return;  // all keys equal (or no items): first-seen order stands
-  const int hb = 64 - __clzll((long long)(kmax - kmin));
-  const int lo = hb > kWindow ? hb - kWindow : 0;
-  int sh = lo;
+__device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEMS], int hb,
+                          int lo) {
+  const int nb = hb - lo;
+  int sh = 0;
   bool fallback = false;
+  if (sx.tid == 0) { sx.flag[0] = 0; sx.flag[1] = 0; }  // ordered by count_scatter's barriers
+  constexpr int kListCap = 256 * WAVES;                 // run starts, kept in hist
 #pragma unroll 1
   while (true) {
-    count_scatter(sx, key, pay, Digit{kmin, sh}, true);
+    const int s0 = sh;
+    const bool fb = fallback;
+    count_scatter(sx, item, [&](uint64_t it) -> uint32_t {
+      if (fb) return (uint32_t)((full_key(sx, it) - sx.kmin) >> s0) & 0xFFu;
+      return (uint32_t)(it >> (32 + s0)) & 0xFFu;
+    }, true);
     sh += 8;
-    if (sh < hb) continue;
+    if (sh < (fallback ? hb : nb)) continue;
     if (fallback || lo == 0) return;
-    // -- fix up runs that agree on the window ------------------------------------
-    // count_scatter left the sorted sequence in skey/spay.
-    if (sx.tid == 0) *sx.flag = 0;
-    __syncthreads();
-    bool moved = false;
-    for (int i = sx.tid; i < sx.U; i += WAVES * 64) {
-      const uint64_t hk = (sx.skey[i] - kmin) >> lo;
-      if (i > 0 && ((sx.skey[i - 1] - kmin) >> lo) == hk) continue;  // not a run start
-      if (i + 1 >= sx.U || ((sx.skey[i + 1] - kmin) >> lo) != hk) continue;  // length 1
-      int L = 2;
-      while (i + L < sx.U && ((sx.skey[i + L] - kmin) >> lo) == hk && L <= kRunMax) ++L;
-      if (L > kRunMax) { atomicOr(sx.flag, 1); continue; }
-      for (int a = i + 1; a < i + L; ++a) {  // stable insertion sort on the full key
-        const uint64_t k = sx.skey[a];
-        const uint16_t v = sx.spay[a];
-        int b = a - 1;
-        while (b >= i && sx.skey[b] > k) {
-          sx.skey[b + 1] = sx.skey[b];
-          sx.spay[b + 1] = sx.spay[b];
-          --b;
-        }
-        if (b + 1 != a) {
-          sx.skey[b + 1] = k;
-          sx.spay[b + 1] = v;
-          moved = true;
-        }
-      }
-    }
-    if (moved) atomicOr(sx.flag, 2);
-    __syncthreads();
-    const int f = *sx.flag;  // block-uniform
-    if (f & 1) {             // a run too long: finish with full LSD passes
-      fallback = true;
-      sh = 0;
-      continue;              // registers still hold the step-1 order
-    }
-    if (f & 2) {
+    // -- A: find the runs to fix (read-only) ----------------------------------------
+    {
       int rp = sx.rows;
       asm volatile("" : "+s"(rp));
+      bool any = false;
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const int i = (sx.wid * rp + j) * 64 + sx.lane;
-        if (j < rp && i < sx.U) {
-          key[j] = sx.skey[i];
-          pay[j] = sx.spay[i];
+        const uint32_t wk = (uint32_t)(item[j] >> 32);
+        uint32_t wp = wave_up1(wk);
+        if (j < rp && i < sx.U && i > 0) {
+          uint64_t ip = 0;
+          if (sx.lane == 0) {
+            ip = sx.sitem[i - 1];
+            wp = (uint32_t)(ip >> 32);
+          }
+          if (wp == wk) {  // same window as the predecessor: compare full keys
+            if (sx.lane != 0) ip = sx.sitem[i - 1];
+            const uint64_t k = full_key(sx, item[j]), kp = full_key(sx, ip);
+            if (kp > k) {  // bad: walk back to the run start
+              any = true;
+              int st = i - 1;
+              uint64_t kc = kp;
+              bool first = true;
+              while (st > 0) {
+                const uint64_t iq = sx.sitem[st - 1];
+                if ((uint32_t)(iq >> 32) != wk) break;
+                const uint64_t kq = full_key(sx, iq);
+                if (kq > kc) { first = false; break; }  // an earlier bad item owns the run
+                kc = kq;
+                --st;
+                if (i - st > kRunMax) break;
+              }
+              if (first) {
+                if (i - st > kRunMax) {
+                  atomicOr(&sx.flag[0], 1);
+                } else {
+                  const int slot = atomicAdd(&sx.flag[1], 1);
+                  if (slot < kListCap) sx.hist[slot] = (uint32_t)st;
+                  else atomicOr(&sx.flag[0], 1);
+                }
+              }
+            }
+          }
         }
       }
+      if (any) atomicOr(&sx.flag[0], 2);
+    }
+    __syncthreads();
+    const int f = sx.flag[0];  // block-uniform
+    if (f == 0) return;        // no bad item: already in full-key order
+    if (!(f & 1)) {
+      // -- B: stable insertion sort of each listed run on the full key -------------
+      const int nr = sx.flag[1];
+      for (int t = sx.tid; t < nr; t += WAVES * 64) {
+        const int i = (int)sx.hist[t];
+        const uint32_t wk = (uint32_t)(sx.sitem[i] >> 32);
+        int L = 1;
+        while (i + L < sx.U && (uint32_t)(sx.sitem[i + L] >> 32) == wk && L <= kRunMax) ++L;
+        if (L > kRunMax) { atomicOr(&sx.flag[0], 1); continue; }
+        for (int a = i + 1; a < i + L; ++a) {
+          const uint64_t ia = sx.sitem[a];
+          const uint64_t ka = full_key(sx, ia);
+          int b = a - 1;
+          while (b >= i && full_key(sx, sx.sitem[b]) > ka) {
+            sx.sitem[b + 1] = sx.sitem[b];
+            --b;
+          }
+          if (b + 1 != a) sx.sitem[b + 1] = ia;
+        }
+      }
+      __syncthreads();
+    }
+    if (sx.flag[0] & 1) {  // a run too long: finish with full LSD passes
+      fallback = true;
+      sh = 0;
+      continue;            // registers still hold the step-1 order
+    }
+    int rp = sx.rows;
+    asm volatile("" : "+s"(rp));
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int i = (sx.wid * rp + j) * 64 + sx.lane;
+      if (j < rp && i < sx.U) item[j] = sx.sitem[i];
     }
     return;
   }
 }
 
-// Sorted items -> perm (u of rank i) and the fused score, coalesced.  Payload
-// bit 15 marks a -0.0 score (the key folds -0.0 onto +0.0 so they tie, as in
-// Python's sort; the value written keeps its sign, as "%.6f" prints it).
-constexpr uint32_t kNegZero = 0x8000u;
-
+// Sorted items -> perm (u of rank i) and the fused score (read back from fused[u]
+// with its sign, -0.0 included, before the block overwrites fused in place).
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
-                                          const uint64_t (&key)[ITEMS],
-                                          const uint32_t (&pay)[ITEMS], uint16_t* operm,
-                                          double* ofused) {
+                                          const uint64_t (&item)[ITEMS], uint16_t* operm,
+                                          double* io) {
   int ro = sx.rows;
   asm volatile("" : "+s"(ro));
+  double v[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = (sx.wid * ro + j) * 64 + sx.lane;
+    v[j] = (j < ro && i < sx.U) ? io[item[j] & kUMask] : 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) asm volatile("" ::"v"(v[j]));  // loads done before the barrier
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (sx.wid * ro + j) * 64 + sx.lane;
     if (j < ro && i < sx.U) {
-      double v = f64_from_asc_key(~key[j]);
-      if (v == 0.0 && (pay[j] & kNegZero)) v = -0.0;
-      operm[i] = (uint16_t)(pay[j] & ~kNegZero);
-      ofused[i] = v;
+      operm[i] = (uint16_t)(item[j] & kUMask);
+      io[i] = v[j];
     }
   }
 }
-
 
 // ============================================================================
 // join_kernel
@@ -530,11 +589,10 @@ template <int BLOCK, int ITEMS, int MINW>
 struct SortCfg {
   static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64, kMinWaves = MINW;
   static constexpr int kUMax = BLOCK * ITEMS;
-  static constexpr int kKeyOff = 0;                                  // u64 [UMAX]
-  static constexpr int kPayOff = 8 * kUMax;                          // u16 [UMAX]
-  static constexpr int kHistOff = (kPayOff + 2 * kUMax + 15) & ~15;  // u32 [W][256]
+  static constexpr int kItemOff = 0;            // u64 [UMAX]
+  static constexpr int kHistOff = 8 * kUMax;    // u32 [W][256]
   static constexpr int kSmem = kHistOff + 4 * 256 * kWaves;
-  static_assert(kUMax < (int)kNegZero, "payload bit 15 is the -0.0 flag");
+  static_assert(kUMax <= (int)kUMask + 1, "u is 16 bits of the item");
   static_assert(kSmem <= 160 * 1024, "LDS budget");
 };
 
@@ -542,7 +600,7 @@ template <class C, int KIND>
 __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParams p, int umin) {
   constexpr int ITEMS = C::kItems, WAVES = C::kWaves, UMAX = C::kUMax;
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
-  __shared__ int s_flag;
+  __shared__ int s_flag[2];
   __shared__ uint32_t s_wtot[16];
   __shared__ unsigned long long s_kmin, s_kmax;
 
@@ -560,35 +618,38 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   if (tid == 0) { s_kmin = ~0ull; s_kmax = 0ull; }
   __syncthreads();
   const int64_t base = p.list_off[q * p.R];
-  uint64_t* skey = (uint64_t*)(smem + C::kKeyOff);
-  uint16_t* spay = (uint16_t*)(smem + C::kPayOff);
-  uint32_t* hist = (uint32_t*)(smem + C::kHistOff);
-  SortCtx<ITEMS, WAVES> sx{hist, skey, spay, s_wtot, &s_flag, U,
-                           (U + 64 * WAVES - 1) / (64 * WAVES), lane, wid, tid};
-  // ---- the unsorted fused scores join_kernel left in fused[ms][u] --------------
-  double* io = p.fused + (int64_t)ms * p.out_stride + base;
-  uint64_t key[ITEMS];
-  uint32_t pay[ITEMS];
+  double* io = p.fused + (int64_t)ms * p.out_stride + base;  // unsorted fused[ms][u]
+  const int rows = (U + 64 * WAVES - 1) / (64 * WAVES);
+  // ---- full keys of the join kernel's unsorted scores, their range -------------
+  uint64_t item[ITEMS];
   uint64_t kmn = ~0ull, kmx = 0ull;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const int i = (wid * sx.rows + j) * 64 + lane;
-    key[j] = ~0ull;
-    pay[j] = (uint32_t)i;
-    if (j < sx.rows && i < U) {
-      const double v = io[i];
-      if (v == 0.0 && __double_as_longlong(v) < 0) pay[j] |= kNegZero;
-      key[j] = ~f64_asc_key(v);  // ascending sort on ~key == descending score
-      kmn = min(kmn, key[j]);
-      kmx = max(kmx, key[j]);
+    const int i = (wid * rows + j) * 64 + lane;
+    item[j] = 0;
+    if (j < rows && i < U) {
+      item[j] = ~f64_asc_key(io[i]);  // ascending sort on ~key == descending score
+      kmn = min(kmn, item[j]);
+      kmx = max(kmx, item[j]);
     }
   }
   block_min_max(kmn, kmx, &s_kmin, &s_kmax, lane);
   __syncthreads();
+  const uint64_t kmin = s_kmin, kmax = s_kmax;
+  SortCtx<ITEMS, WAVES> sx{(uint32_t*)(smem + C::kHistOff), (uint64_t*)(smem + C::kItemOff),
+                           s_wtot, s_flag, io, kmin, U, rows, lane, wid, tid};
+  // ---- items: window key | u ----------------------------------------------------
+  const int hb = kmax > kmin ? 64 - __clzll((long long)(kmax - kmin)) : 0;
+  const int lo = hb > kWindow ? hb - kWindow : 0;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = (wid * rows + j) * 64 + lane;
+    item[j] = (((item[j] - kmin) >> lo) << 32) | (uint32_t)i;
+  }
   QF_STAMP(0);
-  sort_desc(sx, key, pay, (uint64_t)s_kmin, (uint64_t)s_kmax);
+  if (hb > 0) sort_desc(sx, item, hb, lo);  // hb == 0: all keys equal, first-seen order
   QF_STAMP(1);
-  write_out(sx, key, pay, p.perm + (int64_t)ms * p.out_stride + base, io);
+  write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base, io);
   QF_STAMP(2);
 }
 

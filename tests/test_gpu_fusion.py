@@ -187,3 +187,43 @@ def test_too_big_and_unsorted_are_reported(gpu):
     off, doc, sc, doff, ddoc, dsc = _csr([([1, 2, 1], [0.9, 0.5, 0.1]), ([4], [1.0])], gpu)
     out = engine.fuse(doff, ddoc, dsc, 2, ["combsum"], max_entries=4)
     assert out.union_count.cpu().numpy()[0] == -5  # duplicate docid inside one list
+
+
+def _sort_case(kind, n, rng):
+    if kind == "wide_then_clustered":  # coarse window -> long equal-prefix runs -> fallback
+        s = 1.0 + rng.integers(0, 1 << 20, n) * 2.0 ** -52
+        s[: n // 50] = rng.choice([1e300, -1e300, 7.0, -3.0], n // 50)
+    elif kind == "pairs":  # many short runs that only the low bits order
+        base = rng.uniform(0, 1, n // 2)
+        s = np.concatenate([base, base + rng.integers(1, 1 << 12, n // 2) * 2.0 ** -50])[:n]
+        s = np.resize(s, n)
+    elif kind == "zeros_and_ties":
+        s = rng.choice([0.0, -0.0, 1.0, 0.5, 0.5 + 2.0 ** -40, -2.0 ** -1074], n)
+    else:  # uniform
+        s = rng.standard_normal(n) * 10.0 ** rng.integers(-30, 30, n)
+    rng.shuffle(s)
+    return s
+
+
+@pytest.mark.parametrize("n", [700, 2900, 7000])
+@pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform"])
+def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
+    """One retriever, W-CombSUM with weight 1: the fused scores are the inputs, so the
+    kernel's sort (LSD window + run fix-up + full-LSD fallback) is checked against a
+    stable descending sort with -0.0 == +0.0 (Python's sorted(), src/fusion.py:488)."""
+    from qppfuse import engine
+    rng = np.random.default_rng(hash((kind, n)) & 0xFFFF)
+    s = _sort_case(kind, n, rng)
+    doc = np.arange(n, dtype=np.uint32) * 7 + 3
+    off = np.array([0, n], np.int64)
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    w = torch.ones(1, dtype=torch.float64, device=gpu)
+    out = engine.fuse(t(off), t(doc.view(np.int32)), t(s), 1, ["wcombsum"], weights=w,
+                      max_entries=n)
+    assert int(out.union_count[0]) == n
+    perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
+    fused = out.fused.cpu().numpy()[0][:n]
+    want = np.argsort(-s, kind="stable")
+    np.testing.assert_array_equal(perm, want)
+    # defaultdict(float) accumulation: 0.0 + 1.0 * s, so -0.0 comes out as +0.0
+    assert fused.tobytes() == (0.0 + s[want]).tobytes()

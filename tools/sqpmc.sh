@@ -1,0 +1,8 @@
+#!/bin/bash
+# SQ counters of the fusion kernels over tools/microbench.py (two counter passes,
+# kernel trace only — never combined with sys/runtime tracing).
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+OUT=${1:-gpurun_out/sq}
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU --kernel-trace --output-format csv -d $OUT/p1 -o run -- python3 tools/microbench.py > $OUT/p1.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/p2 -o run -- python3 tools/microbench.py > $OUT/p2.log 2>&1
