@@ -116,13 +116,16 @@ __device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, ui
 // execute in program order, so rows stay ordered); the (wave, digit) offsets
 // are one block-wide exclusive scan in [digit][wave] order.  Leaves the
 // scattered sequence in sitem; `readback` reloads the registers.
-template <int ITEMS, int WAVES, class Digit>
+template <int ITEMS, int WAVES>
 __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
-                                              uint64_t (&item)[ITEMS], Digit digit,
-                                              bool readback) {
+                                              uint64_t (&item)[ITEMS], int sh, bool readback) {
   const int lane = sx.lane, wid = sx.wid;
   int rp = sx.rows;
   asm volatile("" : "+s"(rp));
+  // digit = bits sh..sh+7 of the window key (item bits 32..55)
+  auto digit = [sh](uint64_t it) -> uint32_t {
+    return __builtin_amdgcn_ubfe((uint32_t)(it >> 32), (uint32_t)sh, 8u);
+  };
   // hist is [wave][digit] (a wave's leaders hit distinct banks)
   uint32_t* hist = sx.hist;
   QF_STAMP_INIT();
@@ -134,21 +137,28 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
     if (j < rp) {  // wave-uniform
       const int i = (wid * rp + j) * 64 + lane;
       const bool valid = i < sx.U;
-      const uint32_t d = valid ? digit(item[j]) : 0u;
-      // peers = the valid lanes whose digit equals mine: no bit may mismatch
-      uint64_t mis = ~ballot(valid);
+      const uint32_t d = digit(item[j]);
+      // peers = the valid lanes whose digit equals mine: no bit may mismatch.
+      // A lane's own bit b as a 0 / -1 mask m: mismatching lanes = ballot ^ m.
+      const uint64_t vb = ballot(valid);
+      uint32_t mlo = ~(uint32_t)vb, mhi = ~(uint32_t)(vb >> 32);
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
-        const int32_t m = ((int32_t)(d << (31 - b))) >> 31;  // 0 / -1
-        const uint64_t bb = ballot(m != 0);
-        mis |= bb ^ (uint64_t)(int64_t)m;
+        uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)d, (uint32_t)b, 1u);
+        asm("" : "+v"(m));  // keep the ballot on m (one v_cmp), not a re-derived bit test
+        const uint64_t bb = ballot(m != 0u);
+        mlo |= (uint32_t)bb ^ m;
+        mhi |= (uint32_t)(bb >> 32) ^ m;
       }
-      const uint64_t peers = ~mis;
-      const uint32_t before = mbcnt(peers);
-      const int leader = __ffsll((unsigned long long)peers) - 1;
+      const uint32_t plo = ~mlo, phi = ~mhi;
+      const uint32_t before = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
+      // lowest peer (v_ffbl gives -1 on 0: an empty peer set — invalid lane — reads lane 63)
+      const uint32_t llo = (uint32_t)__builtin_ctz(plo | (plo == 0u ? 0x80000000u : 0u));
+      const uint32_t leader = plo ? llo : 32u + (uint32_t)__builtin_ctz(phi | 0x80000000u);
       uint32_t old = 0u;
-      if (valid && before == 0) old = atomicAdd(&hist[wid * 256 + d], (uint32_t)__popcll(peers));
-      old = (uint32_t)__builtin_amdgcn_ds_bpermute((leader & 63) << 2, (int)old);
+      if (valid && before == 0)
+        old = atomicAdd(&hist[wid * 256 + d], (uint32_t)(__popc(plo) + __popc(phi)));
+      old = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)old);
       rank_in[j] = old + before;
     }
   }
@@ -230,12 +240,17 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEM
   constexpr int kListCap = 256 * WAVES;                 // run starts, kept in hist
 #pragma unroll 1
   while (true) {
-    const int s0 = sh;
-    const bool fb = fallback;
-    count_scatter(sx, item, [&](uint64_t it) -> uint32_t {
-      if (fb) return (uint32_t)((full_key(sx, it) - sx.kmin) >> s0) & 0xFFu;
-      return (uint32_t)(it >> (32 + s0)) & 0xFFu;
-    }, true);
+    if (fallback) {  // this pass's digit of the full key becomes the window key
+      int rp = sx.rows;
+      asm volatile("" : "+s"(rp));
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const int i = (sx.wid * rp + j) * 64 + sx.lane;
+        if (j < rp && i < sx.U)
+          item[j] = ((((full_key(sx, item[j]) - sx.kmin) >> sh) & 0xFFu) << 32) | (item[j] & kUMask);
+      }
+    }
+    count_scatter(sx, item, fallback ? 0 : sh, true);
     sh += 8;
     if (sh < (fallback ? hb : nb)) continue;
     if (fallback || lo == 0) return;
@@ -613,11 +628,11 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   const int ms = (int)(grp8 % M);
   if (q >= p.n_queries) return;
   const int U = p.union_count[q];
+  const int64_t base = p.list_off[q * p.R];  // both loads in flight together
   if (U < 0 || U > UMAX || U < umin) return;  // error / other pass
   QF_STAMP_INIT();
   if (tid == 0) { s_kmin = ~0ull; s_kmax = 0ull; }
   __syncthreads();
-  const int64_t base = p.list_off[q * p.R];
   double* io = p.fused + (int64_t)ms * p.out_stride + base;  // unsorted fused[ms][u]
   const int rows = (U + 64 * WAVES - 1) / (64 * WAVES);
   // ---- full keys of the join kernel's unsorted scores, their range -------------
