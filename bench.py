@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--native-sample", type=int, default=400,
                     help="queries timed through the C oracle (0 = skip)")
     ap.add_argument("--check", type=int, default=8, help="queries checked bit-exact vs oracle")
+    ap.add_argument("--ndcg-sample", type=int, default=256,
+                    help="queries whose NDCG@10 is recomputed on the CPU reference path")
     return ap.parse_args()
 
 
@@ -131,6 +133,63 @@ class Pipeline:
         reads = N * (4 + 4) + self.Q * self.R * 8 + (self.Q * self.R + 1) * 8
         writes = int(uc.sum()) * (4 + M * (2 + 8)) + self.Q * 4
         return reads + writes, float(uc.mean())
+
+
+def synth_qrels(q_begin: int, Q: int, K: int):
+    """Judged documents of the synthetic queries: 1-3 pool documents each (the first
+    rel 2, the others rel 1) — ids as qf_synth_runs draws pool documents."""
+    qg = np.arange(q_begin, q_begin + Q, dtype=np.int64)
+    nrel = 1 + qg % 3
+    qo = np.zeros(Q + 1, np.int64)
+    qo[1:] = np.cumsum(nrel)
+    rep = np.repeat(qg, nrel)
+    pidx = np.arange(qo[-1]) - np.repeat(qo[:-1], nrel)
+    qd = ((rep * K + pidx) & 0x7FFFFFFF).astype(np.uint32)
+    qr = np.where(pidx == 0, 2, 1).astype(np.int32)
+    return qo, qd, qr
+
+
+def ndcg_device(p: Pipeline):
+    """NDCG@10 of every fused run on device (qf_eval, scores as the .res text)."""
+    from qppfuse.evaluation import evaluate_device
+    qo, qd, qr = synth_qrels(p.q_begin, p.Q, p.K)
+    t = lambda a: torch.from_numpy(a).to(p.dev)
+    qdev = (t(qo), t(qd.view(np.int32)), t(qr))
+    o = p.out
+    run = lambda: evaluate_device(p.off, p.R, o.union_count, o.union_docid, o.perm, o.fused,
+                                  o.fused.shape[1], len(METHODS), p.Q, qdev,
+                                  int(np.diff(qo).max()), ["nDCG@10"], text_scores=True)
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vals = run()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    return vals[:, :, 0].cpu().numpy(), ms
+
+
+def ndcg_delta(p: Pipeline, dev_vals, nq: int):
+    """NDCG@10 of the CPU reference path (C oracle fusion + trec_eval restatement)
+    on the first nq queries vs the device values: largest |delta|."""
+    from oracle import _loader as coracle
+    h = host_sample(p, nq)
+    sc = h["micro"].astype(np.float64) / 1e6
+    qo, qd, qr = synth_qrels(p.q_begin, nq, p.K)
+    worst_q, worst_mean = 0.0, 0.0
+    for m, name in enumerate(METHODS):
+        ud_all, uc, perm, fused = coracle.fuse(h["off"], h["docid"], sc, p.R, name, 60,
+                                               weights=h["w"])
+        roff = np.zeros(nq + 1, np.int64)
+        roff[1:] = np.cumsum(uc)
+        b = h["off"][:-1:p.R][:nq]
+        rdoc = np.concatenate([ud_all[b[q] + perm[b[q]:b[q] + uc[q]].astype(np.int64)]
+                               for q in range(nq)])
+        rsc = np.concatenate([fused[b[q]:b[q] + uc[q]] for q in range(nq)])
+        ref = coracle.evaluate(roff, rdoc, rsc, qo, qd, qr, ["nDCG@10"], text=True)[:, 0]
+        d = dev_vals[m, :nq]
+        worst_q = max(worst_q, float(np.nanmax(np.abs(d - ref))))
+        worst_mean = max(worst_mean, abs(float(np.nanmean(d)) - float(np.nanmean(ref))))
+    return worst_q, worst_mean
 
 
 def host_sample(p: Pipeline, nq: int):
@@ -260,6 +319,7 @@ def main():
     achieved = fbytes / (fuse_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args)
     parity = check_parity(p, min(args.check, args.queries)) if args.check > 0 else None
+    ndcg_vals, eval_ms = ndcg_device(p)
     result = None
     if rank == 0:
         cpu = None
@@ -293,7 +353,17 @@ def main():
                          "kernel_ms": round(fuse_ms, 4)},
             "cpu_baseline": cpu,
             "parity_vs_oracle": {"queries": min(args.check, args.queries), "bit_exact": parity},
+            "ndcg10": {m: round(float(np.nanmean(ndcg_vals[i])), 6)
+                       for i, m in enumerate(METHODS)},
+            "ndcg10_eval_ms": round(eval_ms, 4),
         }
+        if world == 1 and args.ndcg_sample > 0:
+            nq = min(args.ndcg_sample, args.queries)
+            dq, dm = ndcg_delta(p, ndcg_vals, nq)
+            result["ndcg10_delta_vs_ref"] = {
+                "queries": nq, "max_abs_per_query": dq, "max_abs_mean": dm,
+                "ref": "CPU reference path: C oracle fusion + trec_eval restatement "
+                       "(oracle/), scores as the .res text"}
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

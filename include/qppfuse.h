@@ -143,6 +143,43 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
             uint16_t* perm, double* fused, int64_t out_stride, void* stream);
 
+/* ---- IR evaluation (trec_eval semantics, as ir_measures computes them) ---- */
+#define QF_EVAL_NDCG 0 /* nDCG@k   */
+#define QF_EVAL_RR   1 /* RR@k     */
+#define QF_EVAL_R    2 /* R@k      */
+#define QF_EVAL_P    3 /* P@k      */
+#define QF_EVAL_AP   4 /* AP (cut ignored) */
+#define QF_EVAL_MAX_METRICS 16
+#define QF_EVAL_MAX_QRELS 256 /* judged documents per query */
+
+/*
+ * Evaluation of ranked runs against qrels — the metrics scripts/06_eval_fusion.py
+ * gets from ir_measures (src/evaluation/ir_evaluator.py:51-86, metric list
+ * config/defaults.yaml:224-234) on the fused .res files.  Documents are ranked by
+ * score descending, ties by docno descending (trec_eval), which is docid
+ * descending when docids are interned in docno string order.  text_scores != 0
+ * takes every score as the "%.6f" text write_runfile prints (src/fusion.py:491)
+ * and 06_eval_fusion reads back; 0 takes the doubles as they are.
+ *
+ * Run m (0..n_runs-1), query q: its list is sorted by score descending and holds
+ * n_q = q_count[q] (or, q_count NULL, q_base[(q+1)*base_stride] - b) entries at
+ * b = q_base[q*base_stride]:  score[m*out_stride + b + i], and docid
+ * docid[b + perm[m*out_stride + b + i]] when perm is non-NULL (qf_fuse's
+ * outputs: q_base = list_off, base_stride = R, q_count = union_count, docid =
+ * union_docid), else docid[m*out_stride + b + i].
+ * Qrels (device): qrel_off[Q+1] (int64), qrel_docid (uint32, ascending inside a
+ * query), qrel_rel (int32); at most max_qrels <= QF_EVAL_MAX_QRELS per query.
+ * Metrics (HOST arrays): kind[t] (QF_EVAL_*), cut[t] (k >= 1; ignored for AP).
+ * out[(m*Q + q)*n_metrics + t] (device double): the value, or NaN when the query
+ * has no entries or no qrels (trec_eval does not evaluate it).
+ */
+int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,
+            const int32_t* q_count, const uint32_t* docid, const uint16_t* perm,
+            const double* score, int64_t out_stride, int32_t n_runs, int32_t text_scores,
+            const int64_t* qrel_off, const uint32_t* qrel_docid, const int32_t* qrel_rel,
+            int32_t max_qrels, int32_t n_metrics, const int32_t* kind, const int32_t* cut,
+            double* out, void* stream);
+
 /*
  * Benchmark / test support: generate Q*R synthetic lists of K entries
  * (docid, raw score sorted descending) on device, deterministic in seed.

@@ -13,7 +13,7 @@ _lib = None
 
 
 def build() -> Path:
-    srcs = [HERE / "fusion_oracle.c", HERE / "qpp_oracle.c"]
+    srcs = [HERE / "fusion_oracle.c", HERE / "qpp_oracle.c", HERE / "eval_oracle.c"]
     if not LIB.exists() or any(s.stat().st_mtime > LIB.stat().st_mtime for s in srcs):
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB
@@ -29,6 +29,8 @@ def lib() -> C.CDLL:
         _lib.oracle_fuse.argtypes = [i64, i32, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp]
         _lib.oracle_minmax_per_query.restype = None
         _lib.oracle_minmax_per_query.argtypes = [vp, vp, i64, vp]
+        _lib.oracle_eval.restype = C.c_int
+        _lib.oracle_eval.argtypes = [i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
         _lib.oracle_qpp_raw.restype = None
         _lib.oracle_qpp_raw.argtypes = [vp, vp, i64, vp, vp, vp, vp]
     return _lib
@@ -80,4 +82,34 @@ def qpp_raw(score, list_off, num_terms, maxidf, avgidf):
     ai = np.ascontiguousarray(np.broadcast_to(avgidf, (L,)), dtype=np.float64)
     out = np.zeros((L, 13), np.float64)
     lib().oracle_qpp_raw(_p(score), _p(list_off), L, _p(nt), _p(mi), _p(ai), _p(out))
+    return out
+
+
+EVAL_KINDS = {"ndcg": 0, "rr": 1, "r": 2, "p": 3, "ap": 4}
+
+
+def _measure(name):
+    import re
+    m = re.fullmatch(r"([A-Za-z]+)(?:@(\d+))?", name)
+    kind = EVAL_KINDS[m.group(1).lower()]
+    return kind, int(m.group(2)) if m.group(2) else (0 if kind == 4 else 1 << 30)
+
+
+def evaluate(off, docid, score, qrel_off, qrel_docid, qrel_rel, measures, text=False):
+    """trec_eval restatement: [Q, len(measures)] float64 (NaN = not evaluated)."""
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    docid = np.ascontiguousarray(docid, dtype=np.uint32)
+    score = np.ascontiguousarray(score, dtype=np.float64)
+    qrel_off = np.ascontiguousarray(qrel_off, dtype=np.int64)
+    qrel_docid = np.ascontiguousarray(qrel_docid, dtype=np.uint32)
+    qrel_rel = np.ascontiguousarray(qrel_rel, dtype=np.int32)
+    spec = [_measure(m) for m in measures]
+    kind = np.asarray([k for k, _ in spec], np.int32)
+    cut = np.asarray([c for _, c in spec], np.int32)
+    Q = len(off) - 1
+    out = np.zeros((Q, len(spec)), np.float64)
+    rc = lib().oracle_eval(Q, _p(off), _p(docid), _p(score), int(bool(text)), _p(qrel_off),
+                           _p(qrel_docid), _p(qrel_rel), len(spec), _p(kind), _p(cut), _p(out))
+    if rc != 0:
+        raise MemoryError("oracle_eval")
     return out

@@ -111,6 +111,49 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
                "qf_fuse");
 }
 
+int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,
+            const int32_t* q_count, const uint32_t* docid, const uint16_t* perm,
+            const double* score, int64_t out_stride, int32_t n_runs, int32_t text_scores,
+            const int64_t* qrel_off, const uint32_t* qrel_docid, const int32_t* qrel_rel,
+            int32_t max_qrels, int32_t n_metrics, const int32_t* kind, const int32_t* cut,
+            double* out, void* stream) {
+  if (n_queries < 0 || n_runs < 0 || base_stride <= 0 || out_stride < 0)
+    return fail(QF_EINVAL, "qf_eval: bad sizes");
+  if (n_metrics <= 0 || n_metrics > QF_EVAL_MAX_METRICS || !kind || !cut)
+    return fail(QF_EINVAL, "qf_eval: n_metrics must be in [1, %d]", QF_EVAL_MAX_METRICS);
+  if (max_qrels < 0 || max_qrels > QF_EVAL_MAX_QRELS)
+    return fail(QF_ETOOBIG, "qf_eval: %d judged documents in one query exceed %d", max_qrels,
+                QF_EVAL_MAX_QRELS);
+  qf::EvalParams p{};
+  for (int t = 0; t < n_metrics; ++t) {
+    if (kind[t] < QF_EVAL_NDCG || kind[t] > QF_EVAL_AP)
+      return fail(QF_EINVAL, "qf_eval: bad metric kind %d", kind[t]);
+    if (kind[t] != QF_EVAL_AP && cut[t] < 1)
+      return fail(QF_EINVAL, "qf_eval: metric cutoff must be >= 1");
+    p.kind[t] = kind[t];
+    p.cut[t] = kind[t] == QF_EVAL_AP ? 0 : cut[t];
+  }
+  if (n_queries == 0 || n_runs == 0) return QF_OK;
+  if (!q_base || !docid || !score || !qrel_off || !qrel_docid || !qrel_rel || !out)
+    return fail(QF_EINVAL, "qf_eval: null buffer");
+  p.n_queries = n_queries;
+  p.q_base = q_base;
+  p.base_stride = base_stride;
+  p.q_count = q_count;
+  p.docid = docid;
+  p.perm = perm;
+  p.score = score;
+  p.out_stride = out_stride;
+  p.n_runs = n_runs;
+  p.text_scores = text_scores != 0;
+  p.qrel_off = qrel_off;
+  p.qrel_docid = qrel_docid;
+  p.qrel_rel = qrel_rel;
+  p.n_metrics = n_metrics;
+  p.out = out;
+  return check(qf::eval_launch(p, (hipStream_t)stream), "qf_eval");
+}
+
 int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
                   uint64_t seed, double p_shared, int64_t* list_off, uint32_t* docid,
                   double* score, void* stream) {

@@ -23,7 +23,33 @@ struct FuseParams {
   int64_t out_stride;
 };
 
+// IR evaluation (qf_eval): run m, query q reads its ranked list at
+// [q_base[q*base_stride], + q_count[q] (or up to the next base)) of score /
+// perm (+ m*out_stride) and docid (shared through perm, else + m*out_stride).
+constexpr int kEvalMaxRel = 256;  // judged documents per query
+constexpr int kEvalMaxMetrics = 16;
+struct EvalParams {
+  int64_t n_queries;
+  const int64_t* q_base;
+  int32_t base_stride;
+  const int32_t* q_count;
+  const uint32_t* docid;
+  const uint16_t* perm;
+  const double* score;
+  int64_t out_stride;
+  int32_t n_runs;
+  int32_t text_scores;
+  const int64_t* qrel_off;
+  const uint32_t* qrel_docid;
+  const int32_t* qrel_rel;
+  int32_t n_metrics;
+  int32_t kind[kEvalMaxMetrics];
+  int32_t cut[kEvalMaxMetrics];
+  double* out;
+};
+
 int fuse_max_entries();
+hipError_t eval_launch(const EvalParams& p, hipStream_t st);
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);
 hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t Q, int32_t R,
                           int32_t top_k, const int32_t* nt, const double* tf, double* out,

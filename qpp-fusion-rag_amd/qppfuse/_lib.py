@@ -23,6 +23,8 @@ METHOD_BITS = {"combsum": COMBSUM, "combmnz": COMBMNZ, "rrf": RRF,
 SCORE_F64, SCORE_MICRO = 0, 1
 NORM_NONE, NORM_MINMAX = 0, 1
 QPP_COLS = 13
+EVAL_NDCG, EVAL_RR, EVAL_R, EVAL_P, EVAL_AP = range(5)
+EVAL_MAX_METRICS, EVAL_MAX_QRELS = 16, 256
 
 # name -> (restype, argtypes); must match include/qppfuse.h
 _vp, _i32, _i64, _u64, _f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -36,6 +38,8 @@ SIGNATURES = {
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
                           _vp, _vp, _vp, _vp, _i64, _vp]),
+    "qf_eval": (C.c_int, [_i64, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp,
+                          _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
 }
 

@@ -1,7 +1,8 @@
 """The configuration keys the fusion/QPP path reads.
 
 Mirrors the values of the reference's config/defaults.yaml that this path uses
-(qpp.* :159-200, fusion.* :205-217, processing.retrieval.top_k :152-154) and
+(qpp.* :159-200, fusion.* :205-217, processing.retrieval.top_k :152-154,
+evaluation.ir_metrics :224-234) and
 Config.get_qpp_index (src/config.py:317-333).  Environment plumbing for
 retrievers / LLMs (src/config.py:195-231) is out of scope.
 """
@@ -31,6 +32,9 @@ config = SimpleNamespace(
                         default_index=5, normalization="minmax"),
     fusion=SimpleNamespace(rrf_k=60, methods=list(FUSION_METHODS)),
     processing=SimpleNamespace(retrieval=SimpleNamespace(top_k=100, first_stage_k=100)),
+    # config/defaults.yaml:224-234 (evaluation.ir_metrics)
+    evaluation=SimpleNamespace(ir_metrics=["nDCG@5", "nDCG@10", "nDCG@20", "RR@5", "RR@10",
+                                           "R@5", "R@10", "R@100", "P@10", "AP"]),
 )
 
 

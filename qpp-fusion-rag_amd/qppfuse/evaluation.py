@@ -1,0 +1,230 @@
+"""IR evaluation of (fused) runs on MI355X — the metrics step of the reference.
+
+Mirrors src/evaluation/ir_evaluator.py (IREvaluator :40-150) and the way
+scripts/06_eval_fusion.py:42-140 uses it on the fused .res files: the metrics
+config.evaluation.ir_metrics names (config/defaults.yaml:224-234), computed
+with trec_eval semantics (ir_measures' default backend): documents ranked by
+score descending, ties by docno descending; relevant = rel >= 1; nDCG gains =
+rel levels.  The work runs in the HIP kernel qf_eval (csrc/qf_eval.hip); this
+module packs runs and qrels into its CSR layout.  There is no CPU path.
+"""
+from __future__ import annotations
+
+import re
+from collections.abc import Mapping
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import pandas as pd
+
+from . import _lib, engine
+from .config import config
+from .data_utils import load_qrels, load_run_file
+
+__all__ = ["IREvaluator", "parse_measure", "load_qrels", "load_run_file", "QrelSet",
+           "pack_qrels", "evaluate_device"]
+
+_KINDS = {"ndcg": _lib.EVAL_NDCG, "rr": _lib.EVAL_RR, "r": _lib.EVAL_R, "p": _lib.EVAL_P,
+          "ap": _lib.EVAL_AP}
+_NO_CUT = 1 << 30
+
+
+def parse_measure(name: str) -> Tuple[int, int]:
+    """'nDCG@10' -> (QF_EVAL_NDCG, 10); 'AP' / 'RR' without a cutoff -> whole list."""
+    m = re.fullmatch(r"\s*([A-Za-z]+)\s*(?:@\s*(\d+))?\s*", name)
+    if not m or m.group(1).lower() not in _KINDS:
+        raise ValueError(f"unsupported measure '{name}' (nDCG@k, RR@k, R@k, P@k, AP)")
+    kind = _KINDS[m.group(1).lower()]
+    if m.group(2) is None:
+        if kind in (_lib.EVAL_R, _lib.EVAL_P):
+            raise ValueError(f"measure '{name}' needs a cutoff")
+        return kind, _NO_CUT if kind != _lib.EVAL_AP else 0
+    k = int(m.group(2))
+    if k < 1:
+        raise ValueError(f"measure '{name}': cutoff must be >= 1")
+    return kind, k
+
+
+class QrelSet:
+    """Qrels in the run's query order: CSR of (docid ascending, rel) per query."""
+
+    def __init__(self, off: np.ndarray, docid: np.ndarray, rel: np.ndarray):
+        self.off, self.docid, self.rel = off, docid, rel
+        self.max_per_query = int(np.max(np.diff(off))) if len(off) > 1 else 0
+
+    def to_device(self, device):
+        import torch
+        return (torch.from_numpy(self.off).to(device),
+                torch.from_numpy(self.docid.view(np.int32)).to(device),
+                torch.from_numpy(self.rel).to(device))
+
+
+def pack_qrels(qrels: Dict[str, Dict[str, int]], qids: Sequence[str],
+               docnos: np.ndarray) -> QrelSet:
+    """Map qrels onto the run's queries and docno ids (docnos sorted ascending).
+
+    Judged documents absent from the run keep their place in the counts (they
+    are relevant but never retrieved) under the reserved id 0xFFFFFFFF."""
+    offs = [0]
+    ids: List[np.ndarray] = []
+    rels: List[np.ndarray] = []
+    for qid in qids:
+        judged = qrels.get(qid, {})
+        if not judged:
+            offs.append(offs[-1])
+            continue
+        names = np.asarray(list(judged.keys()), dtype=object)
+        rv = np.fromiter(judged.values(), dtype=np.int32, count=len(judged))
+        pos = np.searchsorted(docnos, names)
+        pos_c = np.minimum(pos, max(len(docnos) - 1, 0))
+        found = (pos < len(docnos)) & (docnos[pos_c] == names) if len(docnos) else \
+            np.zeros(len(names), bool)
+        d = np.where(found, pos_c, 0xFFFFFFFF).astype(np.uint32)
+        o = np.argsort(d, kind="stable")
+        ids.append(d[o])
+        rels.append(rv[o])
+        offs.append(offs[-1] + len(judged))
+    off = np.asarray(offs, dtype=np.int64)
+    docid = np.concatenate(ids) if ids else np.zeros(0, np.uint32)
+    rel = np.concatenate(rels) if rels else np.zeros(0, np.int32)
+    return QrelSet(off, docid, rel)
+
+
+def evaluate_device(q_base, base_stride: int, q_count, docid, perm, score, out_stride: int,
+                    n_runs: int, n_queries: int, qrels_dev, max_qrels: int,
+                    measures: Sequence[str], text_scores: bool = True):
+    """qf_eval on device buffers -> float64 tensor [n_runs, n_queries, n_measures]."""
+    import torch
+    dev = engine.require_device()
+    spec = [parse_measure(m) for m in measures]
+    if len(spec) > _lib.EVAL_MAX_METRICS:
+        raise ValueError(f"at most {_lib.EVAL_MAX_METRICS} measures per call")
+    if max_qrels > _lib.EVAL_MAX_QRELS:
+        raise ValueError(f"{max_qrels} judged documents in one query exceed "
+                         f"{_lib.EVAL_MAX_QRELS}")
+    kind = np.asarray([k for k, _ in spec], dtype=np.int32)
+    cut = np.asarray([c for _, c in spec], dtype=np.int32)
+    out = torch.empty((n_runs, n_queries, len(spec)), dtype=torch.float64, device=dev)
+    qo, qd, qr = qrels_dev
+    p = engine._ptr
+    _lib.call("qf_eval", int(n_queries), p(q_base), int(base_stride), p(q_count), p(docid),
+              p(perm), p(score), int(out_stride), int(n_runs), int(bool(text_scores)), p(qo),
+              p(qd), p(qr), int(max_qrels), len(spec), kind.ctypes.data, cut.ctypes.data,
+              p(out), engine._stream())
+    return out
+
+
+def _run_arrays(run) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+    """{qid: [(docno, score)]} / DataFrame -> qids, docnos (sorted), off, docid, score.
+
+    Each query's list is ordered by score descending (stable), as
+    scripts/06_eval_fusion.py:46-49 orders it before evaluation."""
+    if isinstance(run, pd.DataFrame):
+        q = run["qid" if "qid" in run else "query_id"].astype(str).to_numpy()
+        d = run["docno" if "docno" in run else "doc_id"].astype(str).to_numpy()
+        s = run["score"].to_numpy(dtype=np.float64)
+        # later rows of a repeated (qid, docno) win, as the dict conversion does
+        df = pd.DataFrame({"q": q, "d": d, "s": s}).drop_duplicates(["q", "d"], keep="last")
+        groups = {k: list(zip(g["d"], g["s"])) for k, g in df.groupby("q", sort=False)}
+        run = groups
+    qids = [str(k) for k in run.keys()]
+    per_q = []
+    for qid in run:
+        items = run[qid]
+        if isinstance(items, Mapping):
+            items = list(items.items())
+        dd = {}
+        for doc, sc in items:  # ir_measures' dict: a repeated docno keeps its last score
+            dd[str(doc)] = float(sc)
+        per_q.append(dd)
+    all_docs = np.asarray(sorted({d for dd in per_q for d in dd}), dtype=object)
+    off = np.zeros(len(per_q) + 1, dtype=np.int64)
+    docid_parts, score_parts = [], []
+    for i, dd in enumerate(per_q):
+        names = np.asarray(list(dd.keys()), dtype=object)
+        sc = np.fromiter(dd.values(), dtype=np.float64, count=len(dd))
+        ids = np.searchsorted(all_docs, names).astype(np.uint32)
+        o = np.argsort(-sc, kind="stable")
+        docid_parts.append(ids[o])
+        score_parts.append(sc[o])
+        off[i + 1] = off[i] + len(dd)
+    docid = np.concatenate(docid_parts) if docid_parts else np.zeros(0, np.uint32)
+    score = np.concatenate(score_parts) if score_parts else np.zeros(0)
+    return qids, all_docs, off, docid, score
+
+
+class IREvaluator:
+    """ir_measures-style evaluator (src/evaluation/ir_evaluator.py:40-150) on device."""
+
+    def __init__(self, metrics: Optional[List[str]] = None, text_scores: bool = False):
+        self.metric_names = list(metrics or config.evaluation.ir_metrics)
+        for m in self.metric_names:
+            parse_measure(m)
+        # True: score ties as in the "%.6f" text of a run file (what 06_eval_fusion
+        # evaluates); False: the doubles as given (an in-memory run).
+        self.text_scores = text_scores
+
+    def _per_query_values(self, run, qrels) -> Tuple[List[str], np.ndarray]:
+        import torch
+        from .fusion import FusedRun
+        dev = engine.require_device()
+        if isinstance(qrels, pd.DataFrame):
+            qrels = self._convert_qrels(qrels)
+        if isinstance(run, FusedRun):
+            qids, docnos = run._qids, run._docnos
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+            q_base = t(run._qbase.astype(np.int64))
+            q_count = t(run._counts.astype(np.int32))
+            docid = t(run._udoc.view(np.int32))
+            perm = t(run._perm.view(np.int16))
+            score = t(run._fused)
+            qs = pack_qrels(qrels, qids, docnos)
+            vals = []
+            for a in range(0, len(self.metric_names), _lib.EVAL_MAX_METRICS):
+                names = self.metric_names[a:a + _lib.EVAL_MAX_METRICS]
+                vals.append(evaluate_device(q_base, 1, q_count, docid, perm, score, 0, 1,
+                                            len(qids), qs.to_device(dev), qs.max_per_query,
+                                            names, self.text_scores)[0])
+            return qids, torch.cat(vals, 1).cpu().numpy()
+        qids, docnos, off, docid_h, score_h = _run_arrays(run)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        qs = pack_qrels(qrels, qids, docnos)
+        vals = []
+        for a in range(0, len(self.metric_names), _lib.EVAL_MAX_METRICS):
+            names = self.metric_names[a:a + _lib.EVAL_MAX_METRICS]
+            vals.append(evaluate_device(t(off), 1, None, t(docid_h.view(np.int32)), None,
+                                        t(score_h), 0, 1, len(qids), qs.to_device(dev),
+                                        qs.max_per_query, names, self.text_scores)[0])
+        return qids, torch.cat(vals, 1).cpu().numpy()
+
+    def evaluate(self, run, qrels, per_query: bool = False):
+        """{metric: mean over evaluated queries}, or {metric: {qid: value}}."""
+        qids, v = self._per_query_values(run, qrels)
+        if per_query:
+            return {m: {q: float(v[i, t]) for i, q in enumerate(qids) if not np.isnan(v[i, t])}
+                    for t, m in enumerate(self.metric_names)}
+        out = {}
+        for t, m in enumerate(self.metric_names):
+            col = v[:, t]
+            col = col[~np.isnan(col)]
+            out[m] = float(col.mean()) if col.size else 0.0
+        return out
+
+    def evaluate_multiple(self, runs: Dict[str, object], qrels) -> pd.DataFrame:
+        rows = []
+        for name, run in runs.items():
+            r = self.evaluate(run, qrels)
+            r["run_name"] = name
+            rows.append(r)
+        df = pd.DataFrame(rows).set_index("run_name")
+        return df.sort_values(by=self.metric_names[0], ascending=False)
+
+    @staticmethod
+    def _convert_qrels(qrels: pd.DataFrame) -> Dict[str, Dict[str, int]]:
+        out: Dict[str, Dict[str, int]] = {}
+        qc = "qid" if "qid" in qrels else "query_id"
+        dc = "docno" if "docno" in qrels else "doc_id"
+        lc = "label" if "label" in qrels else "relevance"
+        for q, d, l in zip(qrels[qc].astype(str), qrels[dc].astype(str), qrels[lc]):
+            out.setdefault(q, {})[d] = int(l)
+        return out

@@ -103,7 +103,8 @@ def pack_frames(runs: Dict[str, pd.DataFrame]) -> RunSet:
     r_all = np.concatenate(r_parts)
     qids = sorted(set(qid_all.tolist()))
     qcode = pd.Categorical(qid_all, categories=qids).codes.astype(np.int64)
-    dcode, docnos = pd.factorize(doc_all, sort=False)
+    # ids in docno string order: trec_eval breaks score ties by docno (qf_eval)
+    dcode, docnos = pd.factorize(doc_all, sort=True)
     if len(docnos) >= 0xFFFFFFFF:
         raise ValueError("too many distinct docnos for uint32 ids")
     key = qcode * R + r_all

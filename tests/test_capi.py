@@ -17,7 +17,7 @@ def test_header_declares_expected_entry_points():
     fns = header_functions()
     for name in ["qf_fuse", "qf_minmax_per_query", "qf_qpp_raw", "qf_qpp_colminmax",
                  "qf_qpp_normalize", "qf_last_error", "qf_version", "qf_max_entries_per_query",
-                 "qf_synth_runs"]:
+                 "qf_synth_runs", "qf_eval"]:
         assert name in fns
 
 
@@ -51,6 +51,20 @@ def test_argument_validation_without_device():
     with pytest.raises(ValueError, match="null buffer"):
         _lib.call("qf_fuse", 1, 2, 8, 8, 8, 0, None, None, _lib.RRF, 60, 10, 8, 8, 8, None, 16,
                   None)
+    import ctypes as C
+    import numpy as np
+    kind = np.array([0], np.int32)
+    cut = np.array([0], np.int32)
+    with pytest.raises(ValueError, match="cutoff"):
+        _lib.call("qf_eval", 1, 8, 1, None, 8, None, 8, 0, 1, 0, 8, 8, 8, 1, 1,
+                  kind.ctypes.data, cut.ctypes.data, 8, None)
+    cut[0] = 10
+    with pytest.raises(_lib.QPPFuseError, match="judged"):
+        _lib.call("qf_eval", 1, 8, 1, None, 8, None, 8, 0, 1, 0, 8, 8, 8, 10**6, 1,
+                  kind.ctypes.data, cut.ctypes.data, 8, None)
+    with pytest.raises(ValueError, match="null buffer"):
+        _lib.call("qf_eval", 1, None, 1, None, 8, None, 8, 0, 1, 0, 8, 8, 8, 1, 1,
+                  kind.ctypes.data, cut.ctypes.data, 8, None)
     with pytest.raises(ValueError, match="qpp_index"):
         _lib.call("qf_qpp_normalize", 1, 1, 1, 1, 1, 1, 13, None, None, None, None)
 
