@@ -270,7 +270,7 @@ def cpu_baseline_native(p: Pipeline, nq: int):
     return nq / dt
 
 
-def pmc_traffic(args, kernel_substr="fuse_kernel"):
+def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     """HBM bytes per qf_fuse launch from the newest committed rocprofv3 PMC summary.
 
     profiles/rNN_pmc.json is produced by tools/profile.sh + tools/summarize_profile.py

@@ -611,27 +611,22 @@ struct SortCfg {
   static_assert(kSmem <= 160 * 1024, "LDS budget");
 };
 
-template <class C, int KIND>
-__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParams p, int umin) {
-  constexpr int ITEMS = C::kItems, WAVES = C::kWaves, UMAX = C::kUMax;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
-  __shared__ int s_flag[2];
-  __shared__ uint32_t s_wtot[16];
-  __shared__ unsigned long long s_kmin, s_kmax;
+template <class C>
+struct SortShared {
+  __attribute__((aligned(16))) unsigned char smem[C::kSmem];
+  int flag[2];
+  uint32_t wtot[16];
+  unsigned long long kmin, kmax;
+};
 
+// Sort one (query, method slot): fused[ms][base .. base+U) in place + perm.
+template <class C>
+__device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh, int ms, int U,
+                                         int64_t base) {
+  constexpr int ITEMS = C::kItems, WAVES = C::kWaves;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // block -> (query, method slot): slot-major groups of 8 queries, so that the
-  // blocks resident together on an XCD (blockIdx % 8) read adjacent queries.
-  const int M = __popc(p.methods);
-  const int64_t grp8 = (int64_t)(blockIdx.x >> 3);
-  const int64_t q = (grp8 / M) * 8 + (blockIdx.x & 7);
-  const int ms = (int)(grp8 % M);
-  if (q >= p.n_queries) return;
-  const int U = p.union_count[q];
-  const int64_t base = p.list_off[q * p.R];  // both loads in flight together
-  if (U < 0 || U > UMAX || U < umin) return;  // error / other pass
   QF_STAMP_INIT();
-  if (tid == 0) { s_kmin = ~0ull; s_kmax = 0ull; }
+  if (tid == 0) { sh.kmin = ~0ull; sh.kmax = 0ull; }
   __syncthreads();
   double* io = p.fused + (int64_t)ms * p.out_stride + base;  // unsorted fused[ms][u]
   const int rows = (U + 64 * WAVES - 1) / (64 * WAVES);
@@ -648,11 +643,12 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
       kmx = max(kmx, item[j]);
     }
   }
-  block_min_max(kmn, kmx, &s_kmin, &s_kmax, lane);
+  block_min_max(kmn, kmx, &sh.kmin, &sh.kmax, lane);
   __syncthreads();
-  const uint64_t kmin = s_kmin, kmax = s_kmax;
-  SortCtx<ITEMS, WAVES> sx{(uint32_t*)(smem + C::kHistOff), (uint64_t*)(smem + C::kItemOff),
-                           s_wtot, s_flag, io, kmin, U, rows, lane, wid, tid};
+  const uint64_t kmin = sh.kmin, kmax = sh.kmax;
+  SortCtx<ITEMS, WAVES> sx{(uint32_t*)(sh.smem + C::kHistOff),
+                           (uint64_t*)(sh.smem + C::kItemOff), sh.wtot, sh.flag, io, kmin, U,
+                           rows, lane, wid, tid};
   // ---- items: window key | u ----------------------------------------------------
   const int hb = kmax > kmin ? 64 - __clzll((long long)(kmax - kmin)) : 0;
   const int lo = hb > kWindow ? hb - kWindow : 0;
@@ -666,6 +662,57 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   QF_STAMP(1);
   write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base, io);
   QF_STAMP(2);
+}
+
+// One workgroup per (query, method slot), the queries with U in [umin, UMAX].
+template <class C>
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParams p, int umin) {
+  __shared__ SortShared<C> sh;
+  // block -> (query, method slot): slot-major groups of 8 queries, so that the
+  // blocks resident together on an XCD (blockIdx % 8) read adjacent queries.
+  const int M = __popc(p.methods);
+  const int64_t grp8 = (int64_t)(blockIdx.x >> 3);
+  const int64_t q = (grp8 / M) * 8 + (blockIdx.x & 7);
+  const int ms = (int)(grp8 % M);
+  if (q >= p.n_queries) return;
+  const int U = p.union_count[q];
+  const int64_t base = p.list_off[q * p.R];  // both loads in flight together
+  if (U < 0 || U > C::kUMax || U < umin) return;  // error / other pass
+  sort_one<C>(p, sh, ms, U, base);
+}
+
+// The same for the few large queries (U in [umin, UMAX]): a grid of one
+// workgroup per CU, each listing the (query, method) pairs of its stride
+// that qualify (one parallel load of their counts) and sorting them in turn —
+// so a batch without large queries costs a few microseconds, not one
+// dispatched workgroup per pair.
+template <class C>
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(FuseParams p,
+                                                                            int umin) {
+  __shared__ SortShared<C> sh;
+  __shared__ int s_list[C::kBlock];
+  __shared__ int s_n;
+  const int tid = threadIdx.x;
+  const int M = __popc(p.methods);
+  const int64_t pairs = p.n_queries * M;
+  const int64_t span = (int64_t)gridDim.x * C::kBlock;
+  for (int64_t c0 = 0; c0 < pairs; c0 += span) {
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    const int64_t idx = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
+    if (idx < pairs) {
+      const int U = p.union_count[idx / M];
+      if (U >= umin && U <= C::kUMax) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
+    }
+    __syncthreads();
+    const int n = s_n;
+    for (int t = 0; t < n; ++t) {
+      const int64_t id = c0 + s_list[t];
+      const int64_t q = id / M;
+      sort_one<C>(p, sh, (int)(id % M), p.union_count[q], p.list_off[q * p.R]);
+      __syncthreads();
+    }
+  }
 }
 
 // ---- launch -----------------------------------------------------------------
@@ -686,23 +733,30 @@ static void launch_join(const FuseParams& p, int kind, hipStream_t st) {
 }
 
 template <class S>
-static void launch_sort(const FuseParams& p, int kind, int umin, hipStream_t st) {
+static void launch_sort(const FuseParams& p, int umin, hipStream_t st) {
   const int M = __builtin_popcount((unsigned)p.methods);
   const int64_t groups = (p.n_queries + 7) / 8;
-  dim3 grid((unsigned)(groups * 8 * M)), block(S::kBlock);
-  if (kind == 1) hipLaunchKernelGGL((fuse_kernel<S, 1>), grid, block, 0, st, p, umin);
-  else hipLaunchKernelGGL((fuse_kernel<S, 0>), grid, block, 0, st, p, umin);
+  hipLaunchKernelGGL((fuse_kernel<S>), dim3((unsigned)(groups * 8 * M)), dim3(S::kBlock), 0, st,
+                     p, umin);
+}
+
+template <class S>
+static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st) {
+  const int64_t pairs = p.n_queries * __builtin_popcount((unsigned)p.methods);
+  const int64_t grid = pairs < 256 ? pairs : 256;  // one per CU (VGPR-bound)
+  hipLaunchKernelGGL((fuse_large_kernel<S>), dim3((unsigned)grid), dim3(S::kBlock), 0, st, p,
+                     umin);
 }
 
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
   if (max_entries <= JoinS::kNMax) {
     launch_join<JoinS>(p, kind, st);
-    launch_sort<SortS>(p, kind, 0, st);
+    launch_sort<SortS>(p, 0, st);
   } else {
     if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
     else launch_join<JoinL>(p, kind, st);
-    launch_sort<SortM>(p, kind, 0, st);
-    launch_sort<SortL>(p, kind, SortM::kUMax + 1, st);  // the queries SortM left
+    launch_sort<SortM>(p, 0, st);
+    launch_sort_large<SortL>(p, SortM::kUMax + 1, st);  // the queries SortM left
   }
   return hipGetLastError();
 }

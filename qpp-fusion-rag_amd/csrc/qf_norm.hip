@@ -89,7 +89,10 @@ __global__ __launch_bounds__(256) void synth_kernel(int64_t q_begin, int64_t n_q
       A += 2;
       if (A >= (uint32_t)P) A = 1;
     }
-    const uint32_t B = (uint32_t)((hl >> 32) % (uint64_t)P);
+    // with probability 1/2 the list's first position maps to pool index 0..2 —
+    // the documents the bench's synthetic qrels judge relevant
+    const uint32_t B = ((hl >> 20) & 1u) ? (uint32_t)((hl >> 32) % 3u)
+                                         : (uint32_t)((hl >> 32) % (uint64_t)P);
     const uint32_t pidx = (uint32_t)(((uint64_t)A * (uint64_t)i + B) % (uint64_t)P);
     d = (uint32_t)(((uint64_t)qg * (uint64_t)P + pidx) & 0x7FFFFFFFull);
   } else {

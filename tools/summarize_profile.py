@@ -34,5 +34,15 @@ for k, d in pmc.items():
                   "write_bytes": None if w is None else w * 1024,
                   "hbm_bytes": None if f is None or w is None else (f + w) * 1024,
                   "avg_ns": stats.get(k)}
+# qf_fuse = its join kernel + the sort kernels (every launch of one qf_fuse call)
+parts = [k for k in summary if "join_kernel" in k or "fuse_kernel" in k]
+if parts:
+    tot = lambda f: (None if any(summary[k][f] is None for k in parts)
+                     else sum(summary[k][f] for k in parts))
+    summary["qf_fuse (sum of its kernels)"] = {
+        "kernels": parts, "fetch_bytes": tot("fetch_bytes"), "write_bytes": tot("write_bytes"),
+        "hbm_bytes": tot("hbm_bytes"),
+        "avg_ns": None if any(summary[k]["avg_ns"] is None for k in parts)
+        else sum(summary[k]["avg_ns"] for k in parts)}
 (out / f"{tag}_pmc.json").write_text(json.dumps(summary, indent=1))
 print(json.dumps(summary, indent=1))
