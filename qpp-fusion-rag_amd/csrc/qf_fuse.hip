@@ -401,6 +401,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t q = blockIdx.x;
   if (q >= p.n_queries) return;
+  QF_STAMP_INIT();
   const int R = p.R;
   if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
   if (tid == 0) s_status = 0;
@@ -438,6 +439,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     sc[j] = e < N ? ScoreIn<KIND>::load(p.score, base + e) : 0.0;
   }
   __syncthreads();
+  QF_STAMP(3);
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
   int status = 0;
   uint32_t rj[ITEMS];
@@ -473,6 +475,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   }
   if (status) atomicMin(&s_status, status);
   __syncthreads();
+  QF_STAMP(4);
   // ---- number distinct documents in first-seen order; size their groups ------
   uint32_t repm = 0u;
 #pragma unroll
@@ -511,6 +514,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     if (lane == 0) s_U = (int)c1;
   }
   __syncthreads();
+  QF_STAMP(5);
   const int U = s_U;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -545,6 +549,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     }
   }
   __syncthreads();  // the hash table is dead; its LDS becomes the groups
+  QF_STAMP(6);
   double* gsc = (double*)(smem + C::kGscOff);
   uint32_t* gpr = (uint32_t*)(smem + C::kGprOff);
   uint16_t* ugo = (uint16_t*)(smem + C::kGoOff);
@@ -559,6 +564,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     }
   }
   __syncthreads();
+  QF_STAMP(7);
   // ---- fused score of every document, every requested method ------------------
   const int methods = p.methods, rrf_k = p.rrf_k;
   int slot[6];
@@ -595,6 +601,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     if (methods & QF_WRRF) out[slot[5] * st] = a5;
   }
   if (tid == 0) p.union_count[q] = s_status ? s_status : U;
+  QF_STAMP(14);
 }
 
 // ============================================================================

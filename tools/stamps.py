@@ -42,4 +42,8 @@ for ms in (["rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"
     tot = st[:, :3].sum(1).mean()
     out["+".join(ms)] = {"cycles_per_block": round(tot),
                          **{n: round(float(st[:, i].mean())) for i, n in enumerate(names)}}
+    js = buf.reshape(NB, NS)[:Q].astype(np.float64)
+    jn = {3: "join:load+init", 4: "join:insert", 5: "join:reps+scans", 6: "join:placement",
+          7: "join:groups", 14: "join:sums+write"}
+    out["join " + "+".join(ms)] = {v: round(float(js[:, k].mean())) for k, v in jn.items()}
 print(json.dumps(out, indent=1))
