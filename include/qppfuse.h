@@ -50,7 +50,12 @@ extern "C" {
 #define QF_WCOMBSUM (1 << 3) /* weighted_combsum          src/fusion.py:237-281 */
 #define QF_WCOMBMNZ (1 << 4) /* weighted_combmnz          src/fusion.py:284-330 */
 #define QF_WRRF     (1 << 5) /* weighted_rrf              src/fusion.py:333-380 */
-#define QF_ALL_METHODS 0x3F
+#define QF_LEARNED  (1 << 6) /* learned_fusion's sum      src/fusion.py:436-446:
+                                sum of score * w per (qid, docno) in pandas'
+                                groupby-sum (Kahan) order; ties by docno.  Takes
+                                its weights (qf_learned_weights) in `weights`, so
+                                it cannot share a call with the W-* methods. */
+#define QF_ALL_METHODS 0x3F  /* the six fusions of config.fusion.methods */
 
 /* ---- score column encodings --------------------------------------------- */
 #define QF_SCORE_F64   0 /* double                                              */
@@ -142,6 +147,34 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
             int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
             uint16_t* perm, double* fused, int64_t out_stride, void* stream);
+
+/*
+ * LightGBM inference for learned fusion (src/fusion.py:415-429 ->
+ * MultiOutputLGBM / PerRetrieverLGBM .predict, src/models/lightgbm_models.py):
+ * out[row*n_boosters + b] = raw prediction of booster b on X[row*n_features ..]
+ * (its first best_iteration trees).  The model is flat arrays (qppfuse/lgbm.py
+ * pack_model): trees of booster b = [tree_off[b], tree_off[b+1]); internal nodes
+ * of tree t = [node_off[t], node_off[t+1]) with feature / threshold /
+ * decision_type (LightGBM bits: 2 = default left, (d >> 2) & 3 = missing type)
+ * / left / right (child >= 0: node, < 0: leaf ~child); leaves of tree t =
+ * leaf_value[leaf_off[t] ..].  Numerical splits only.  All pointers device.
+ */
+int qf_gbdt_predict(int64_t n_rows, const double* X, int32_t n_features, int32_t n_boosters,
+                    const int32_t* tree_off, const int32_t* node_off, const int32_t* leaf_off,
+                    const int32_t* feature, const double* threshold,
+                    const int32_t* decision_type, const int32_t* left, const int32_t* right,
+                    const double* leaf_value, double* out, void* stream);
+
+/*
+ * Learned weights (src/models/base.py:120-125 _normalize_weights, then
+ * src/fusion.py:431-440): per query clip the n_boosters predictions at 0,
+ * divide by their numpy row sum (1 when 0); run r gets the weight of booster
+ * run_to_booster[r] (HOST array, n_runs <= 16), or 1/n_boosters when it is -1
+ * (a run the model does not know).  w_out[q*n_runs + r] feeds qf_fuse(QF_LEARNED).
+ */
+int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters,
+                       int32_t n_runs, const int32_t* run_to_booster, double* w_out,
+                       void* stream);
 
 /* ---- IR evaluation (trec_eval semantics, as ir_measures computes them) ---- */
 #define QF_EVAL_NDCG 0 /* nDCG@k   */

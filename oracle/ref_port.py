@@ -305,3 +305,21 @@ def qpp_file_text(results: Dict[str, List[float]]) -> str:
     for qid in sorted(results.keys(), key=lambda x: int(x) if x.isdigit() else x):
         lines.append(f"{qid}\t" + "\t".join(f"{s:.6f}" for s in results[qid]) + "\n")
     return "".join(lines)
+
+
+def learned_fusion_from_weights(runs: Dict[str, pd.DataFrame], weights_dict, n_retrievers: int):
+    """learned_fusion after the model step, src/fusion.py:436-448, with the same
+    pandas calls (row-wise apply, concat, groupby-sum, iterrows)."""
+    all_dfs = []
+    for ranker, df in runs.items():
+        df_copy = df[["qid", "docno", "score"]].copy()
+        df_copy["weighted_score"] = df_copy.apply(
+            lambda row: row["score"] * weights_dict.get(row["qid"], {}).get(
+                ranker, 1.0 / n_retrievers), axis=1)
+        all_dfs.append(df_copy[["qid", "docno", "weighted_score"]])
+    combined = pd.concat(all_dfs, ignore_index=True)
+    aggregated = combined.groupby(["qid", "docno"])["weighted_score"].sum().reset_index()
+    fused = defaultdict(list)
+    for _, row in aggregated.iterrows():
+        fused[row["qid"]].append((row["docno"], row["weighted_score"]))
+    return dict(fused)

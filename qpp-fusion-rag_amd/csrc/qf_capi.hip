@@ -91,10 +91,12 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             int64_t out_stride, void* stream) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "qf_fuse: n_retrievers must be in [1, %d]", kMaxR);
-  if (methods <= 0 || (methods & ~QF_ALL_METHODS))
+  if (methods <= 0 || (methods & ~(QF_ALL_METHODS | QF_LEARNED)))
     return fail(QF_EINVAL, "qf_fuse: bad method mask 0x%x", methods);
-  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF)) && !weights)
+  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_LEARNED)) && !weights)
     return fail(QF_EINVAL, "qf_fuse: weighted method requested without weights");
+  if ((methods & QF_LEARNED) && (methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF)))
+    return fail(QF_EINVAL, "qf_fuse: QF_LEARNED and the W-* methods need different weights");
   if (score_kind != QF_SCORE_F64 && score_kind != QF_SCORE_MICRO)
     return fail(QF_EINVAL, "qf_fuse: bad score_kind %d", score_kind);
   if (max_entries > qf::fuse_max_entries())
@@ -152,6 +154,45 @@ int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,
   p.n_metrics = n_metrics;
   p.out = out;
   return check(qf::eval_launch(p, (hipStream_t)stream), "qf_eval");
+}
+
+int qf_gbdt_predict(int64_t n_rows, const double* X, int32_t n_features, int32_t n_boosters,
+                    const int32_t* tree_off, const int32_t* node_off, const int32_t* leaf_off,
+                    const int32_t* feature, const double* threshold,
+                    const int32_t* decision_type, const int32_t* left, const int32_t* right,
+                    const double* leaf_value, double* out, void* stream) {
+  if (n_rows < 0 || n_features <= 0 || n_boosters <= 0 || n_boosters > qf::kMaxBoosters)
+    return fail(QF_EINVAL, "qf_gbdt_predict: bad sizes (n_boosters must be in [1, %d])",
+                qf::kMaxBoosters);
+  if (n_rows == 0) return QF_OK;
+  if (!X || !tree_off || !node_off || !leaf_off || !feature || !threshold || !decision_type ||
+      !left || !right || !leaf_value || !out)
+    return fail(QF_EINVAL, "qf_gbdt_predict: null buffer");
+  qf::GbdtParams p{n_rows, X, n_features, n_boosters, tree_off, node_off, leaf_off, feature,
+                   threshold, decision_type, left, right, leaf_value, out};
+  return check(qf::gbdt_predict_launch(p, (hipStream_t)stream), "qf_gbdt_predict");
+}
+
+int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters,
+                       int32_t n_runs, const int32_t* run_to_booster, double* w_out,
+                       void* stream) {
+  if (n_queries < 0 || n_boosters <= 0 || n_boosters > qf::kMaxBoosters || n_runs <= 0 ||
+      n_runs > kMaxR || !run_to_booster)
+    return fail(QF_EINVAL, "qf_learned_weights: bad sizes");
+  qf::LearnedWeightParams p{};
+  for (int r = 0; r < n_runs; ++r) {
+    if (run_to_booster[r] < -1 || run_to_booster[r] >= n_boosters)
+      return fail(QF_EINVAL, "qf_learned_weights: run_to_booster[%d] out of range", r);
+    p.run_to_booster[r] = run_to_booster[r];
+  }
+  if (n_queries == 0) return QF_OK;
+  if (!pred || !w_out) return fail(QF_EINVAL, "qf_learned_weights: null buffer");
+  p.n_queries = n_queries;
+  p.pred = pred;
+  p.n_boosters = n_boosters;
+  p.n_runs = n_runs;
+  p.w_out = w_out;
+  return check(qf::learned_weights_launch(p, (hipStream_t)stream), "qf_learned_weights");
 }
 
 int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,

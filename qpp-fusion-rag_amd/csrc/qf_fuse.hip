@@ -567,14 +567,14 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   QF_STAMP(7);
   // ---- fused score of every document, every requested method ------------------
   const int methods = p.methods, rrf_k = p.rrf_k;
-  int slot[6];
-  for (int t = 0, c = 0; t < 6; ++t) {
+  int slot[7];
+  for (int t = 0, c = 0; t < 7; ++t) {
     slot[t] = c;
     c += (methods >> t) & 1;
   }
   for (int u = tid; u < U; u += BLOCK) {
     const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0, a6 = 0.0, c6 = 0.0;
     for (int k = gs; k < ge; ++k) {
       const double s = gsc[k];
       const uint32_t q2 = gpr[k];
@@ -589,6 +589,13 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
         const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
         a5 += s_w[r] / (double)(rrf_k + rk);
       }
+      if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
+        const double y = s * s_w[r] - c6;
+        const double t = a6 + y;
+        c6 = (t - a6) - y;
+        if (c6 != c6) c6 = 0.0;  // +-inf contributions (pandas GH#53606)
+        a6 = t;
+      }
     }
     const double cnt = (double)(ge - gs);  // CombMNZ: sum x count (src/fusion.py:327)
     double* out = p.fused + base + u;
@@ -599,6 +606,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     if (methods & QF_WCOMBSUM) out[slot[3] * st] = a2;
     if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
     if (methods & QF_WRRF) out[slot[5] * st] = a5;
+    if (methods & QF_LEARNED) out[slot[6] * st] = a6;
   }
   if (tid == 0) p.union_count[q] = s_status ? s_status : U;
   QF_STAMP(14);
@@ -624,22 +632,33 @@ struct SortShared {
   int flag[2];
   uint32_t wtot[16];
   unsigned long long kmin, kmax;
+  unsigned int dmin, dmax;
 };
 
 // Sort one (query, method slot): fused[ms][base .. base+U) in place + perm.
+// Ties keep first-seen order, or (by_docid: learned fusion, whose groupby
+// output is in docno order, src/fusion.py:443-446) docid order: LSD passes over
+// the docids first, then the score passes, all stable.
 template <class C>
 __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh, int ms, int U,
-                                         int64_t base) {
+                                         int64_t base, bool by_docid) {
   constexpr int ITEMS = C::kItems, WAVES = C::kWaves;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   QF_STAMP_INIT();
-  if (tid == 0) { sh.kmin = ~0ull; sh.kmax = 0ull; }
+  if (tid == 0) {
+    sh.kmin = ~0ull;
+    sh.kmax = 0ull;
+    sh.dmin = ~0u;
+    sh.dmax = 0u;
+  }
   __syncthreads();
   double* io = p.fused + (int64_t)ms * p.out_stride + base;  // unsorted fused[ms][u]
+  const uint32_t* udoc = p.union_docid + base;
   const int rows = (U + 64 * WAVES - 1) / (64 * WAVES);
   // ---- full keys of the join kernel's unsorted scores, their range -------------
   uint64_t item[ITEMS];
   uint64_t kmn = ~0ull, kmx = 0ull;
+  uint32_t dmn = ~0u, dmx = 0u;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rows + j) * 64 + lane;
@@ -648,27 +667,81 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
       item[j] = ~f64_asc_key(io[i]);  // ascending sort on ~key == descending score
       kmn = min(kmn, item[j]);
       kmx = max(kmx, item[j]);
+      if (by_docid) {
+        const uint32_t d = udoc[i];
+        dmn = min(dmn, d);
+        dmx = max(dmx, d);
+      }
     }
   }
   block_min_max(kmn, kmx, &sh.kmin, &sh.kmax, lane);
+  if (by_docid) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      dmn = min(dmn, (uint32_t)__shfl_xor((int)dmn, d, 64));
+      dmx = max(dmx, (uint32_t)__shfl_xor((int)dmx, d, 64));
+    }
+    if (lane == 0) {
+      atomicMin(&sh.dmin, dmn);
+      atomicMax(&sh.dmax, dmx);
+    }
+  }
   __syncthreads();
   const uint64_t kmin = sh.kmin, kmax = sh.kmax;
   SortCtx<ITEMS, WAVES> sx{(uint32_t*)(sh.smem + C::kHistOff),
                            (uint64_t*)(sh.smem + C::kItemOff), sh.wtot, sh.flag, io, kmin, U,
                            rows, lane, wid, tid};
-  // ---- items: window key | u ----------------------------------------------------
   const int hb = kmax > kmin ? 64 - __clzll((long long)(kmax - kmin)) : 0;
   const int lo = hb > kWindow ? hb - kWindow : 0;
+  if (by_docid && sh.dmax > sh.dmin) {
+    // ---- learned fusion: first into docid order ------------------------------------
+    const uint32_t dmin = sh.dmin;
+    const int db = 32 - __clz((int)(sh.dmax - dmin));
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const int i = (wid * rows + j) * 64 + lane;
-    item[j] = (((item[j] - kmin) >> lo) << 32) | (uint32_t)i;
+    for (int j = 0; j < ITEMS; ++j) item[j] = (uint64_t)((wid * rows + j) * 64 + lane);
+#pragma unroll 1
+    for (int s0 = 0; s0 < db; s0 += 8) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const int i = (wid * rows + j) * 64 + lane;
+        if (j < rows && i < U) {
+          const uint32_t u = (uint32_t)(item[j] & kUMask);
+          item[j] = ((uint64_t)(((udoc[u] - dmin) >> s0) & 0xFFu) << 32) | u;
+        }
+      }
+      count_scatter(sx, item, 0, true);
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {  // registers now hold docid order: re-key
+      const int i = (wid * rows + j) * 64 + lane;
+      if (j < rows && i < U) {
+        const uint32_t u = (uint32_t)(item[j] & kUMask);
+        item[j] = (((~f64_asc_key(io[u]) - kmin) >> lo) << 32) | u;
+      }
+    }
+  } else {
+    // ---- items: window key | u --------------------------------------------------
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int i = (wid * rows + j) * 64 + lane;
+      item[j] = (((item[j] - kmin) >> lo) << 32) | (uint32_t)i;
+    }
   }
   QF_STAMP(0);
-  if (hb > 0) sort_desc(sx, item, hb, lo);  // hb == 0: all keys equal, first-seen order
+  if (hb > 0) sort_desc(sx, item, hb, lo);  // hb == 0: all keys equal, order stands
   QF_STAMP(1);
   write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base, io);
   QF_STAMP(2);
+}
+
+// Method bit of output slot ms.
+__device__ __forceinline__ int slot_method(int methods, int ms) {
+  for (int t = 0, c = 0; t < 7; ++t)
+    if ((methods >> t) & 1) {
+      if (c == ms) return t;
+      ++c;
+    }
+  return 0;
 }
 
 // One workgroup per (query, method slot), the queries with U in [umin, UMAX].
@@ -685,7 +758,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   const int U = p.union_count[q];
   const int64_t base = p.list_off[q * p.R];  // both loads in flight together
   if (U < 0 || U > C::kUMax || U < umin) return;  // error / other pass
-  sort_one<C>(p, sh, ms, U, base);
+  sort_one<C>(p, sh, ms, U, base, slot_method(p.methods, ms) == 6);
 }
 
 // The same for the few large queries (U in [umin, UMAX]): a grid of one
@@ -716,7 +789,9 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
     for (int t = 0; t < n; ++t) {
       const int64_t id = c0 + s_list[t];
       const int64_t q = id / M;
-      sort_one<C>(p, sh, (int)(id % M), p.union_count[q], p.list_off[q * p.R]);
+      const int ms = (int)(id % M);
+      sort_one<C>(p, sh, ms, p.union_count[q], p.list_off[q * p.R],
+                  slot_method(p.methods, ms) == 6);
       __syncthreads();
     }
   }

@@ -48,6 +48,35 @@ struct EvalParams {
   double* out;
 };
 
+// LightGBM inference (qf_gbdt_predict) and learned weights (qf_learned_weights).
+constexpr int kMaxBoosters = 16;
+struct GbdtParams {
+  int64_t n_rows;
+  const double* X;
+  int32_t n_features;
+  int32_t n_boosters;
+  const int32_t* tree_off;
+  const int32_t* node_off;
+  const int32_t* leaf_off;
+  const int32_t* feature;
+  const double* threshold;
+  const int32_t* dtype;
+  const int32_t* left;
+  const int32_t* right;
+  const double* leaf_value;
+  double* out;
+};
+struct LearnedWeightParams {
+  int64_t n_queries;
+  const double* pred;
+  int32_t n_boosters;
+  int32_t n_runs;
+  int32_t run_to_booster[kMaxBoosters];
+  double* w_out;
+};
+hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st);
+hipError_t learned_weights_launch(const LearnedWeightParams& p, hipStream_t st);
+
 int fuse_max_entries();
 hipError_t eval_launch(const EvalParams& p, hipStream_t st);
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);

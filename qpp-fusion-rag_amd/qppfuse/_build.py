@@ -15,7 +15,7 @@ PKG_DIR = Path(__file__).resolve().parent
 ROOT = PKG_DIR.parent  # qpp-fusion-rag_amd/
 CSRC = ROOT / "csrc"
 LIB_PATH = PKG_DIR / "libqppfuse.so"
-SOURCES = ["qf_fuse.hip", "qf_qpp.hip", "qf_norm.hip", "qf_eval.hip", "qf_capi.hip"]
+SOURCES = ["qf_fuse.hip", "qf_qpp.hip", "qf_norm.hip", "qf_eval.hip", "qf_learn.hip", "qf_capi.hip"]
 HEADERS = ["qf_common.h", "qf_internal.h", "qf_log2_table.h"]
 ARCH = os.environ.get("QPPFUSE_ARCH", "gfx950")
 # -ffp-contract=off: the reference's arithmetic is sequential IEEE double; an

@@ -17,9 +17,9 @@ QF_QSTATUS = {-1: "query exceeds the fusion kernel's entry limit",
               -4: "reserved docid 0xFFFFFFFF",
               -5: "a docno repeats within one run list (unsupported)"}
 
-COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF = (1 << i for i in range(6))
+COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF, LEARNED = (1 << i for i in range(7))
 METHOD_BITS = {"combsum": COMBSUM, "combmnz": COMBMNZ, "rrf": RRF,
-               "wcombsum": WCOMBSUM, "wcombmnz": WCOMBMNZ, "wrrf": WRRF}
+               "wcombsum": WCOMBSUM, "wcombmnz": WCOMBMNZ, "wrrf": WRRF, "learned": LEARNED}
 SCORE_F64, SCORE_MICRO = 0, 1
 NORM_NONE, NORM_MINMAX = 0, 1
 QPP_COLS = 13
@@ -40,6 +40,9 @@ SIGNATURES = {
                           _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_eval": (C.c_int, [_i64, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp,
                           _i32, _i32, _vp, _vp, _vp, _vp]),
+    "qf_gbdt_predict": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _vp]),
+    "qf_learned_weights": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
 }
 

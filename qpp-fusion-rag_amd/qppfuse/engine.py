@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 
-_MNAMES = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+_MNAMES = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf", "learned"]
 
 
 def require_device() -> torch.device:
@@ -163,3 +163,29 @@ def synth_runs(q_begin: int, n_queries: int, n_retrievers: int, k: int, seed: in
               int(seed) & (2**64 - 1), float(p_shared), _ptr(list_off), _ptr(docid), _ptr(score),
               _stream())
     return list_off, docid[:E], score[:E]
+
+
+def gbdt_predict(X: torch.Tensor, packed) -> torch.Tensor:
+    """qf_gbdt_predict: [n_rows, n_boosters] raw predictions (qppfuse.lgbm.PackedModel)."""
+    dev = require_device()
+    if X.dtype != torch.float64 or X.dim() != 2 or X.shape[1] != packed.n_features:
+        raise ValueError(f"X must be float64 [n, {packed.n_features}]")
+    d = packed.to_device(dev)
+    out = torch.empty((X.shape[0], packed.n_boosters), dtype=torch.float64, device=dev)
+    _lib.call("qf_gbdt_predict", X.shape[0], _ptr(X.contiguous()), packed.n_features,
+              packed.n_boosters, _ptr(d["tree_off"]), _ptr(d["node_off"]), _ptr(d["leaf_off"]),
+              _ptr(d["feature"]), _ptr(d["threshold"]), _ptr(d["dtype"]), _ptr(d["left"]),
+              _ptr(d["right"]), _ptr(d["leaf_value"]), _ptr(out), _stream())
+    return out
+
+
+def learned_weights(pred: torch.Tensor, run_to_booster) -> torch.Tensor:
+    """qf_learned_weights: [Q * R] run weights from [Q, B] predictions."""
+    import numpy as np
+    dev = require_device()
+    rb = np.ascontiguousarray(run_to_booster, dtype=np.int32)
+    Q, B = pred.shape
+    w = torch.empty(Q * len(rb), dtype=torch.float64, device=dev)
+    _lib.call("qf_learned_weights", Q, _ptr(pred.contiguous()), B, len(rb), rb.ctypes.data,
+              _ptr(w), _stream())
+    return w

@@ -13,7 +13,8 @@ computed for every query by one launch of the HIP kernel qf_fuse
 {qid: [(docno, score), ...]} that materialises lists on access — in the order
 the reference returns them: score-descending for combsum/combmnz/rrf (ranx +
 _ranx_to_dict, src/fusion.py:469-477), first-seen order for the weighted
-methods (src/fusion.py:278-279).
+methods (src/fusion.py:278-279), docno order for learned_fusion (its pandas
+groupby, src/fusion.py:443-446).
 """
 from __future__ import annotations
 
@@ -103,7 +104,7 @@ class FusedRun(Mapping):
         self._udoc = union_docid
         self._perm = perm
         self._fused = fused
-        self.order = order  # "sorted" or "first_seen"
+        self.order = order  # "sorted", "first_seen" or "docno"
 
     def __len__(self):
         return len(self._qids)
@@ -131,7 +132,11 @@ class FusedRun(Mapping):
             return list(zip(docs.tolist(), s.tolist()))
         by_u = np.empty(n, dtype=np.float64)
         by_u[p] = s
-        docs = self._docnos[self._udoc[b:b + n]]
+        ids = self._udoc[b:b + n]
+        if self.order == "docno":  # ids are interned in docno order
+            o = np.argsort(ids, kind="stable")
+            ids, by_u = ids[o], by_u[o]
+        docs = self._docnos[ids]
         return list(zip(docs.tolist(), by_u.tolist()))
 
     def to_dict(self) -> Dict[str, List[Tuple[str, float]]]:
@@ -172,7 +177,10 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
     import torch
     engine.require_device()
     d = rs.to_device()
-    wd = None if weights is None else torch.from_numpy(weights).to(d["list_off"].device)
+    if weights is None or isinstance(weights, torch.Tensor):
+        wd = weights
+    else:
+        wd = torch.from_numpy(weights).to(d["list_off"].device)
     out = engine.fuse(d["list_off"], d["docid"], d["score"], rs.n_rankers, list(methods),
                       rrf_k=rrf_k, weights=wd, rank=d["rank"], max_entries=rs.max_entries())
     counts = out.union_count.cpu().numpy()[:rs.n_queries]
@@ -187,7 +195,8 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
     fused = out.fused.cpu().numpy()[:, :E]
     res = {}
     for m, name in enumerate(out.methods):
-        order = "sorted" if name in UNWEIGHTED else "first_seen"
+        order = ("sorted" if name in UNWEIGHTED else "docno" if name == "learned"
+                 else "first_seen")
         res[name] = FusedRun(rs.qids, rs.docnos, rs.query_base(), counts, udoc, perm[m],
                              fused[m], order)
     return res
@@ -251,11 +260,51 @@ def weighted_rrf(runs, qpp_data, qpp_index: int = None, k: int = None) -> FusedR
     return fuse_many(runs, ["wrrf"], qpp_data, qpp_index, k)["wrrf"]
 
 
-def learned_fusion(runs, qpp_data, model_path: str, retrievers: Optional[List[str]] = None):
-    """Learned (LightGBM / MLP) weights — SURVEY §8(f) "next", not in this build."""
-    raise NotImplementedError(
-        "learned_fusion (LightGBM inference on the QPP features) is the next row of the build "
-        "plan (SURVEY.md §8(f) #1); it is not implemented on MI355X yet")
+def learned_fusion(runs: Dict[str, pd.DataFrame], qpp_data, model_path: str,
+                   retrievers: Optional[List[str]] = None) -> FusedRun:
+    """Fusion with per-query weights from the learned LightGBM model (src/fusion.py:387-448).
+
+    The model pickle is read statically (qppfuse.lgbm: no unpickling); the 13·R
+    QPP features go through the boosters on device (qf_gbdt_predict), the
+    predictions are normalised as BaseFusionModel._normalize_weights does
+    (qf_learned_weights), and qf_fuse(QF_LEARNED) forms Σ score·w per document in
+    pandas' groupby-sum order.  Lists come back in docno order, as the
+    reference's groupby returns them."""
+    import torch
+    from . import lgbm
+    print(f"[fusion] Running learned fusion from {model_path}...")
+    key = (os.path.abspath(model_path), os.path.getmtime(model_path))
+    cached = _MODELS.get(key)
+    if cached is None:
+        model = lgbm.load_fusion_model(model_path)
+        cached = _MODELS[key] = (model, lgbm.pack_model(model))
+    model, packed = cached
+    retrievers = list(retrievers or model.retrievers)
+    n_qpp = model.n_qpp
+    if len(retrievers) != len(model.boosters):
+        raise ValueError(f"the model predicts {len(model.boosters)} weights but "
+                         f"{len(retrievers)} retrievers were given")
+    rs = _pack(runs)
+    Q = rs.n_queries
+    X = np.zeros((Q, n_qpp * len(retrievers)))  # src/fusion.py:421-427
+    for i, qid in enumerate(rs.qids):
+        qd = qpp_data.get(qid)
+        if qd is None:
+            continue
+        for j, retriever in enumerate(retrievers):
+            if retriever in qd:
+                X[i, j * n_qpp:(j + 1) * n_qpp] = qd[retriever][:n_qpp]
+    dev = engine.require_device()
+    pred = engine.gbdt_predict(torch.from_numpy(X).to(dev), packed)
+    run_to_booster = [retrievers.index(r) if r in retrievers else -1 for r in rs.rankers]
+    w = engine.learned_weights(pred, run_to_booster)
+    res = _launch(rs, ["learned"], config.fusion.rrf_k, w)
+    fused = res["learned"]
+    print(f"[fusion] Learned fusion done: {len(fused)} queries")
+    return fused
+
+
+_MODELS: Dict[tuple, tuple] = {}  # (path, mtime) -> (FusionModel, PackedModel)
 
 
 # ------------------------------------------------------------------ output ---

@@ -1,0 +1,116 @@
+"""Learned fusion on device vs the CPU restatement — needs an MI355X.
+
+LightGBM inference (qf_gbdt_predict), the weight normalisation
+(qf_learned_weights) and the fused lists / run file of learned_fusion are
+compared bit for bit with oracle/lgbm_oracle.py + oracle/ref_port.py (the
+reference's own pandas calls for the fusion step).
+"""
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from oracle import lgbm_oracle, ref_port
+from tests.test_lgbm_host import TOY
+
+pytestmark = pytest.mark.gpu
+
+GOLD = Path(__file__).resolve().parent / "golden" / "lgbm"
+NAMES = ["fusion_multioutput", "fusion_per_retriever"]
+
+
+def _model(name):
+    from qppfuse import lgbm
+    return lgbm.load_fusion_model(GOLD / f"nq_{name}.json.gz")
+
+
+def _X(rng, n, f):
+    X = rng.uniform(0, 1, (n, f))
+    X[rng.random((n, f)) < 0.15] = 0.0          # zero features (missing qpp -> 0)
+    X[rng.random((n, f)) < 0.05] = np.round(X[rng.random((n, f)) < 0.05].mean(), 6)
+    return X
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_gbdt_predict_matches_restatement(gpu, name):
+    from qppfuse import engine, lgbm
+    m = _model(name)
+    p = lgbm.pack_model(m)
+    rng = np.random.default_rng(7)
+    X = _X(rng, 600, p.n_features)
+    # values exactly on thresholds take the left branch
+    thr = p.threshold[:50]
+    X[:50, p.feature[:50]] = thr
+    got = engine.gbdt_predict(torch.from_numpy(X).to(gpu), p).cpu().numpy()
+    want = np.column_stack([lgbm_oracle.booster_predict(b, X) for b in m.boosters])
+    assert got.tobytes() == want.tobytes()
+
+
+def test_gbdt_missing_types_and_single_leaf_trees(gpu):
+    from qppfuse import engine, lgbm
+    b = lgbm.parse_lgbm_model(TOY)
+    m = lgbm.FusionModel("MultiOutputLGBM", ["a"], 3, [b])
+    p = lgbm.pack_model(m)
+    X = np.array([[0.4, 0.2, 1.0], [0.4, 0.3, 2.0], [0.6, 0.0, 1.5], [0.4, 0.0, 5.0],
+                  [0.4, 1e-36, 0.0], [np.nan, 0.3, np.nan], [-0.0, -1e-40, 1.5]])
+    got = engine.gbdt_predict(torch.from_numpy(X).to(gpu), p).cpu().numpy()[:, 0]
+    want = lgbm_oracle.booster_predict(b, X)
+    assert got.tobytes() == want.tobytes()
+
+
+def test_learned_weights_match_numpy(gpu):
+    from qppfuse import engine
+    rng = np.random.default_rng(3)
+    raw = rng.standard_normal((400, 5))
+    raw[:40] = -np.abs(raw[:40])
+    raw[40:60, 2] = 0.0
+    raw[60:70] = -0.0
+    rb = [4, -1, 0, 1, 2, 3]  # run order differs from model order; one unknown run
+    got = engine.learned_weights(torch.from_numpy(raw).to(gpu), rb).cpu().numpy().reshape(400, 6)
+    w = lgbm_oracle.normalize_weights(raw)
+    want = np.column_stack([w[:, j] if j >= 0 else np.full(400, 1.0 / 5) for j in rb])
+    assert got.tobytes() == want.tobytes()
+
+
+def _runs(rng, qids, rankers, k, overlap=0.6, ties=False):
+    frames = {}
+    for r in rankers:
+        rows = []
+        for q in qids:
+            pool = [f"d{q}_{i}" for i in range(2 * k)]
+            docs = list(rng.choice(pool, size=k, replace=False)) if rng.random() < overlap else \
+                [f"x{r}_{q}_{i}" for i in range(k)]
+            sc = np.sort(rng.uniform(0, 1, k))[::-1]
+            if ties:
+                sc = np.round(sc * 4) / 4
+            sc = np.round(sc, 6)
+            rows += [(q, d, i + 1, float(s)) for i, (d, s) in enumerate(zip(docs, sc))]
+        df = pd.DataFrame(rows, columns=["qid", "docno", "rank", "score"])
+        df.insert(1, "iter", "Q0")
+        df["runid"] = r
+        frames[r] = df
+    return frames
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("ties", [False, True])
+def test_learned_fusion_matches_reference_pandas(gpu, name, ties, tmp_path, capsys):
+    from qppfuse import fusion
+    rng = np.random.default_rng(11 if ties else 12)
+    model = _model(name)
+    qids = [f"test{i}" for i in range(60)]
+    rankers = ["Splade", "BM25", "BGE", "BM25_TCT", "BM25_MonoT5", "Extra"]  # listdir-like order
+    runs = _runs(rng, qids, rankers, 40, ties=ties)
+    qpp = {q: {r: [float(np.round(v, 6)) for v in rng.uniform(0, 1, 13)]
+               for r in model.retrievers if rng.random() < 0.9} for q in qids[:-3]}
+    got = fusion.learned_fusion(runs, qpp, str(GOLD / f"nq_{name}.json.gz"))
+    wd = lgbm_oracle.weights_dict(runs, qpp, model)
+    want = ref_port.learned_fusion_from_weights(runs, wd, len(model.retrievers))
+    assert list(got.keys()) == sorted(want.keys())
+    for q in want:
+        assert got[q] == want[q], q
+    p = tmp_path / "learned.res"
+    fusion.write_runfile(got, str(p), "learned")
+    assert p.read_text() == ref_port.runfile_text(want, "learned")
