@@ -15,8 +15,8 @@
 //   first best_iteration trees (LightGBM NumericalDecision; see qppfuse/lgbm.py)
 //   and adds the leaf values in tree order from 0.0, as GBDT::PredictRaw does.
 //   The model (≈4.5 k nodes for the reference's NQ model) stays in L1/L2.
-// learned_weights_kernel — one thread per query: numpy's clip (np.maximum:
-//   -0.0 and NaN kept), numpy's row sum (0.0 + pairwise_sum: sequential below 8
+// learned_weights_kernel — one thread per query: numpy's clip (NaN kept, -0.0
+//   becomes +0.0 — measured on numpy 2.2), numpy's row sum (0.0 + pairwise_sum: sequential below 8
 //   values, 8 accumulators from 8), the zero guard and the division.
 #include <math.h>
 
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void learned_weights_kernel(LearnedWeightParam
   double c[kMaxBoosters];
   for (int b = 0; b < p.n_boosters; ++b) {
     const double v = p.pred[q * p.n_boosters + b];
-    c[b] = (v >= 0.0 || isnan(v)) ? v : 0.0;  // np.clip(pred, 0, None) == np.maximum(pred, 0)
+    c[b] = (v > 0.0 || isnan(v)) ? v : 0.0;  // np.clip(pred, 0, None): NaN kept, -0.0 -> +0.0
   }
   double s = 0.0 + np_pairwise_sum(c, p.n_boosters);  // the reduction starts from 0.0
   if (s == 0.0) s = 1.0;
