@@ -52,5 +52,12 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     return LIB_PATH
 
 
+def build_variant(out: Path, extra_flags) -> Path:
+    """Development builds (e.g. -DQF_STAMPS for tools/stamps.py) from the same sources."""
+    cmd = [_hipcc(), *FLAGS, *extra_flags, "-o", str(out)] + [str(CSRC / s) for s in SOURCES]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 if __name__ == "__main__":
     build(force=True)
