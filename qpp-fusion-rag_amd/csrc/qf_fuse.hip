@@ -53,16 +53,22 @@ __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 // Score as stored: int32 micro-units (exact "%.6f" text) or double.
 template <int KIND>
 struct ScoreIn {
-  static __device__ __forceinline__ double load(const void* p, int64_t i) {
+  using raw_t = double;
+  static __device__ __forceinline__ raw_t raw(const void* p, int64_t i) {
     return ((const double*)p)[i];
   }
+  static __device__ __forceinline__ double val(raw_t r) { return r; }
+  static __device__ __forceinline__ double load(const void* p, int64_t i) { return raw(p, i); }
 };
 template <>
 struct ScoreIn<1> {
-  // m / 1e6 is the nearest double to the "%.6f" text, i.e. pandas' parse.
-  static __device__ __forceinline__ double load(const void* p, int64_t i) {
-    return (double)((const int32_t*)p)[i] / 1e6;
+  using raw_t = int32_t;
+  static __device__ __forceinline__ raw_t raw(const void* p, int64_t i) {
+    return ((const int32_t*)p)[i];
   }
+  // m / 1e6 is the nearest double to the "%.6f" text, i.e. pandas' parse.
+  static __device__ __forceinline__ double val(raw_t r) { return (double)r / 1e6; }
+  static __device__ __forceinline__ double load(const void* p, int64_t i) { return val(raw(p, i)); }
 };
 
 // ---- block-level helpers ------------------------------------------------------
@@ -373,30 +379,46 @@ __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
 // ============================================================================
 // join_kernel
 // ============================================================================
-template <int BLOCK, int ITEMS, int TB>
+template <int BLOCK, int ITEMS, int TB, int MINW = 1>
 struct JoinCfg {
-  static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64;
+  static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64, kMinWaves = MINW;
   static constexpr int kNMax = BLOCK * ITEMS, kTS = 1 << TB, kTB = TB;
-  // LDS: the hash table (tkey, tmask: u32 [TS] each), later overlaid by the
-  // grouped contributions gsc f64 [NMAX], gpr u32 [NMAX] and group starts u16 [NMAX]
-  static constexpr int kGscOff = 0, kGprOff = 8 * kNMax, kGoOff = 12 * kNMax;
-  static constexpr int kSmem = (8 * kTS > 14 * kNMax ? 8 * kTS : 14 * kNMax);
   static_assert(kTS >= kNMax, "hash table must hold every entry");
   static_assert(kNMax <= 65535, "u / group offsets are uint16");
-  static_assert(kSmem <= 160 * 1024, "LDS budget");
+};
+
+// LDS of the join: the hash table — tkey u32 [TS], retriever masks u16 [TS]
+// (packed two per word) — later overlaid by the grouped contributions: scores
+// as stored (int32 micro-units or f64) [NMAX], position | retriever u32 [NMAX],
+// group starts u16 [NMAX].  Micro-unit scores keep JoinM at 50 KB: 3 per CU.
+template <class C, int KIND>
+struct JoinLds {
+  using raw_t = typename ScoreIn<KIND>::raw_t;
+  static constexpr int kTable = 6 * C::kTS;
+  static constexpr int kGscOff = 0;
+  static constexpr int kGprOff = (int)sizeof(raw_t) * C::kNMax;
+  static constexpr int kGoOff = kGprOff + 4 * C::kNMax;
+  static constexpr int kGroups = kGoOff + 2 * C::kNMax;
+  static constexpr int kBytes = ((kTable > kGroups ? kTable : kGroups) + 15) & ~15;
+  static_assert(kBytes <= 160 * 1024, "LDS budget");
 };
 
 template <class C, int KIND>
-__global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_kernel(FuseParams p) {
   constexpr int BLOCK = C::kBlock, ITEMS = C::kItems, WAVES = C::kWaves;
   constexpr int NMAX = C::kNMax, TS = C::kTS;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[C::kSmem];
+  using L = JoinLds<C, KIND>;
+  using raw_t = typename L::raw_t;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[L::kBytes];
   __shared__ int64_t s_off[kRMax + 1];
   __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax];
   __shared__ int s_cnt[ITEMS * WAVES], s_gof[ITEMS * WAVES];
   __shared__ int s_U, s_status;
   uint32_t* tkey = (uint32_t*)smem;
-  uint32_t* tmask = (uint32_t*)(smem + 4 * TS);
+  uint32_t* tmask2 = (uint32_t*)(smem + 4 * TS);  // two u16 masks per word
+  auto mask_of = [&](uint32_t slot) -> uint32_t {
+    return (tmask2[slot >> 1] >> ((slot & 1u) * 16u)) & 0xFFFFu;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t q = blockIdx.x;
@@ -426,17 +448,17 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     s_min[tid] = mn;
     s_den[tid] = mx - mn;
   }
-  for (int i = tid * 4; i < TS; i += BLOCK * 4) {
+  for (int i = tid * 4; i < TS; i += BLOCK * 4)
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
-    *(uint4*)&tmask[i] = make_uint4(0u, 0u, 0u, 0u);
-  }
+  for (int i = tid * 4; i < TS / 2; i += BLOCK * 4)
+    *(uint4*)&tmask2[i] = make_uint4(0u, 0u, 0u, 0u);
   uint32_t dk[ITEMS];
-  double sc[ITEMS];
+  raw_t sc[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {  // all loads in flight before the first use
     const int e = j * BLOCK + tid;
     dk[j] = e < N ? p.docid[base + e] : kEmpty;
-    sc[j] = e < N ? ScoreIn<KIND>::load(p.score, base + e) : 0.0;
+    sc[j] = e < N ? ScoreIn<KIND>::raw(p.score, base + e) : (raw_t)0;
   }
   __syncthreads();
   QF_STAMP(3);
@@ -446,6 +468,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
+    const raw_t nxt = __shfl_down(sc[j], 1, 64);  // entry e + 1, but at lane 63
     rj[j] = 0u;
     if (e < N) {
       const uint32_t d = dk[j];
@@ -459,15 +482,17 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
         if (prev == kEmpty || prev == d) break;
         h = (h + 1) & (TS - 1);
       }
-      const uint32_t old = atomicOr(&tmask[h], 1u << r);
-      if ((old >> r) & 1u) status = QF_QSTATUS_DUPDOC;
+      const uint32_t hs = (h & 1u) * 16u;
+      const uint32_t old = atomicOr(&tmask2[h >> 1], (1u << r) << hs);
+      if ((old >> (hs + r)) & 1u) status = QF_QSTATUS_DUPDOC;
       dk[j] = h;  // keep the slot
       // preconditions of the ranx methods / W-RRF (checked once, here)
       const int64_t g = base + e;
       if (g + 1 < s_off[r + 1]) {
-        if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
-            ScoreIn<KIND>::load(p.score, g + 1) > sc[j])
-          status = QF_QSTATUS_UNSORTED;
+        if (p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) {
+          const raw_t nx = lane == 63 ? ScoreIn<KIND>::raw(p.score, g + 1) : nxt;
+          if (ScoreIn<KIND>::val(nx) > ScoreIn<KIND>::val(sc[j])) status = QF_QSTATUS_UNSORTED;
+        }
         if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
           status = QF_QSTATUS_RANKORDER;
       }
@@ -484,7 +509,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     uint32_t pc = 0u;
     bool rep = false;
     if (e < N) {
-      const uint32_t msk = tmask[dk[j]];
+      const uint32_t msk = mask_of(dk[j]);
       rep = (uint32_t)(__ffs(msk) - 1) == rj[j];
       pc = rep ? (uint32_t)__popc(msk) : 0u;
     }
@@ -522,7 +547,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     const uint64_t b = ballot(rep);
     uint32_t msk = 0u, pc = 0u;
     if (rep) {
-      msk = tmask[dk[j]];
+      msk = mask_of(dk[j]);
       pc = (uint32_t)__popc(msk);
     }
     const uint32_t gpre = wave_incl_scan_dpp(pc) - pc;
@@ -530,8 +555,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
       const uint32_t u = (uint32_t)s_cnt[j * WAVES + wid] + mbcnt(b);
       const uint32_t go = (uint32_t)s_gof[j * WAVES + wid] + gpre;
       p.union_docid[base + u] = tkey[dk[j]];
-      tkey[dk[j]] = u;                    // slot -> u
-      tmask[dk[j]] = go | (msk << 16);    // slot -> group offset | retriever mask
+      tkey[dk[j]] = go | (u << 16);  // slot -> group offset | u (the docid is dead)
     }
   }
   __syncthreads();
@@ -541,18 +565,18 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
     if (e < N) {
-      const uint32_t gm = tmask[dk[j]];
+      const uint32_t gu = tkey[dk[j]];
       const uint32_t r = rj[j];
-      const uint32_t k = (gm & 0xFFFFu) + (uint32_t)__popc((gm >> 16) & ((1u << r) - 1u));
-      const uint32_t u = ((repm >> j) & 1u) ? tkey[dk[j]] : 0u;
+      const uint32_t k = (gu & 0xFFFFu) + (uint32_t)__popc(mask_of(dk[j]) & ((1u << r) - 1u));
+      const uint32_t u = ((repm >> j) & 1u) ? gu >> 16 : 0u;
       dk[j] = k | (u << 16);
     }
   }
   __syncthreads();  // the hash table is dead; its LDS becomes the groups
   QF_STAMP(6);
-  double* gsc = (double*)(smem + C::kGscOff);
-  uint32_t* gpr = (uint32_t*)(smem + C::kGprOff);
-  uint16_t* ugo = (uint16_t*)(smem + C::kGoOff);
+  raw_t* gsc = (raw_t*)(smem + L::kGscOff);
+  uint32_t* gpr = (uint32_t*)(smem + L::kGprOff);
+  uint16_t* ugo = (uint16_t*)(smem + L::kGoOff);
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
@@ -576,7 +600,7 @@ __global__ __launch_bounds__(C::kBlock) void join_kernel(FuseParams p) {
     const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0, a6 = 0.0, c6 = 0.0;
     for (int k = gs; k < ge; ++k) {
-      const double s = gsc[k];
+      const double s = ScoreIn<KIND>::val(gsc[k]);
       const uint32_t q2 = gpr[k];
       const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
       if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // ranx min-max normalised score
@@ -799,7 +823,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 
 // ---- launch -----------------------------------------------------------------
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
-using JoinM = JoinCfg<512, 10, 13>;   // N <= 5120
+using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
 using SortS = SortCfg<256, 4, 4>;     // U <= 1024
 using SortM = SortCfg<512, 6, 8>;     // U <= 3072

@@ -45,5 +45,8 @@ for ms in (["rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"
     js = buf.reshape(NB, NS)[:Q].astype(np.float64)
     jn = {3: "join:load+init", 4: "join:insert", 5: "join:reps+scans", 6: "join:placement",
           7: "join:groups", 14: "join:sums+write"}
-    out["join " + "+".join(ms)] = {v: round(float(js[:, k].mean())) for k, v in jn.items()}
+    # persistent join workgroups accumulate over their queries: per-query means
+    out["join " + "+".join(ms)] = {v: round(float(js[:, k].sum() / Q)) for k, v in jn.items()}
+Path("gpurun_out").mkdir(exist_ok=True)
+Path("gpurun_out/stamps.json").write_text(json.dumps(out, indent=1))
 print(json.dumps(out, indent=1))
