@@ -403,8 +403,10 @@ struct JoinLds {
   static_assert(kBytes <= 160 * 1024, "LDS budget");
 };
 
+// f64 scores need 72 KB of LDS (2 per CU), so only micro-unit scores aim higher
 template <class C, int KIND>
-__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_kernel(FuseParams p) {
+__global__ __launch_bounds__(C::kBlock, KIND == 1 ? C::kMinWaves : (C::kMinWaves < 4 ? C::kMinWaves : 4))
+void join_kernel(FuseParams p) {
   constexpr int BLOCK = C::kBlock, ITEMS = C::kItems, WAVES = C::kWaves;
   constexpr int NMAX = C::kNMax, TS = C::kTS;
   using L = JoinLds<C, KIND>;
