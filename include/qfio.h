@@ -1,0 +1,75 @@
+/*
+ * qfio.h — host-side TREC run I/O for the fusion path (libqfio.so, C++/OpenMP).
+ *
+ * The reference reads runs with pandas (load_runs, src/fusion.py:46-76:
+ * read_csv(sep=r"\s+", names=[qid, iter, docno, rank, score, runid], qid and
+ * docno as str)) and writes fused runs with a Python loop (write_runfile,
+ * src/fusion.py:480-492).  These entry points do the same work natively and
+ * produce the packed layout of include/qppfuse.h directly.  Host pointers only.
+ */
+#ifndef QFIO_H
+#define QFIO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QFIO_OK     0
+#define QFIO_EINVAL 1
+#define QFIO_ENOENT 2 /* a file cannot be opened (FileNotFoundError)  */
+#define QFIO_EIO    3
+#define QFIO_EPARSE 4 /* a line is not "qid Q0 docno rank score tag" */
+
+typedef struct qfio_runset qfio_runset;
+
+const char* qfio_last_error(void);
+
+/*
+ * Parse n_files run files (one run each, in the given order = the runs dict
+ * order) with n_threads threads (<= 0: OpenMP default).  Queries are the
+ * sorted distinct qids, docnos are interned in byte (= Python str) order; the
+ * CSR list (q, r) holds file r's rows of query q in file order.
+ */
+int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
+                   qfio_runset** out);
+/* sizes[8]: n_queries, n_docnos, n_entries, qid bytes, docno bytes,
+ * micro_ok (every score is an exact 6-decimal number), n_iter | n_tag << 32,
+ * iter bytes | tag bytes << 32 */
+void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes);
+/* CSR: list_off[Q*R+1], docid[E], score[E], micro[E] (nullable; only if
+ * micro_ok), rank[E] (file rank column) */
+int qfio_runset_csr(const qfio_runset* rs, int64_t* list_off, uint32_t* docid, double* score,
+                    int32_t* micro, int64_t* rank);
+/* interned strings: offsets [n+1] + concatenated bytes, for qids, docnos, the
+ * iter column and the tag column */
+int qfio_runset_strings(const qfio_runset* rs, int64_t* qid_off, char* qid_chars,
+                        int64_t* docno_off, char* docno_chars, int64_t* iter_off,
+                        char* iter_chars, int64_t* tag_off, char* tag_chars);
+/* rows of every file in file order (the DataFrames load_runs returns):
+ * file_off[R+1], codes into qids / docnos / iters / tags, rank, score */
+int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, uint32_t* docid,
+                     uint32_t* iter, uint32_t* tag, int64_t* rank, double* score);
+void qfio_runset_free(qfio_runset* rs);
+
+/* Python's f"{x:.6f}" of x into out (>= 400 bytes); returns the length. */
+size_t qfio_format_score(double x, char* out);
+
+/*
+ * write_runfile for one fused run (qf_fuse outputs copied to the host):
+ * queries order[0..n_out) (indices into qbase / counts / qid strings), for each
+ * its counts[q] documents union_docid[qbase[q] + perm[qbase[q] + k]] with rank
+ * k + 1 and score fused[qbase[q] + k]; one line "qid Q0 docno rank score tag".
+ */
+int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
+                   const int32_t* counts, const uint32_t* union_docid, const uint16_t* perm,
+                   const double* fused, const int64_t* qid_off, const char* qid_chars,
+                   const int64_t* docno_off, const char* docno_chars, const char* tag,
+                   int32_t n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QFIO_H */

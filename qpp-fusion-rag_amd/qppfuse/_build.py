@@ -15,6 +15,8 @@ PKG_DIR = Path(__file__).resolve().parent
 ROOT = PKG_DIR.parent  # qpp-fusion-rag_amd/
 CSRC = ROOT / "csrc"
 LIB_PATH = PKG_DIR / "libqppfuse.so"
+IO_LIB_PATH = PKG_DIR / "libqfio.so"  # host run-file I/O (C++ / OpenMP)
+IO_SOURCES = ["qf_io.cpp"]
 SOURCES = ["qf_fuse.hip", "qf_qpp.hip", "qf_norm.hip", "qf_eval.hip", "qf_learn.hip", "qf_capi.hip"]
 HEADERS = ["qf_common.h", "qf_internal.h", "qf_log2_table.h"]
 ARCH = os.environ.get("QPPFUSE_ARCH", "gfx950")
@@ -38,8 +40,26 @@ def _stale() -> bool:
     return any(d.exists() and d.stat().st_mtime > t for d in deps)
 
 
+def build_io(force: bool = False, verbose: bool = True) -> Path:
+    """Compile the host I/O library qppfuse/libqfio.so (g++, OpenMP)."""
+    deps = [CSRC / s for s in IO_SOURCES] + [ROOT.parent / "include" / "qfio.h"]
+    if not force and IO_LIB_PATH.exists() and all(
+            d.stat().st_mtime <= IO_LIB_PATH.stat().st_mtime for d in deps if d.exists()):
+        return IO_LIB_PATH
+    cxx = os.environ.get("CXX", shutil.which("g++") or "g++")
+    tmp = IO_LIB_PATH.with_suffix(".so.tmp")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-o", str(tmp)] + \
+        [str(CSRC / s) for s in IO_SOURCES]
+    if verbose:
+        print("[qppfuse] " + " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, IO_LIB_PATH)
+    return IO_LIB_PATH
+
+
 def build(force: bool = False, verbose: bool = True) -> Path:
-    """Compile every HIP source into qppfuse/libqppfuse.so (gfx950)."""
+    """Compile every HIP source into qppfuse/libqppfuse.so (gfx950), and libqfio.so."""
+    build_io(force, verbose)
     if not force and not _stale():
         return LIB_PATH
     cmd = [_hipcc(), *FLAGS, "-o", str(LIB_PATH)] + [str(CSRC / s) for s in SOURCES]

@@ -1,0 +1,183 @@
+"""Native TREC run I/O (libqfio.so, csrc/qf_io.cpp) for the fusion path.
+
+load_runs parses every run file in C++ (memory-mapped, multithreaded) straight
+into the packed RunSet the device kernels read, and also returns the
+DataFrames the reference's load_runs returns (src/fusion.py:46-76) — qid /
+docno / iter / runid as pandas categoricals over the interned strings, rank
+int64, score float64, rows in file order — with the RunSet cached for them, so
+the fusions that follow skip packing.  write_run writes one fused run the way
+write_runfile does (src/fusion.py:480-492), formatting in C++ with Python's
+exact "%.6f".
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import pandas as pd
+
+from ._build import IO_LIB_PATH
+
+_LIB = None
+_vp, _i32, _i64 = C.c_void_p, C.c_int32, C.c_int64
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = Path(os.environ.get("QPPFUSE_IO_LIB", IO_LIB_PATH))
+        if not path.exists():
+            raise ImportError(f"{path} is missing: build it with `python __graft_entry__.py build`")
+        L = C.CDLL(str(path))
+        L.qfio_last_error.restype = C.c_char_p
+        L.qfio_load_runs.restype = C.c_int
+        L.qfio_load_runs.argtypes = [C.POINTER(C.c_char_p), _i32, _i32, C.POINTER(_vp)]
+        L.qfio_runset_sizes.restype = None
+        L.qfio_runset_sizes.argtypes = [_vp, _vp]
+        L.qfio_runset_csr.restype = C.c_int
+        L.qfio_runset_csr.argtypes = [_vp] + [_vp] * 5
+        L.qfio_runset_strings.restype = C.c_int
+        L.qfio_runset_strings.argtypes = [_vp] + [_vp] * 8
+        L.qfio_runset_rows.restype = C.c_int
+        L.qfio_runset_rows.argtypes = [_vp] + [_vp] * 7
+        L.qfio_runset_free.restype = None
+        L.qfio_runset_free.argtypes = [_vp]
+        L.qfio_format_score.restype = C.c_size_t
+        L.qfio_format_score.argtypes = [C.c_double, C.c_char_p]
+        L.qfio_write_run.restype = C.c_int
+        L.qfio_write_run.argtypes = [C.c_char_p, _i64] + [_vp] * 10 + [C.c_char_p, _i32]
+        _LIB = L
+    return _LIB
+
+
+def _check(rc: int, what: str):
+    if rc == 0:
+        return
+    msg = lib().qfio_last_error().decode(errors="replace")
+    if rc == 2:
+        raise FileNotFoundError(msg)
+    if rc == 4:
+        raise ValueError(f"{what}: {msg}")
+    raise OSError(f"{what}: {msg}")
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_vp)
+
+
+def _strings(off: np.ndarray, chars: np.ndarray) -> np.ndarray:
+    """Offsets + bytes -> object array of str (one C-speed decode + split)."""
+    n = len(off) - 1
+    if n == 0:
+        return np.zeros(0, dtype=object)
+    total = int(off[-1])
+    blob = np.zeros(total + n, np.uint8)  # each string followed by a NUL
+    lens = np.diff(off)
+    blob[np.arange(total) + np.repeat(np.arange(n), lens)] = chars[:total]
+    parts = blob.tobytes().decode().split("\0")
+    out = np.empty(n, dtype=object)
+    out[:] = parts[:n]
+    return out
+
+
+def format_score(x: float) -> str:
+    buf = C.create_string_buffer(400)
+    n = lib().qfio_format_score(float(x), buf)
+    return buf.raw[:n].decode()
+
+
+def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
+    """Parse run files -> (RunSet, {name: DataFrame})."""
+    from .runset import RunSet
+    L = lib()
+    arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    h = _vp()
+    _check(L.qfio_load_runs(arr, len(paths), int(n_threads), C.byref(h)), "load_runs")
+    try:
+        sz = np.zeros(8, np.int64)
+        L.qfio_runset_sizes(h, _p(sz))
+        Q, D, E, qb, db, micro_ok = (int(x) for x in sz[:6])
+        n_iter, n_tag = int(sz[6]) & 0xFFFFFFFF, int(sz[6]) >> 32
+        ib, tb = int(sz[7]) & 0xFFFFFFFF, int(sz[7]) >> 32
+        R = len(paths)
+        list_off = np.zeros(Q * R + 1, np.int64)
+        docid = np.zeros(E, np.uint32)
+        score = np.zeros(E, np.float64)
+        micro = np.zeros(E, np.int32) if micro_ok else None
+        rank = np.zeros(E, np.int64)
+        L.qfio_runset_csr(h, _p(list_off), _p(docid), _p(score),
+                          None if micro is None else _p(micro), _p(rank))
+        qo, qc = np.zeros(Q + 1, np.int64), np.zeros(max(qb, 1), np.uint8)
+        do, dc = np.zeros(D + 1, np.int64), np.zeros(max(db, 1), np.uint8)
+        io, ic = np.zeros(n_iter + 1, np.int64), np.zeros(max(ib, 1), np.uint8)
+        to, tc = np.zeros(n_tag + 1, np.int64), np.zeros(max(tb, 1), np.uint8)
+        L.qfio_runset_strings(h, _p(qo), _p(qc), _p(do), _p(dc), _p(io), _p(ic), _p(to), _p(tc))
+        fo = np.zeros(R + 1, np.int64)
+        rq, rd = np.zeros(E, np.uint32), np.zeros(E, np.uint32)
+        ri, rt = np.zeros(E, np.uint32), np.zeros(E, np.uint32)
+        rr, rsc = np.zeros(E, np.int64), np.zeros(E, np.float64)
+        L.qfio_runset_rows(h, _p(fo), _p(rq), _p(rd), _p(ri), _p(rt), _p(rr), _p(rsc))
+    finally:
+        L.qfio_runset_free(h)
+    qids = _strings(qo, qc)
+    docnos = _strings(do, dc)
+    iters, tags = _strings(io, ic), _strings(to, tc)
+    rs = RunSet(qids=list(qids), rankers=list(names), docnos=docnos, list_off=list_off,
+                docid=docid, score=score, rank=rank, micro=micro)
+    lid = np.repeat(np.arange(Q * R, dtype=np.int64), np.diff(list_off))
+    same = lid[1:] == lid[:-1]
+    pos = np.arange(E, dtype=np.int64) - list_off[lid] if E else np.zeros(0, np.int64)
+    rs.rank_is_position = bool(np.array_equal(rank, pos + 1))
+    rs.canonical = bool(np.all(score[1:][same] <= score[:-1][same]) and
+                        np.all(rank[1:][same] > rank[:-1][same])) if E > 1 else True
+    rs._strtab = {"qid": (qo, qc.tobytes()), "docno": (do, dc.tobytes())}
+    qcat = pd.CategoricalDtype(pd.Index(qids, dtype=object))
+    dcat = pd.CategoricalDtype(pd.Index(docnos, dtype=object))
+    icat = pd.CategoricalDtype(pd.Index(iters, dtype=object))
+    tcat = pd.CategoricalDtype(pd.Index(tags, dtype=object))
+    frames = {}
+    for r, name in enumerate(names):
+        a, b = int(fo[r]), int(fo[r + 1])
+        frames[name] = pd.DataFrame({
+            "qid": pd.Categorical.from_codes(rq[a:b].astype(np.int64), dtype=qcat),
+            "iter": pd.Categorical.from_codes(ri[a:b].astype(np.int64), dtype=icat),
+            "docno": pd.Categorical.from_codes(rd[a:b].astype(np.int64), dtype=dcat),
+            "rank": rr[a:b], "score": rsc[a:b],
+            "runid": pd.Categorical.from_codes(rt[a:b].astype(np.int64), dtype=tcat)})
+    return rs, frames
+
+
+def string_table(rs, which: str) -> Tuple[np.ndarray, bytes]:
+    """(offsets [n+1], bytes) of a RunSet's qids or docnos (cached)."""
+    tab = getattr(rs, "_strtab", None)
+    if tab is None:
+        tab = rs._strtab = {}
+    if which not in tab:
+        vals = rs.qids if which == "qid" else rs.docnos
+        enc = [str(v).encode() for v in vals]
+        off = np.zeros(len(enc) + 1, np.int64)
+        np.cumsum([len(e) for e in enc], out=off[1:])
+        tab[which] = (off, b"".join(enc))
+    return tab[which]
+
+
+def write_run(path: str, order: np.ndarray, qbase: np.ndarray, counts: np.ndarray,
+              union_docid: np.ndarray, perm: np.ndarray, fused: np.ndarray, rs, tag: str,
+              n_threads: int = 0) -> None:
+    """One fused run -> TREC text (queries in `order`, documents as ranked)."""
+    qo, qc = string_table(rs, "qid")
+    do, dc = string_table(rs, "docno")
+    order = np.ascontiguousarray(order, np.int64)
+    qbase = np.ascontiguousarray(qbase, np.int64)
+    counts = np.ascontiguousarray(counts, np.int32)
+    ud = np.ascontiguousarray(union_docid, np.uint32)
+    pm = np.ascontiguousarray(perm, np.uint16)
+    fz = np.ascontiguousarray(fused, np.float64)
+    qcb = np.frombuffer(qc, np.uint8) if qc else np.zeros(1, np.uint8)
+    dcb = np.frombuffer(dc, np.uint8) if dc else np.zeros(1, np.uint8)
+    _check(lib().qfio_write_run(os.fsencode(path), len(order), _p(order), _p(qbase), _p(counts),
+                                _p(ud), _p(pm), _p(fz), _p(qo), _p(qcb), _p(do), _p(dcb),
+                                tag.encode(), int(n_threads)), "write_runfile")

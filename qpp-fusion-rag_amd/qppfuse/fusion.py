@@ -44,19 +44,20 @@ WEIGHTED = ("wcombsum", "wcombmnz", "wrrf")
 # ------------------------------------------------------------------ loading --
 
 def load_runs(res_path: str, use_normalized: bool = True) -> Dict[str, pd.DataFrame]:
-    """{ranker: DataFrame[qid, iter, docno, rank, score, runid]} in os.listdir order."""
+    """{ranker: DataFrame[qid, iter, docno, rank, score, runid]} in os.listdir order.
+
+    Parsed natively (qppfuse.fastio, csrc/qf_io.cpp) into the packed run set the
+    kernels read — cached for these frames, so the fusions skip packing.  The
+    string columns are pandas categoricals over the interned values."""
+    from . import fastio
     suffix = ".norm.res" if use_normalized else ".res"
     files = [f for f in os.listdir(res_path) if f.endswith(suffix)]
     if not files:
         raise FileNotFoundError(f"No {suffix} files found in {res_path}")
-    runs = {}
-    for f in files:
-        df = pd.read_csv(os.path.join(res_path, f), sep=r"\s+",
-                         names=["qid", "iter", "docno", "rank", "score", "runid"],
-                         dtype={"qid": str, "docno": str})
-        df["qid"] = df["qid"].astype(str)
-        runs[f.replace(suffix, "")] = df
-    return runs
+    names = [f.replace(suffix, "") for f in files]
+    rs, frames = fastio.parse_runs([os.path.join(res_path, f) for f in files], names)
+    _remember(frames, rs)
+    return frames
 
 
 def load_qpp_scores(qpp_path: str) -> Dict[str, Dict[str, List[float]]]:
@@ -95,7 +96,9 @@ def qid_sort_key(x: str):
 class FusedRun(Mapping):
     """{qid: [(docno, score)]} backed by the kernel's packed output arrays."""
 
-    def __init__(self, qids, docnos, qbase, counts, union_docid, perm, fused, order: str):
+    def __init__(self, qids, docnos, qbase, counts, union_docid, perm, fused, order: str,
+                 runset: Optional[RunSet] = None):
+        self._rs = runset
         self._qids = list(qids)
         self._index = {q: i for i, q in enumerate(self._qids)}
         self._docnos = docnos
@@ -148,16 +151,21 @@ class FusedRun(Mapping):
 _PACK_CACHE: Dict[tuple, RunSet] = {}
 
 
+def _remember(runs: Dict[str, pd.DataFrame], rs: RunSet) -> None:
+    key = tuple((name, id(df), len(df)) for name, df in runs.items())
+    _PACK_CACHE.clear()
+    _PACK_CACHE[key] = rs
+    for df in runs.values():
+        weakref.finalize(df, _PACK_CACHE.pop, key, None)
+
+
 def _pack(runs: Dict[str, pd.DataFrame]) -> RunSet:
     """Pack once per runs dict (cached on the frames' identity while they live)."""
     key = tuple((name, id(df), len(df)) for name, df in runs.items())
     rs = _PACK_CACHE.get(key)
     if rs is None:
         rs = pack_frames(runs)
-        _PACK_CACHE.clear()
-        _PACK_CACHE[key] = rs
-        for df in runs.values():
-            weakref.finalize(df, _PACK_CACHE.pop, key, None)
+        _remember(runs, rs)
     return rs
 
 
@@ -198,7 +206,7 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
         order = ("sorted" if name in UNWEIGHTED else "docno" if name == "learned"
                  else "first_seen")
         res[name] = FusedRun(rs.qids, rs.docnos, rs.query_base(), counts, udoc, perm[m],
-                             fused[m], order)
+                             fused[m], order, rs)
     return res
 
 
@@ -310,19 +318,24 @@ _MODELS: Dict[tuple, tuple] = {}  # (path, mtime) -> (FusionModel, PackedModel)
 # ------------------------------------------------------------------ output ---
 
 def write_runfile(fused: Mapping, output_path: str, tag: str = "fusion") -> None:
-    """TREC run file: qids by qid_sort_key, docs by score desc (stable), '%.6f' scores."""
+    """TREC run file: qids by qid_sort_key, docs by score desc (stable), '%.6f' scores.
+
+    A FusedRun is written by the native writer (qppfuse.fastio: csrc/qf_io.cpp)
+    straight from the kernel's ranked arrays; any other mapping as the
+    reference does it."""
+    if isinstance(fused, FusedRun) and fused._rs is not None:
+        from . import fastio
+        idx = fused._index
+        order = np.asarray([idx[q] for q in sorted(fused.keys(), key=qid_sort_key)], np.int64)
+        fastio.write_run(output_path, order, fused._qbase, fused._counts, fused._udoc,
+                         fused._perm, fused._fused, fused._rs, tag)
+        print(f"Wrote fused run to {output_path}")
+        return
     with open(output_path, "w") as fout:
         for qid in sorted(fused.keys(), key=qid_sort_key):
-            if isinstance(fused, FusedRun):
-                ids, scores = fused.arrays(qid)
-                docs = fused._docnos[ids].tolist()
-                scores = scores.tolist()
-                fout.write("".join(f"{qid} Q0 {d} {i} {s:.6f} {tag}\n"
-                                   for i, (d, s) in enumerate(zip(docs, scores), start=1)))
-            else:
-                ranked = sorted(fused[qid], key=lambda x: x[1], reverse=True)
-                fout.write("".join(f"{qid} Q0 {d} {i} {s:.6f} {tag}\n"
-                                   for i, (d, s) in enumerate(ranked, start=1)))
+            ranked = sorted(fused[qid], key=lambda x: x[1], reverse=True)
+            fout.write("".join(f"{qid} Q0 {d} {i} {s:.6f} {tag}\n"
+                               for i, (d, s) in enumerate(ranked, start=1)))
     print(f"Wrote fused run to {output_path}")
 
 

@@ -77,8 +77,8 @@ def _micro_encoding(score: np.ndarray) -> Optional[np.ndarray]:
     m = np.rint(score * 1e6)
     if np.any(np.abs(m) >= 2**31 - 1):
         return None
-    if not np.array_equal(m / 1e6, score):
-        return None
+    if not np.array_equal(m / 1e6, score) or np.any((score == 0) & np.signbit(score)):
+        return None  # a -0.0 score is not the micro-unit 0
     return m.astype(np.int32)
 
 

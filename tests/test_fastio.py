@@ -1,0 +1,156 @@
+"""Native run-file I/O (libqfio.so, csrc/qf_io.cpp) vs pandas / Python (CPU).
+
+The parser must produce exactly what read_csv + qppfuse.runset.pack_frames
+produce, and the writer exactly the bytes of write_runfile's f-strings
+(src/fusion.py:480-492), including Python's "%.6f" rounding.
+"""
+import math
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from qppfuse import fastio
+from qppfuse.runset import pack_frames
+
+
+def _write_runs(tmp_path, rng, n_runs=4, n_q=30, k=50, text_fmt="%.6f"):
+    names, paths = [], []
+    for r in range(n_runs):
+        name = f"Run{r}" if r != 2 else "BM25_MonoT5"
+        lines = []
+        for q in rng.permutation(n_q):  # queries interleaved in arbitrary file order
+            qid = f"test{q}" if q % 5 else f"q{q:03d}"
+            n = int(rng.integers(0, k))
+            docs = rng.choice(5 * k, size=n, replace=False)
+            sc = np.sort(rng.standard_normal(n) * 3)[::-1]
+            if r == 1:
+                sc = np.round(sc * 2) / 2  # ties
+            for i, (d, s) in enumerate(zip(docs, sc)):
+                docno = f"doc{d}" if d % 7 else f"Δ{d}"  # non-ASCII docnos
+                lines.append(f"{qid}\tQ0 {docno}  {i + 1} {text_fmt % s} tag{r}\n")
+        if r == 3:
+            lines.insert(3, "\n")  # a blank line
+        p = tmp_path / f"{name}.norm.res"
+        p.write_text("".join(lines))
+        names.append(name)
+        paths.append(str(p))
+    return names, paths
+
+
+def _pandas_frames(paths, names):
+    out = {}
+    for p, n in zip(paths, names):
+        df = pd.read_csv(p, sep=r"\s+", names=["qid", "iter", "docno", "rank", "score", "runid"],
+                         dtype={"qid": str, "docno": str})
+        df["qid"] = df["qid"].astype(str)
+        out[n] = df
+    return out
+
+
+@pytest.mark.parametrize("fmt", ["%.6f", "%.9g"])
+def test_parse_matches_pandas_and_pack(tmp_path, fmt):
+    rng = np.random.default_rng(1)
+    names, paths = _write_runs(tmp_path, rng, text_fmt=fmt)
+    rs, frames = fastio.parse_runs(paths, names, n_threads=3)
+    pf = _pandas_frames(paths, names)
+    ref = pack_frames(pf)
+    assert rs.qids == ref.qids and rs.rankers == ref.rankers
+    assert list(rs.docnos) == list(ref.docnos)
+    np.testing.assert_array_equal(rs.list_off, ref.list_off)
+    np.testing.assert_array_equal(rs.docid, ref.docid)
+    assert rs.score.tobytes() == ref.score.tobytes()
+    np.testing.assert_array_equal(rs.rank, ref.rank)
+    assert rs.canonical == ref.canonical and rs.rank_is_position == ref.rank_is_position
+    assert (rs.micro is None) == (ref.micro is None)
+    if rs.micro is not None:
+        np.testing.assert_array_equal(rs.micro, ref.micro)
+    for n in names:
+        a, b = frames[n], pf[n]
+        assert list(a.columns) == list(b.columns)
+        for c in ("qid", "iter", "docno", "runid"):
+            assert a[c].astype(str).tolist() == b[c].astype(str).tolist()
+        np.testing.assert_array_equal(a["rank"].to_numpy(), b["rank"].to_numpy())
+        assert a["score"].to_numpy().tobytes() == b["score"].to_numpy().tobytes()
+
+
+def test_micro_units_when_every_score_is_six_decimal_text(tmp_path):
+    p = tmp_path / "a.res"
+    p.write_text("q1 Q0 d1 1 0.123456 t\nq1 Q0 d2 2 -3 t\nq2 Q0 d1 1 12.5 t\n")
+    rs, _ = fastio.parse_runs([str(p)], ["a"])
+    assert rs.micro.tolist() == [123456, -3000000, 12500000]
+    p.write_text("q1 Q0 d1 1 0.000000 t\nq1 Q0 d2 2 -0.000000 t\n")  # -0.0 is no micro-unit
+    rs, _ = fastio.parse_runs([str(p)], ["a"])
+    assert rs.micro is None and math.copysign(1, rs.score[1]) < 0
+
+
+def test_threads_do_not_change_the_result(tmp_path):
+    rng = np.random.default_rng(2)
+    names, paths = _write_runs(tmp_path, rng, n_q=80)
+    a, _ = fastio.parse_runs(paths, names, n_threads=1)
+    b, _ = fastio.parse_runs(paths, names, n_threads=8)
+    np.testing.assert_array_equal(a.docid, b.docid)
+    np.testing.assert_array_equal(a.list_off, b.list_off)
+
+
+def test_parse_errors(tmp_path):
+    p = tmp_path / "bad.res"
+    p.write_text("q1 Q0 d1 1 0.5 t\nq1 Q0 d2 2 t\n")
+    with pytest.raises(ValueError, match="6 fields"):
+        fastio.parse_runs([str(p)], ["bad"])
+    with pytest.raises(FileNotFoundError):
+        fastio.parse_runs([str(tmp_path / "missing.res")], ["m"])
+
+
+def test_format_score_is_pythons_percent_6f():
+    rng = np.random.default_rng(3)
+    vals = list(rng.standard_normal(20000) * 10.0 ** rng.integers(-8, 9, 20000))
+    vals += [k / 128 for k in range(-300, 300)]            # exact decimal ties
+    vals += [(2 * k + 1) / 2e6 for k in range(-500, 500)]  # near ties
+    vals += [0.0, -0.0, -1e-9, 1e-9, -4.9999999e-7, 5e-7, 2.0 ** 33, -(2.0 ** 33) - 0.5,
+             1e15 + 0.125, 1.7976931348623157e308, 5e-324, math.inf, -math.inf, math.nan]
+    for x in vals:
+        assert fastio.format_score(x) == f"{x:.6f}", repr(x)
+
+
+def test_write_run_matches_python_writer(tmp_path):
+    from qppfuse.runset import RunSet
+    rng = np.random.default_rng(4)
+    Q, U = 25, 40
+    qids = [f"test{i}" for i in range(Q)]
+    docnos = np.array(sorted(f"d{i}" for i in range(300)), dtype=object)
+    counts = rng.integers(0, U, Q).astype(np.int32)
+    counts[3] = 0
+    qbase = np.arange(Q, dtype=np.int64) * U
+    ud = np.zeros(Q * U, np.uint32)
+    perm = np.zeros(Q * U, np.uint16)
+    fused = np.zeros(Q * U)
+    for q in range(Q):
+        n = counts[q]
+        ud[q * U:q * U + n] = rng.choice(300, n, replace=False)
+        perm[q * U:q * U + n] = rng.permutation(n)
+        fused[q * U:q * U + n] = np.sort(rng.standard_normal(n))[::-1]
+    fused[5] = -0.0
+    rs = RunSet(qids=qids, rankers=["a"], docnos=docnos, list_off=np.zeros(2, np.int64),
+                docid=np.zeros(0, np.uint32), score=np.zeros(0), rank=np.zeros(0, np.int64))
+    order = np.array(sorted(range(Q), key=lambda i: int(qids[i][4:])), np.int64)
+    out = tmp_path / "x.res"
+    fastio.write_run(str(out), order, qbase, counts, ud, perm, fused, rs, "tag-1")
+    want = []
+    for q in order:
+        for k in range(counts[q]):
+            d = docnos[ud[qbase[q] + perm[qbase[q] + k]]]
+            want.append(f"{qids[q]} Q0 {d} {k + 1} {fused[qbase[q] + k]:.6f} tag-1\n")
+    assert out.read_text() == "".join(want)
+
+
+def test_load_runs_returns_frames_and_caches_the_pack(tmp_path):
+    from qppfuse import fusion
+    rng = np.random.default_rng(5)
+    names, paths = _write_runs(tmp_path, rng)
+    frames = fusion.load_runs(str(tmp_path))
+    assert list(frames) == [f.replace(".norm.res", "") for f in os.listdir(tmp_path)
+                            if f.endswith(".norm.res")]
+    rs = fusion._pack(frames)
+    assert rs.n_entries == sum(len(df) for df in frames.values())
