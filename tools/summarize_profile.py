@@ -35,7 +35,7 @@ for k, d in pmc.items():
                   "hbm_bytes": None if f is None or w is None else (f + w) * 1024,
                   "avg_ns": stats.get(k)}
 # qf_fuse = its join kernel + the sort kernels (every launch of one qf_fuse call)
-parts = [k for k in summary if "join_kernel" in k or "fuse_kernel" in k]
+parts = [k for k in summary if any(s in k for s in ("join_kernel", "fuse_kernel", "fuse_large_kernel"))]
 if parts:
     tot = lambda f: (None if any(summary[k][f] is None for k in parts)
                      else sum(summary[k][f] for k in parts))
