@@ -5,18 +5,18 @@
 // per-column min-max normalisation (src/qpp.py:340-374) + "%.6f" write-back
 // (src/qpp.py:329-334) + get_qpp_weight (src/fusion.py:116-158).
 //
-// k = min(50, n) <= 64 values per list, so lane i holds rsv[i].  Java's
-// sequential summation order is reproduced exactly: every sum that Java forms
-// left-to-right is formed left-to-right here too (broadcast reads of rsv[j]
-// from LDS, j uniform), and every DoubleStream.average() is the JDK's
-// compensated (Kahan) sum.  Prefix statistics (SigmaMax, CumNQC) are lane
-// parallel: lane i owns prefix rsv[0..i].
+// k = min(50, n) <= 64 values per list.  A workgroup takes 8 lists, one wave
+// each: lane i holds rsv[i] for the per-element terms (every transcendental
+// runs once per element) and owns prefix rsv[0..i] for the prefix statistics
+// (SigmaMax, CumNQC).  Java's sequential summation order is reproduced
+// exactly: every sum Java forms left to right is a serial chain here too, and
+// every DoubleStream.average() is the JDK's compensated (Kahan) sum.  The
+// chains of the 8 lists run batched in one wave (lane = list x chain), so the
+// serial work costs one lane each, not a whole wave.
 #include "qf_common.h"
 #include "qf_internal.h"
 
 namespace qf {
-
-constexpr int kQppBlock = 256;  // 4 lists per workgroup
 
 // v of lane l (l wave-uniform) as a scalar: two v_readlane_b32.
 __device__ __forceinline__ double readlane_f64(double v, int l) {
@@ -25,55 +25,70 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-// Java's left-to-right sum of t[0..k) (t held one per lane): a serial chain of
-// scalar-broadcast adds, exactly the reference's order.
-__device__ __forceinline__ double ordered_sum(double t, int k) {
-  double acc = 0.0;
-  for (int j = 0; j < k; ++j) acc += readlane_f64(t, j);
-  return acc;
-}
+// A workgroup takes kQppLists lists, one wavefront each.  The per-element and
+// per-prefix work is lane parallel inside the list's wave (lane i holds rsv[i] /
+// owns prefix i); the sums Java forms left to right are serial chains, and those
+// run batched: one wave, one lane per (list, chain), so a chain costs one lane
+// of one instruction instead of a whole wave's.
+constexpr int kQppLists = 8;
+constexpr int kQppBlock = 64 * kQppLists;
+constexpr int kChains = 8;   // cum, smv, wig, skew, snqc, uw, w, SigmaX-x
+constexpr int kRow = 65;     // padded LDS row (doubles)
 
 __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     int32_t R, int32_t top_k, const int32_t* __restrict__ num_terms,
     const double* __restrict__ text_feat, double* __restrict__ out) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t l = (int64_t)blockIdx.x * (kQppBlock / 64) + wid;
-  if (l >= n_lists) return;  // wave-uniform; no block barrier below
-  const int64_t a = list_off[l], b = list_off[l + 1];
-  int64_t n64 = b - a;
-  if (top_k > 0 && n64 > top_k) n64 = top_k;  // sorted(...)[:top_k], src/qpp.py:305
-  const int n = (int)n64;
-  const int k = n < 50 ? n : 50;                 // QPPBridge.java:141
-  double* o = out + l * kQppCols;
-  if (k == 0) {  // empty map -> every column 0.0 (src/qpp.py:321)
-    if (lane < kQppCols) o[lane] = 0.0;
-    return;
+  __shared__ double s_x[kQppLists][kRow];           // rsv (float32-rounded)
+  __shared__ double s_pm[kQppLists][kRow];          // prefix means
+  __shared__ double s_t[kQppLists][kChains][kRow];  // per-element terms of the chains
+  __shared__ double s_res[kQppLists][kChains + 1];  // chain sums; [8] = SigmaX
+  __shared__ unsigned long long s_fmask[kQppLists];
+  __shared__ int s_k[kQppLists];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t l = (int64_t)blockIdx.x * kQppLists + w;
+  const bool lv = l < n_lists;  // every wave stays for the barriers
+  int k = 0;
+  int64_t a = 0;
+  if (lv) {
+    a = list_off[l];
+    int64_t n64 = list_off[l + 1] - a;
+    if (top_k > 0 && n64 > top_k) n64 = top_k;  // sorted(...)[:top_k], src/qpp.py:305
+    k = n64 < 50 ? (int)n64 : 50;                // QPPBridge.java:141
   }
-  const int64_t q = l / R;
   const bool act = lane < k;
   // float32 rounding of the JSON value (Gson getAsFloat), then widened.
   const double x = act ? (double)(float)score[a + lane] : 0.0;
-  const int nt_raw = num_terms[q];
-  const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
+  s_x[w][lane] = x;
+  if (lane == 0) s_k[w] = k;
+  __syncthreads();
 
-  // prefix Kahan means (DoubleStream.average): lane i -> mean of rsv[0..i]
-  Kahan kp;
-  kahan_init(kp);
-  for (int j = 0; j < k; ++j) {
-    const double xj = readlane_f64(x, j);
-    if (j <= lane) kahan_add(kp, xj);
+  // ---- B (wave 0, lane = list): Java's compensated prefix means
+  // (DoubleStream.average of rsv[0..i]), one serial chain per list
+  if (w == 0 && lane < kQppLists) {
+    const int kl = s_k[lane];
+    Kahan kp;
+    kahan_init(kp);
+    for (int j = 0; j < kl; ++j) {
+      kahan_add(kp, s_x[lane][j]);
+      s_pm[lane][j] = kahan_final(kp) / (double)(j + 1);
+    }
   }
-  const double mean_i = kahan_final(kp) / (double)(lane + 1);
-  const double mu = readlane_f64(mean_i, k - 1);  // Arrays.stream(rsvs).average()
+  __syncthreads();
 
-  // squared deviations around each prefix mean: simple sum -> NQC of the prefix
-  // (NQC, CumNQC), compensated average -> population variance (SigmaMax, RSD)
+  // ---- C (each list's wave): squared deviations around each prefix mean
+  // (lane i = prefix i): simple sum -> NQC of the prefix (NQC, CumNQC),
+  // compensated average -> population variance (SigmaMax, RSD)
+  const int64_t q = lv ? l / R : 0;
+  const int nt_raw = lv ? num_terms[q] : 1;
+  const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
+  const double mean_i = act ? s_pm[w][lane] : 0.0;
+  const double mu = k > 0 ? s_pm[w][k - 1] : 0.0;  // Arrays.stream(rsvs).average()
   Kahan kv;
   kahan_init(kv);
   double sq = 0.0;
   for (int j = 0; j < k; ++j) {
-    const double del = readlane_f64(x, j) - mean_i;
+    const double del = s_x[w][j] - mean_i;
     const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
     if (j <= lane) {
       sq += d2;
@@ -83,20 +98,17 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
   const double nqc_i = sq / (double)(lane + 1);
   const double var_i = kahan_final(kv) / (double)(lane + 1);
   const double sigma_i = sqrt(var_i);
-  const double nqc = readlane_f64(nqc_i, k - 1);          // col 0: NQC (:202-216)
-  const double var_full = readlane_f64(var_i, k - 1);
-  double sm = (lane >= 1 && act) ? sigma_i : 0.0;          // col 3: SigmaMax (:269-293)
+  const double nqc = k > 0 ? readlane_f64(nqc_i, k - 1) : 0.0;  // col 0: NQC (:202-216)
+  const double var_full = k > 0 ? readlane_f64(var_i, k - 1) : 0.0;
+  double sm = (lane >= 1 && act) ? sigma_i : 0.0;                // col 3: SigmaMax (:269-293)
   sm = wave_max(sm);
   const double sigmamax = k < 2 ? 0.0 : sm / sqrt((double)numTerms);
-  // col 9: CumNQC (:400-410), sum over prefix sizes 2..n in order
-  const double cum = ordered_sum((lane >= 1 && act) ? nqc_i : 0.0, k);
-  const double cumnqc = k < 2 ? 0.0 : cum / (double)(k - 1);
 
   // per-element terms, one element per lane (transcendentals run once each)
   const double muhat = mu <= 0.0 ? 1.0 : mu;                  // SMV
   const double baseline = 1.0 / (0.01 > mu ? 0.01 : mu);      // WIG
   const double std_full = sqrt(var_full);                     // RSD
-  const double x0 = readlane_f64(x, 0);
+  const double x0 = s_x[w][0];
   const double thr = x0 * 0.5;                                // SigmaX
   double t_smv = 0.0, t_snqc = 0.0, t_skew = 0.0, t_wig = 0.0, t_uw = 0.0, t_w = 0.0;
   if (act) {
@@ -114,34 +126,71 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     }
   }
   // Java adds the x <= 0 terms of SMV / SNQC as "skip": adding +0.0 is the same.
-  const double smv = ordered_sum(t_smv, k);
-  const double wig = ordered_sum(t_wig, k);
-  const double skew = ordered_sum(t_skew, k);
-  const double snqc = ordered_sum(t_snqc, k);
-  const int ku = k < 20 ? k : 20;
-  const double util = ordered_sum(t_uw, ku);
-  const double wsum = ordered_sum(t_w, ku);
-  // col 4: SigmaX (:299-319): compensated mean / variance of {x >= thr} in order
-  const bool inF = act && x >= thr;
-  const uint64_t fmask = ballot(inF);
-  const int nf = __popcll(fmask);
-  double sigmax = 0.0;
-  if (k >= 2 && nf >= 2) {
-    Kahan kf;
-    kahan_init(kf);
-    for (int j = 0; j < k; ++j)
-      if ((fmask >> j) & 1ull) kahan_add(kf, readlane_f64(x, j));
-    const double mf = kahan_final(kf) / (double)nf;
-    const double dv = x - mf;
-    const double t = dv * dv;
-    Kahan kfv;
-    kahan_init(kfv);
-    for (int j = 0; j < k; ++j)
-      if ((fmask >> j) & 1ull) kahan_add(kfv, readlane_f64(t, j));
-    sigmax = sqrt(kahan_final(kfv) / (double)nf);
-  }
+  // col 9: CumNQC (:400-410) sums the NQC of prefix sizes 2..n in order.
+  s_t[w][0][lane] = (lane >= 1 && act) ? nqc_i : 0.0;
+  s_t[w][1][lane] = t_smv;
+  s_t[w][2][lane] = t_wig;
+  s_t[w][3][lane] = t_skew;
+  s_t[w][4][lane] = t_snqc;
+  s_t[w][5][lane] = t_uw;
+  s_t[w][6][lane] = t_w;
+  s_t[w][7][lane] = x;
+  // col 4: SigmaX (:299-319) takes {x >= thr} in order
+  const uint64_t fmask = ballot(act && x >= thr);
+  if (lane == 0) s_fmask[w] = fmask;
   const double mx = wave_max(act ? x : -INFINITY);
   const double mn = wave_min(act ? x : INFINITY);
+  __syncthreads();
+
+  // ---- D (wave 0, lane = list * 8 + chain): the left-to-right sums, all chains
+  // of all lists at once; chain 7 is SigmaX's compensated mean over F
+  if (w == 0) {
+    const int ll = lane >> 3, c = lane & 7;
+    const int kl = s_k[ll];
+    const int len = (c == 5 || c == 6) ? (kl < 20 ? kl : 20) : kl;
+    const uint64_t fm = s_fmask[ll];
+    const double* row = s_t[ll][c];
+    double acc = 0.0;
+    Kahan kf;
+    kahan_init(kf);
+    for (int j = 0; j < len; ++j) {
+      const double v = row[j];
+      acc += v;
+      if (c == 7 && ((fm >> j) & 1ull)) kahan_add(kf, v);
+    }
+    const int nf = __popcll(fm);
+    const double mf = kahan_final(kf) / (double)nf;
+    s_res[ll][c] = c == 7 ? mf : acc;
+    // SigmaX variance: compensated mean of (x - mf)^2 over F, in order
+    const double mfl = __shfl(mf, ll * 8 + 7, 64);
+    if (c == 0) {
+      double sigmax = 0.0;
+      if (kl >= 2 && nf >= 2) {
+        const double* xr = s_t[ll][7];
+        Kahan kfv;
+        kahan_init(kfv);
+        for (int j = 0; j < kl; ++j)
+          if ((fm >> j) & 1ull) {
+            const double dv = xr[j] - mfl;
+            kahan_add(kfv, dv * dv);
+          }
+        sigmax = sqrt(kahan_final(kfv) / (double)nf);
+      }
+      s_res[ll][8] = sigmax;
+    }
+  }
+  __syncthreads();
+
+  if (!lv) return;
+  double* o = out + l * kQppCols;
+  if (k == 0) {  // empty map -> every column 0.0 (src/qpp.py:321)
+    if (lane < kQppCols) o[lane] = 0.0;
+    return;
+  }
+  const double cum = s_res[w][0], smv = s_res[w][1], wig = s_res[w][2], skew = s_res[w][3];
+  const double snqc = s_res[w][4], util = s_res[w][5], wsum = s_res[w][6];
+  const double sigmax = s_res[w][8];
+  const double cumnqc = k < 2 ? 0.0 : cum / (double)(k - 1);
   double res[kQppCols];
   res[0] = nqc;
   res[1] = smv / (double)k;
@@ -231,7 +280,7 @@ hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t 
                           hipStream_t st) {
   const int64_t L = Q * R;
   if (L == 0) return hipSuccess;
-  const unsigned grid = (unsigned)((L + 3) / 4);
+  const unsigned grid = (unsigned)((L + kQppLists - 1) / kQppLists);
   hipLaunchKernelGGL(qpp_raw_kernel, dim3(grid), dim3(kQppBlock), 0, st, score, list_off, L, R,
                      top_k, nt, tf, out);
   return hipGetLastError();
