@@ -91,32 +91,35 @@ __device__ __forceinline__ void block_min_max(uint64_t kmn, uint64_t kmx,
 
 // ---- the per-(query, method) sort -------------------------------------------
 //
-// Items are 64-bit words, held in registers wave-major (item i = (wid*rows +
+// Items are 32-bit words, held in registers wave-major (item i = (wid*rows +
 // j)*64 + lane) and scattered through LDS between passes:
-//   bits 32..55  window key: the kWindow most significant bits of (key - kmin),
-//                key = ~orderable(score) (ascending key == descending score)
-//   bits  0..15  u, the document's first-seen index
+//   bits 13..30  window key: the kWindow most significant bits of (wkey - wmin),
+//                a non-decreasing function of key = ~orderable(score)
+//                (ascending key == descending score), see sort_one
+//   bits  0..12  u, the document's first-seen index
 // The full key of an item is re-derived from fused[u] (the unsorted scores in
-// HBM/L2), which only the rare fix-up and the fallback need.
+// HBM/L2), which only the rare fix-up and the output need.
+constexpr int kDigit = 9;                // bits per LSD pass
+constexpr int kBuckets = 1 << kDigit;    // counters per wave, 16 bits each
+constexpr int kUBits = 13;
+constexpr uint32_t kUMask = (1u << kUBits) - 1u;
 template <int ITEMS, int WAVES>
 struct SortCtx {
-  uint32_t* hist;    // [WAVES][256]
-  uint64_t* sitem;   // [UMAX]
-  uint32_t* wtot;    // [WAVES] scan carries
-  int* flag;         // [2]: fix-up status, listed runs
-  const double* io;  // fused[slot] of the query: unsorted scores by u
+  uint32_t* hist;      // [WAVES][kBuckets] u16 counters, two per word
+  uint32_t* sitem;     // [UMAX]
+  const double* sval;  // fused[slot] of the query: the unsorted scores by u
+  uint32_t* wtot;      // [WAVES] scan carries
+  int* flag;           // [2]: fix-up status, listed runs
   uint64_t kmin;
   int U, rows, lane, wid, tid;
 };
 
-constexpr uint32_t kUMask = 0xFFFFu;
-
 template <int ITEMS, int WAVES>
-__device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, uint64_t item) {
-  return ~f64_asc_key(sx.io[item & kUMask]);
+__device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, uint32_t item) {
+  return ~f64_asc_key(sx.sval[item & kUMask]);
 }
 
-// One stable counting-scatter pass on an 8-bit digit of the items.  Within a
+// One stable counting-scatter pass on a kDigit-bit digit of the items.  Within a
 // wave a row's items are ranked by a ballot match of their digits; the row's
 // leader lane claims a run of slots with one LDS atomicAdd (LDS ops of a wave
 // execute in program order, so rows stay ordered); the (wave, digit) offsets
@@ -124,18 +127,20 @@ __device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, ui
 // scattered sequence in sitem; `readback` reloads the registers.
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
-                                              uint64_t (&item)[ITEMS], int sh, bool readback) {
+                                              uint32_t (&item)[ITEMS], int sh, bool readback) {
   const int lane = sx.lane, wid = sx.wid;
   int rp = sx.rows;
   asm volatile("" : "+s"(rp));
-  // digit = bits sh..sh+7 of the window key (item bits 32..55)
-  auto digit = [sh](uint64_t it) -> uint32_t {
-    return __builtin_amdgcn_ubfe((uint32_t)(it >> 32), (uint32_t)sh, 8u);
+  // digit = bits sh..sh+8 of the window key
+  auto digit = [sh](uint32_t it) -> uint32_t {
+    return __builtin_amdgcn_ubfe(it, (uint32_t)(kUBits + sh), (uint32_t)kDigit);
   };
-  // hist is [wave][digit] (a wave's leaders hit distinct banks)
+  // hist is [wave][digit] u16 counters (digit d: word d >> 1, half d & 1; a
+  // wave's leaders hit distinct banks); counts and offsets stay below 2^16
   uint32_t* hist = sx.hist;
+  uint16_t* hist16 = (uint16_t*)sx.hist;
   QF_STAMP_INIT();
-  for (int k = lane; k < 256; k += 64) hist[wid * 256 + k] = 0u;
+  for (int k = lane; k < kBuckets / 2; k += 64) hist[wid * (kBuckets / 2) + k] = 0u;
   uint32_t rank_in[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -149,7 +154,7 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
       const uint64_t vb = ballot(valid);
       uint32_t mlo = ~(uint32_t)vb, mhi = ~(uint32_t)(vb >> 32);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
+      for (int b = 0; b < kDigit; ++b) {
         uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)d, (uint32_t)b, 1u);
         asm("" : "+v"(m));  // keep the ballot on m (one v_cmp), not a re-derived bit test
         const uint64_t bb = ballot(m != 0u);
@@ -162,8 +167,12 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
       const uint32_t llo = (uint32_t)__builtin_ctz(plo | (plo == 0u ? 0x80000000u : 0u));
       const uint32_t leader = plo ? llo : 32u + (uint32_t)__builtin_ctz(phi | 0x80000000u);
       uint32_t old = 0u;
-      if (valid && before == 0)
-        old = atomicAdd(&hist[wid * 256 + d], (uint32_t)(__popc(plo) + __popc(phi)));
+      if (valid && before == 0) {
+        const uint32_t hs = (d & 1u) * 16u;
+        old = atomicAdd(&hist[wid * (kBuckets / 2) + (d >> 1)],
+                        (uint32_t)(__popc(plo) + __popc(phi)) << hs);
+        old = (old >> hs) & 0xFFFFu;
+      }
       old = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)old);
       rank_in[j] = old + before;
     }
@@ -171,13 +180,15 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   QF_STAMP(8);
   __syncthreads();
   QF_STAMP(9);
-  // block-wide exclusive scan of the 256*WAVES counters, 4 per thread
+  // block-wide exclusive scan of the kBuckets*WAVES counters in [digit][wave]
+  // order, kPer per thread (16-bit loads and stores: no word is shared)
   {
-    uint32_t v[4], t = 0u;
+    constexpr int kPer = kBuckets / 64;
+    uint32_t v[kPer], t = 0u;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int f = 4 * sx.tid + c;
-      v[c] = hist[(f % WAVES) * 256 + f / WAVES];
+    for (int c = 0; c < kPer; ++c) {
+      const int f = kPer * sx.tid + c;
+      v[c] = hist16[(f % WAVES) * kBuckets + f / WAVES];
       t += v[c];
     }
     const uint32_t incl = wave_incl_scan_dpp(t);
@@ -188,9 +199,9 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
     for (int w = 0; w < WAVES; ++w)
       if (w < wid) ex += sx.wtot[w];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int f = 4 * sx.tid + c;
-      hist[(f % WAVES) * 256 + f / WAVES] = ex;
+    for (int c = 0; c < kPer; ++c) {
+      const int f = kPer * sx.tid + c;
+      hist16[(f % WAVES) * kBuckets + f / WAVES] = (uint16_t)ex;
       ex += v[c];
     }
   }
@@ -201,7 +212,7 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rp + j) * 64 + lane;
     if (j < rp && i < sx.U)
-      sx.sitem[hist[wid * 256 + digit(item[j])] + rank_in[j]] = item[j];
+      sx.sitem[hist16[wid * kBuckets + digit(item[j])] + rank_in[j]] = item[j];
   }
   QF_STAMP(11);
   __syncthreads();
@@ -223,27 +234,28 @@ __device__ __forceinline__ uint32_t wave_up1(uint32_t v) {
 }
 
 // Stable sort of the items by full key ascending (scores descending; ties keep
-// input = first-seen order), given the window width nb = min(hb, kWindow):
-//  1. LSD counting passes over the window key (bits 32.. of the item);
-//  2. if the window dropped low bits (lo > 0): inside a run of items with equal
-//     window keys an item is "bad" when its predecessor has a larger full key.
-//     No bad item anywhere (the usual case; long runs of equal keys are never
-//     bad): sorted.  Otherwise the run of each first bad item is put in
-//     full-key order by a stable insertion sort run by one thread.
+// input = first-seen order), given the window width nb (<= kWindow):
+//  1. LSD counting passes over the window key;
+//  2. unless the window is exact (every bit of the full key): inside a run of
+//     items with equal window keys an item is "bad" when its predecessor has a
+//     larger full key.  No bad item anywhere (the usual case; long runs of equal
+//     keys are never bad): sorted.  Otherwise the run of each first bad item is
+//     put in full-key order by a stable insertion sort run by one thread.
 // A run longer than kRunMax that needs fixing sends the block on with LSD passes
-// over every bit of (full key - kmin) from bit 0: started from the order of
-// step 1 (equal keys still first-seen) they give the same stable result.
+// over every bit of (full key - kmin) (hb_full bits) from bit 0: started from
+// the order of step 1 (equal keys still first-seen) they give the same stable
+// result.
 constexpr int kRunMax = 64;
-constexpr int kWindow = 24;  // bits sorted by LSD passes (3 passes of 8)
+constexpr int kWindow = 2 * kDigit;  // bits sorted by LSD passes (2 passes of 9)
+static_assert(kWindow + kUBits <= 32, "items are 32-bit");
 
 template <int ITEMS, int WAVES>
-__device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEMS], int hb,
-                          int lo) {
-  const int nb = hb - lo;
+__device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEMS], int nb,
+                          bool exact, int hb_full) {
   int sh = 0;
   bool fallback = false;
   if (sx.tid == 0) { sx.flag[0] = 0; sx.flag[1] = 0; }  // ordered by count_scatter's barriers
-  constexpr int kListCap = 256 * WAVES;                 // run starts, kept in hist
+  constexpr int kListCap = (kBuckets / 2) * WAVES;     // run starts, kept in hist
 #pragma unroll 1
   while (true) {
     if (fallback) {  // this pass's digit of the full key becomes the window key
@@ -253,13 +265,14 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEM
       for (int j = 0; j < ITEMS; ++j) {
         const int i = (sx.wid * rp + j) * 64 + sx.lane;
         if (j < rp && i < sx.U)
-          item[j] = ((((full_key(sx, item[j]) - sx.kmin) >> sh) & 0xFFu) << 32) | (item[j] & kUMask);
+          item[j] = ((uint32_t)(((full_key(sx, item[j]) - sx.kmin) >> sh) &
+                                (uint64_t)(kBuckets - 1)) << kUBits) | (item[j] & kUMask);
       }
     }
     count_scatter(sx, item, fallback ? 0 : sh, true);
-    sh += 8;
-    if (sh < (fallback ? hb : nb)) continue;
-    if (fallback || lo == 0) return;
+    sh += kDigit;
+    if (sh < (fallback ? hb_full : nb)) continue;
+    if (fallback || exact) return;
     // -- A: find the runs to fix (read-only) ----------------------------------------
     {
       int rp = sx.rows;
@@ -268,13 +281,13 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEM
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const int i = (sx.wid * rp + j) * 64 + sx.lane;
-        const uint32_t wk = (uint32_t)(item[j] >> 32);
+        const uint32_t wk = item[j] >> kUBits;
         uint32_t wp = wave_up1(wk);
         if (j < rp && i < sx.U && i > 0) {
-          uint64_t ip = 0;
+          uint32_t ip = 0;
           if (sx.lane == 0) {
             ip = sx.sitem[i - 1];
-            wp = (uint32_t)(ip >> 32);
+            wp = ip >> kUBits;
           }
           if (wp == wk) {  // same window as the predecessor: compare full keys
             if (sx.lane != 0) ip = sx.sitem[i - 1];
@@ -285,8 +298,8 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEM
               uint64_t kc = kp;
               bool first = true;
               while (st > 0) {
-                const uint64_t iq = sx.sitem[st - 1];
-                if ((uint32_t)(iq >> 32) != wk) break;
+                const uint32_t iq = sx.sitem[st - 1];
+                if ((iq >> kUBits) != wk) break;
                 const uint64_t kq = full_key(sx, iq);
                 if (kq > kc) { first = false; break; }  // an earlier bad item owns the run
                 kc = kq;
@@ -316,12 +329,12 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEM
       const int nr = sx.flag[1];
       for (int t = sx.tid; t < nr; t += WAVES * 64) {
         const int i = (int)sx.hist[t];
-        const uint32_t wk = (uint32_t)(sx.sitem[i] >> 32);
+        const uint32_t wk = sx.sitem[i] >> kUBits;
         int L = 1;
-        while (i + L < sx.U && (uint32_t)(sx.sitem[i + L] >> 32) == wk && L <= kRunMax) ++L;
+        while (i + L < sx.U && (sx.sitem[i + L] >> kUBits) == wk && L <= kRunMax) ++L;
         if (L > kRunMax) { atomicOr(&sx.flag[0], 1); continue; }
         for (int a = i + 1; a < i + L; ++a) {
-          const uint64_t ia = sx.sitem[a];
+          const uint32_t ia = sx.sitem[a];
           const uint64_t ka = full_key(sx, ia);
           int b = a - 1;
           while (b >= i && full_key(sx, sx.sitem[b]) > ka) {
@@ -349,11 +362,12 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint64_t (&item)[ITEM
   }
 }
 
-// Sorted items -> perm (u of rank i) and the fused score (read back from fused[u]
-// with its sign, -0.0 included, before the block overwrites fused in place).
+// Sorted items -> perm (u of rank i) and the fused score (read back from
+// fused[u] with its sign, -0.0 included, before the block overwrites fused in
+// place).
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
-                                          const uint64_t (&item)[ITEMS], uint16_t* operm,
+                                          const uint32_t (&item)[ITEMS], uint16_t* operm,
                                           double* io) {
   int ro = sx.rows;
   asm volatile("" : "+s"(ro));
@@ -645,10 +659,10 @@ template <int BLOCK, int ITEMS, int MINW>
 struct SortCfg {
   static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64, kMinWaves = MINW;
   static constexpr int kUMax = BLOCK * ITEMS;
-  static constexpr int kItemOff = 0;            // u64 [UMAX]
-  static constexpr int kHistOff = 8 * kUMax;    // u32 [W][256]
-  static constexpr int kSmem = kHistOff + 4 * 256 * kWaves;
-  static_assert(kUMax <= (int)kUMask + 1, "u is 16 bits of the item");
+  static constexpr int kItemOff = 0;                // u32 [UMAX]
+  static constexpr int kHistOff = 4 * kUMax;         // u16 [W][kBuckets]
+  static constexpr int kSmem = kHistOff + 2 * kBuckets * kWaves;
+  static_assert(kUMax <= (int)kUMask + 1, "u is kUBits bits of the item");
   static_assert(kSmem <= 160 * 1024, "LDS budget");
 };
 
@@ -681,18 +695,18 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
   double* io = p.fused + (int64_t)ms * p.out_stride + base;  // unsorted fused[ms][u]
   const uint32_t* udoc = p.union_docid + base;
   const int rows = (U + 64 * WAVES - 1) / (64 * WAVES);
-  // ---- full keys of the join kernel's unsorted scores, their range -------------
-  uint64_t item[ITEMS];
+  // ---- the join kernel's unsorted scores -> LDS, their key range -----------------
+  uint64_t fk[ITEMS];
   uint64_t kmn = ~0ull, kmx = 0ull;
   uint32_t dmn = ~0u, dmx = 0u;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rows + j) * 64 + lane;
-    item[j] = 0;
+    fk[j] = 0;
     if (j < rows && i < U) {
-      item[j] = ~f64_asc_key(io[i]);  // ascending sort on ~key == descending score
-      kmn = min(kmn, item[j]);
-      kmx = max(kmx, item[j]);
+      fk[j] = ~f64_asc_key(io[i]);  // ascending sort on ~key == descending score
+      kmn = min(kmn, fk[j]);
+      kmx = max(kmx, fk[j]);
       if (by_docid) {
         const uint32_t d = udoc[i];
         dmn = min(dmn, d);
@@ -715,24 +729,42 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
   __syncthreads();
   const uint64_t kmin = sh.kmin, kmax = sh.kmax;
   SortCtx<ITEMS, WAVES> sx{(uint32_t*)(sh.smem + C::kHistOff),
-                           (uint64_t*)(sh.smem + C::kItemOff), sh.wtot, sh.flag, io, kmin, U,
+                           (uint32_t*)(sh.smem + C::kItemOff), io, sh.wtot, sh.flag, kmin, U,
                            rows, lane, wid, tid};
-  const int hb = kmax > kmin ? 64 - __clzll((long long)(kmax - kmin)) : 0;
+  const int hb_full = kmax > kmin ? 64 - __clzll((long long)(kmax - kmin)) : 0;
+  // Window key.  The raw key's top bits are mostly exponent, so a short window
+  // of it collides a lot; for a finite score range the window is cut from
+  // wkey(v) = ~orderable((v - smin) + rng * 2^-6) instead: non-decreasing in
+  // the full key (each rounding is monotone), so different windows are in
+  // full-key order and only equal windows need the fix-up.  Its extremes are
+  // wkey(smax) and wkey(smin) by the same monotonicity.
+  const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
+  const double rng = smax - smin;
+  const bool lin = hb_full > 0 && isfinite(rng);
+  const double delta = rng * 0x1p-6;
+  auto wkey = [&](uint64_t key) -> uint64_t {
+    return lin ? ~f64_asc_key((f64_from_asc_key(~key) - smin) + delta) : key;
+  };
+  const uint64_t wmin = lin ? ~f64_asc_key((smax - smin) + delta) : kmin;
+  const uint64_t wmax = lin ? ~f64_asc_key((smin - smin) + delta) : kmax;
+  const int hb = wmax > wmin ? 64 - __clzll((long long)(wmax - wmin)) : 0;
   const int lo = hb > kWindow ? hb - kWindow : 0;
+  const bool exact = !lin && lo == 0;  // the window holds the whole key
+  uint32_t item[ITEMS];
   if (by_docid && sh.dmax > sh.dmin) {
     // ---- learned fusion: first into docid order ------------------------------------
     const uint32_t dmin = sh.dmin;
     const int db = 32 - __clz((int)(sh.dmax - dmin));
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) item[j] = (uint64_t)((wid * rows + j) * 64 + lane);
+    for (int j = 0; j < ITEMS; ++j) item[j] = (uint32_t)((wid * rows + j) * 64 + lane);
 #pragma unroll 1
-    for (int s0 = 0; s0 < db; s0 += 8) {
+    for (int s0 = 0; s0 < db; s0 += kDigit) {
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const int i = (wid * rows + j) * 64 + lane;
         if (j < rows && i < U) {
-          const uint32_t u = (uint32_t)(item[j] & kUMask);
-          item[j] = ((uint64_t)(((udoc[u] - dmin) >> s0) & 0xFFu) << 32) | u;
+          const uint32_t u = item[j] & kUMask;
+          item[j] = ((((udoc[u] - dmin) >> s0) & (uint32_t)(kBuckets - 1)) << kUBits) | u;
         }
       }
       count_scatter(sx, item, 0, true);
@@ -741,8 +773,8 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
     for (int j = 0; j < ITEMS; ++j) {  // registers now hold docid order: re-key
       const int i = (wid * rows + j) * 64 + lane;
       if (j < rows && i < U) {
-        const uint32_t u = (uint32_t)(item[j] & kUMask);
-        item[j] = (((~f64_asc_key(io[u]) - kmin) >> lo) << 32) | u;
+        const uint32_t u = item[j] & kUMask;
+        item[j] = ((uint32_t)((wkey(~f64_asc_key(io[u])) - wmin) >> lo) << kUBits) | u;
       }
     }
   } else {
@@ -750,16 +782,15 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const int i = (wid * rows + j) * 64 + lane;
-      item[j] = (((item[j] - kmin) >> lo) << 32) | (uint32_t)i;
+      item[j] = ((uint32_t)((wkey(fk[j]) - wmin) >> lo) << kUBits) | (uint32_t)i;
     }
   }
   QF_STAMP(0);
-  if (hb > 0) sort_desc(sx, item, hb, lo);  // hb == 0: all keys equal, order stands
+  if (hb_full > 0) sort_desc(sx, item, hb - lo, exact, hb_full);  // else all keys equal
   QF_STAMP(1);
   write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base, io);
   QF_STAMP(2);
 }
-
 // Method bit of output slot ms.
 __device__ __forceinline__ int slot_method(int methods, int ms) {
   for (int t = 0, c = 0; t < 7; ++t)
@@ -849,9 +880,10 @@ static void launch_sort(const FuseParams& p, int umin, hipStream_t st) {
 }
 
 template <class S>
-static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st) {
+static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st, int per_cu) {
   const int64_t pairs = p.n_queries * __builtin_popcount((unsigned)p.methods);
-  const int64_t grid = pairs < 256 ? pairs : 256;  // one per CU (VGPR-bound)
+  const int64_t cap = 256 * per_cu;  // resident workgroups (LDS / VGPR-bound)
+  const int64_t grid = pairs < cap ? pairs : cap;
   hipLaunchKernelGGL((fuse_large_kernel<S>), dim3((unsigned)grid), dim3(S::kBlock), 0, st, p,
                      umin);
 }
@@ -864,7 +896,7 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
     else launch_join<JoinL>(p, kind, st);
     launch_sort<SortM>(p, 0, st);
-    launch_sort_large<SortL>(p, SortM::kUMax + 1, st);  // the queries SortM left
+    launch_sort_large<SortL>(p, SortM::kUMax + 1, st, 1);  // the queries SortM left
   }
   return hipGetLastError();
 }

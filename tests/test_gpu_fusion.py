@@ -197,6 +197,9 @@ def _sort_case(kind, n, rng):
         base = rng.uniform(0, 1, n // 2)
         s = np.concatenate([base, base + rng.integers(1, 1 << 12, n // 2) * 2.0 ** -50])[:n]
         s = np.resize(s, n)
+    elif kind == "huge_and_inf":  # score range overflows: the raw-key window path
+        s = rng.uniform(-1, 1, n)
+        s[: n // 10] = rng.choice([1.7e308, -1.7e308, np.inf, -np.inf, 0.0], n // 10)
     elif kind == "zeros_and_ties":
         s = rng.choice([0.0, -0.0, 1.0, 0.5, 0.5 + 2.0 ** -40, -2.0 ** -1074], n)
     else:  # uniform
@@ -205,8 +208,9 @@ def _sort_case(kind, n, rng):
     return s
 
 
-@pytest.mark.parametrize("n", [700, 2900, 7000])
-@pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform"])
+@pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000])
+@pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform",
+                                  "huge_and_inf"])
 def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
     """One retriever, W-CombSUM with weight 1: the fused scores are the inputs, so the
     kernel's sort (LSD window + run fix-up + full-LSD fallback) is checked against a

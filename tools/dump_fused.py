@@ -18,6 +18,7 @@ off = p.off.cpu().numpy()
 out = {"uc": uc, "off": off}
 for m, name in enumerate(bench.METHODS):
     out[name] = p.out.fused[m].cpu().numpy()
+    out[name + "_perm"] = p.out.perm[m].cpu().numpy()
 Path("gpurun_out").mkdir(exist_ok=True)
 np.savez_compressed("gpurun_out/fused_c2.npz", **out)
 print("ok")
