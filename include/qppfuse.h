@@ -64,6 +64,7 @@ extern "C" {
 /* ---- QPP normalisation modes (src/qpp.py:340-374) ----------------------- */
 #define QF_NORM_NONE   0
 #define QF_NORM_MINMAX 1
+#define QF_NORM_ZSCORE 2
 
 #define QF_QPP_COLS 13 /* Java column order: nqc smv wig SigmaMax SigmaX RSD UEF
                           MaxIDF avgidf cumnqc snqc dense-qpp dense-qpp-m
@@ -109,7 +110,22 @@ int qf_qpp_colminmax(const double* raw, const int64_t* list_off, int64_t n_queri
                      int32_t n_retrievers, double* mm_out, void* stream);
 
 /*
- * Normalise raw predictors with mm (src/qpp.py:362-372) and round each value
+ * zscore statistics (src/qpp.py:358-359): per (retriever, column) numpy's
+ * arr.mean() and the scale arr.std() (population; 1.0 when not > 0) over the
+ * queries with a non-empty list, in query order.  Bit-identical to numpy: its
+ * float64 sum is reproduced exactly (0.0 + pairwise sums of 8192-element
+ * chunks; pairwise = numpy's fixed recursion with 8 accumulators below 128).
+ * st_out holds 2*R*13 doubles: [0, R*13) = mean, [R*13, 2*R*13) = scale.
+ * Queries are not shardable for this (the sum's tree depends on positions):
+ * one device sees every query.
+ */
+int qf_qpp_colmeanstd(const double* raw, const int64_t* list_off, int64_t n_queries,
+                      int32_t n_retrievers, double* st_out, void* stream);
+
+/*
+ * Normalise raw predictors (src/qpp.py:362-372) — mode QF_NORM_MINMAX with
+ * mm from qf_qpp_colminmax, QF_NORM_ZSCORE with mm from qf_qpp_colmeanstd,
+ * QF_NORM_NONE without — and round each value
  * as the .qpp writer's f"{s:.6f}" does (src/qpp.py:333): micro_out (nullable,
  * int64 micro-units) and norm_out (nullable, the unrounded double).  Then, if
  * w_out is non-null, the fusion weight of every (q, r) as

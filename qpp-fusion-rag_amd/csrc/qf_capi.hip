@@ -69,12 +69,21 @@ int qf_qpp_colminmax(const double* raw, const int64_t* list_off, int64_t n_queri
                "qf_qpp_colminmax");
 }
 
+int qf_qpp_colmeanstd(const double* raw, const int64_t* list_off, int64_t n_queries,
+                      int32_t n_retrievers, double* st_out, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off || !st_out)
+    return fail(QF_EINVAL, "qf_qpp_colmeanstd: bad arguments");
+  return check(qf::qpp_colmeanstd_launch(raw, list_off, n_queries, n_retrievers, st_out,
+                                         (hipStream_t)stream),
+               "qf_qpp_colmeanstd");
+}
+
 int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_off,
                      int64_t n_queries, int32_t n_retrievers, int32_t mode, int32_t qpp_index,
                      double* norm_out, int64_t* micro_out, double* w_out, void* stream) {
-  if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off || (mode == QF_NORM_MINMAX && !mm))
+  if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off || (mode != QF_NORM_NONE && !mm))
     return fail(QF_EINVAL, "qf_qpp_normalize: bad arguments");
-  if (mode != QF_NORM_NONE && mode != QF_NORM_MINMAX)
+  if (mode != QF_NORM_NONE && mode != QF_NORM_MINMAX && mode != QF_NORM_ZSCORE)
     return fail(QF_EINVAL, "qf_qpp_normalize: unsupported mode %d", mode);
   if (qpp_index < -1 || qpp_index >= QF_QPP_COLS)
     return fail(QF_EINVAL, "qf_qpp_normalize: qpp_index %d out of range", qpp_index);

@@ -85,6 +85,8 @@ hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t 
                           hipStream_t st);
 hipError_t qpp_colminmax_launch(const double* raw, const int64_t* list_off, int64_t Q, int32_t R,
                                 double* mm, hipStream_t st);
+hipError_t qpp_colmeanstd_launch(const double* raw, const int64_t* list_off, int64_t Q,
+                                 int32_t R, double* st, hipStream_t stm);
 hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64_t* list_off,
                                 int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
                                 double* norm_out, int64_t* micro_out, double* w_out,

@@ -244,6 +244,168 @@ __global__ __launch_bounds__(256) void qpp_colminmax_kernel(
   }
 }
 
+// ---- zscore statistics: numpy's mean / std of each column --------------------
+//
+// src/qpp.py:358-359 takes arr.mean() and arr.std() of a float64 column.  numpy
+// sums a contiguous float64 array as acc = 0.0; acc += pairwise(chunk) over
+// 8192-element chunks (the ufunc buffer), pairwise() being its fixed recursion
+// (n < 8: left to right from -0.0; n <= 128: 8 interleaved accumulators; else
+// split at n/2 rounded down to a multiple of 8).  std = sqrt(sum((x - mean)^2) / n)
+// with mean = sum(x) / n.  Both are reproduced exactly: one workgroup per
+// (retriever, column) gathers the present rows of a chunk into LDS, sums the
+// recursion's leaves in parallel and combines them in the recursion's order.
+constexpr int kNpChunk = 8192;
+constexpr int kNpLeaves = 128;  // leaves hold 64..128 elements of a full chunk
+
+struct NpFrame {
+  int lo, n, st;
+  double left;
+};
+
+// Walks pairwise(0, m) depth first.  LEAF(lo, n) returns the sum of a leaf.
+template <class LEAF>
+__device__ double np_pairwise_walk(int m, LEAF leaf) {
+  NpFrame f[12];
+  int sp = 0;
+  f[0] = {0, m, 0, 0.0};
+  double ret = 0.0;
+  while (true) {
+    if (f[sp].n <= 128) {
+      ret = leaf(f[sp].lo, f[sp].n);
+      while (true) {  // deliver ret upwards
+        if (sp == 0) return ret;
+        --sp;
+        if (f[sp].st == 1) {
+          f[sp].left = ret;
+          f[sp].st = 2;
+          int n2 = f[sp].n / 2;
+          n2 -= n2 % 8;
+          f[sp + 1] = {f[sp].lo + n2, f[sp].n - n2, 0, 0.0};
+          ++sp;
+          break;
+        }
+        ret = f[sp].left + ret;
+      }
+    } else {
+      f[sp].st = 1;
+      int n2 = f[sp].n / 2;
+      n2 -= n2 % 8;
+      f[sp + 1] = {f[sp].lo, n2, 0, 0.0};
+      ++sp;
+    }
+  }
+}
+
+// numpy's leaf: DOUBLE_pairwise_sum for n <= 128.
+__device__ double np_leaf_sum(const double* a, int n) {
+  if (n < 8) {
+    double res = -0.0;
+    for (int i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+__global__ __launch_bounds__(256) void qpp_colmeanstd_kernel(
+    const double* __restrict__ raw, const int64_t* __restrict__ list_off, int64_t Q, int32_t R,
+    double* __restrict__ st) {
+  __shared__ double s_val[kNpChunk];
+  __shared__ double s_leaf[kNpLeaves];
+  __shared__ int s_llo[kNpLeaves], s_ln[kNpLeaves];
+  __shared__ int s_nleaf, s_fill, s_take;
+  __shared__ int s_wcnt[4];
+  __shared__ double s_acc;
+  const int rc = blockIdx.x;  // r * 13 + c
+  const int r = rc / kQppCols, c = rc % kQppCols;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double mean = 0.0;
+  int64_t n_total = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (tid == 0) s_acc = 0.0;
+    int64_t cursor = 0;  // next row to scan
+    n_total = 0;
+    while (true) {
+      // ---- gather the next <= kNpChunk present rows (in row order) into s_val
+      if (tid == 0) s_fill = 0;
+      __syncthreads();
+      while (cursor < Q && s_fill < kNpChunk) {
+        const int64_t row = cursor + tid;
+        bool pres = false;
+        if (row < Q) {
+          const int64_t l = row * R + r;
+          pres = list_off[l + 1] > list_off[l];
+        }
+        const uint64_t b = ballot(pres);
+        if (lane == 0) s_wcnt[wid] = __popcll(b);
+        __syncthreads();
+        int before = (int)mbcnt(b);
+        for (int w = 0; w < wid; ++w) before += s_wcnt[w];
+        const int total = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+        const int fill = s_fill, room = kNpChunk - fill;
+        if (pres && before < room) {
+          double v = raw[(row * R + r) * kQppCols + c];
+          if (pass == 1) {
+            const double d = v - mean;  // numpy: x = arr - arrmean; x * x
+            v = d * d;
+          }
+          s_val[fill + before] = v;
+          if (before == room - 1) s_take = tid + 1;  // the row that fills the chunk
+        }
+        __syncthreads();
+        if (total <= room) {
+          cursor += 256;
+          if (tid == 0) s_fill = fill + total;
+        } else {
+          cursor += s_take;
+          if (tid == 0) s_fill = kNpChunk;
+        }
+        __syncthreads();
+      }
+      const int m = s_fill;
+      if (m == 0) break;
+      n_total += m;
+      // ---- leaves of pairwise(0, m) in recursion order, summed in parallel
+      if (tid == 0) {
+        int k = 0;
+        np_pairwise_walk(m, [&](int lo, int n) {
+          s_llo[k] = lo;
+          s_ln[k] = n;
+          ++k;
+          return 0.0;
+        });
+        s_nleaf = k;
+      }
+      __syncthreads();
+      if (tid < s_nleaf) s_leaf[tid] = np_leaf_sum(s_val + s_llo[tid], s_ln[tid]);
+      __syncthreads();
+      if (tid == 0) {
+        int k = 0;
+        const double chunk = np_pairwise_walk(m, [&](int, int) { return s_leaf[k++]; });
+        s_acc = s_acc + chunk;
+      }
+      __syncthreads();
+      if (m < kNpChunk) break;
+    }
+    const double sum = s_acc;
+    if (pass == 0) mean = sum / (double)n_total;
+    else if (tid == 0) {
+      const double sd = sqrt(sum / (double)n_total);
+      st[rc] = n_total ? mean : 0.0;
+      st[R * kQppCols + rc] = sd > 0.0 ? sd : 1.0;  // arr.std() if arr.std() > 0 else 1.0
+    }
+    __syncthreads();
+  }
+}
+
 // Normalise (src/qpp.py:356-372), round as "%.6f" (src/qpp.py:333), and derive
 // the fusion weight the .qpp text round trip gives (src/fusion.py:150-158).
 __global__ __launch_bounds__(256) void qpp_normalize_kernel(
@@ -263,6 +425,8 @@ __global__ __launch_bounds__(256) void qpp_normalize_kernel(
       const double vmax = -mm[R * kQppCols + r * kQppCols + c];
       const double scale = vmax > vmin ? vmax - vmin : 1.0;
       v = scale > 0.0 ? (x - vmin) / scale : 0.0;
+    } else if (mode == 2) {  // zscore: mm = [mean, scale] (qpp_colmeanstd)
+      v = (x - mm[r * kQppCols + c]) / mm[R * kQppCols + r * kQppCols + c];
     }
     if (!present) v = 0.0;
     const long long m = round6(v);
@@ -290,6 +454,13 @@ hipError_t qpp_colminmax_launch(const double* raw, const int64_t* list_off, int6
                                 double* mm, hipStream_t st) {
   hipLaunchKernelGGL(qpp_colminmax_kernel, dim3(R * kQppCols), dim3(256), 0, st, raw, list_off, Q,
                      R, mm);
+  return hipGetLastError();
+}
+
+hipError_t qpp_colmeanstd_launch(const double* raw, const int64_t* list_off, int64_t Q,
+                                 int32_t R, double* st, hipStream_t stm) {
+  hipLaunchKernelGGL(qpp_colmeanstd_kernel, dim3(R * kQppCols), dim3(256), 0, stm, raw, list_off,
+                     Q, R, st);
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF, LEARNED = (1 << i for i in rang
 METHOD_BITS = {"combsum": COMBSUM, "combmnz": COMBMNZ, "rrf": RRF,
                "wcombsum": WCOMBSUM, "wcombmnz": WCOMBMNZ, "wrrf": WRRF, "learned": LEARNED}
 SCORE_F64, SCORE_MICRO = 0, 1
-NORM_NONE, NORM_MINMAX = 0, 1
+NORM_NONE, NORM_MINMAX, NORM_ZSCORE = 0, 1, 2
 QPP_COLS = 13
 EVAL_NDCG, EVAL_RR, EVAL_R, EVAL_P, EVAL_AP = range(5)
 EVAL_MAX_METRICS, EVAL_MAX_QRELS = 16, 256
@@ -35,6 +35,7 @@ SIGNATURES = {
     "qf_minmax_per_query": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "qf_qpp_raw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "qf_qpp_colmeanstd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
                           _vp, _vp, _vp, _vp, _i64, _vp]),

@@ -133,6 +133,18 @@ def qpp_colminmax(raw: torch.Tensor, list_off: torch.Tensor, n_retrievers: int,
     return out
 
 
+def qpp_colmeanstd(raw: torch.Tensor, list_off: torch.Tensor, n_retrievers: int,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[2*R*13]: numpy's column means then stds (1.0 when not > 0), for zscore."""
+    require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    if out is None:
+        out = torch.empty(2 * R * _lib.QPP_COLS, dtype=torch.float64, device=raw.device)
+    _lib.call("qf_qpp_colmeanstd", _ptr(raw), _ptr(list_off), Q, R, _ptr(out), _stream())
+    return out
+
+
 def qpp_normalize(raw: torch.Tensor, mm: Optional[torch.Tensor], list_off: torch.Tensor,
                   n_retrievers: int, mode: str = "minmax", qpp_index: int = 5,
                   want_norm=False, want_micro=True, want_weights=True) -> Dict[str, torch.Tensor]:
@@ -140,7 +152,8 @@ def qpp_normalize(raw: torch.Tensor, mm: Optional[torch.Tensor], list_off: torch
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
     dev = raw.device
-    mode_id = {"none": _lib.NORM_NONE, "minmax": _lib.NORM_MINMAX}.get(mode)
+    mode_id = {"none": _lib.NORM_NONE, "minmax": _lib.NORM_MINMAX,
+               "zscore": _lib.NORM_ZSCORE}.get(mode)
     if mode_id is None:
         raise NotImplementedError(f"QPP normalisation '{mode}' is not implemented on device")
     norm = torch.empty_like(raw) if want_norm else None

@@ -3,7 +3,8 @@
 The reference computes the 13 QPP predictors in a JVM subprocess
 (QPPBridge.java, fed JSON over stdin, src/qpp.py:117-171).  Here the same
 predictors are a HIP kernel (csrc/qf_qpp.hip, one wavefront per ranked list);
-the per-column min-max normalisation and the "%.6f" write-back are kernels too.
+the per-column normalisation (minmax / zscore) and the "%.6f" write-back are
+kernels too.
 Public surface kept: QPPResult, QPPBridge (compute_batch / compute),
 compute_qpp_for_res_file, _normalize_qpp — same arguments, return values,
 output files and exception types (RuntimeError when the engine is unavailable,
@@ -135,20 +136,19 @@ def compute_qpp_for_res_file(res_path: str, output_path: Optional[str] = None,
 
 
 def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, List[float]]:
-    """Per-column normalisation across queries (src/qpp.py:340-374), on device for minmax."""
+    """Per-column normalisation across queries (src/qpp.py:340-374), on device:
+    minmax (min / max) or zscore (numpy's mean / population std, bit-exact)."""
     qids = list(results.keys())
     arr = np.asarray([results[q] for q in qids], dtype=np.float64).reshape(len(qids), -1)
-    if method == "minmax" and arr.shape[1] == _lib.QPP_COLS:
-        import torch
-        dev = engine.require_device()
-        raw = torch.from_numpy(arr).to(dev)
-        off = torch.arange(len(qids) + 1, dtype=torch.int64, device=dev)  # every list present
-        mm = engine.qpp_colminmax(raw, off, 1)
-        norm = engine.qpp_normalize(raw, mm, off, 1, "minmax", qpp_index=0, want_norm=True,
-                                    want_micro=False, want_weights=False)["norm"]
-        vals = norm.cpu().numpy()
-    else:
-        raise NotImplementedError(
-            f"QPP normalisation '{method}' is not implemented on device (minmax, the default "
-            "of config/defaults.yaml:200, is)")
+    if arr.shape[1] != _lib.QPP_COLS:
+        raise ValueError(f"expected {_lib.QPP_COLS} QPP columns, got {arr.shape[1]}")
+    method = "minmax" if method == "minmax" else "zscore"  # src/qpp.py:357-359: else -> zscore
+    import torch
+    dev = engine.require_device()
+    raw = torch.from_numpy(arr).to(dev)
+    off = torch.arange(len(qids) + 1, dtype=torch.int64, device=dev)  # every list present
+    stats = (engine.qpp_colminmax if method == "minmax" else engine.qpp_colmeanstd)(raw, off, 1)
+    norm = engine.qpp_normalize(raw, stats, off, 1, method, qpp_index=0, want_norm=True,
+                                want_micro=False, want_weights=False)["norm"]
+    vals = norm.cpu().numpy()
     return {q: [float(v) for v in vals[i]] for i, q in enumerate(qids)}

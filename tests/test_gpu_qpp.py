@@ -155,3 +155,55 @@ def test_compute_qpp_for_res_file(gpu, tmp_path):
     a = np.array([[float(x) for x in l.split("\t")[1:]] for l in lines])
     b = np.array([[float(x) for x in l.split("\t")[1:]] for l in want_lines])
     assert np.abs(a - b).max() <= 1.0000001e-6
+
+
+def _fmt6(m: int) -> str:
+    sign = "-" if m < 0 else ""
+    m = abs(int(m))
+    return f"{sign}{m // 10**6}.{m % 10**6:06d}"
+
+
+@pytest.mark.parametrize("Q,R", [(1, 1), (7, 1), (8, 1), (129, 1), (3452, 1), (8192, 1),
+                                 (8193, 1), (20000, 1), (1500, 3)])
+def test_zscore_is_numpy_bit_exact(gpu, Q, R):
+    """qf_qpp_colmeanstd + QF_NORM_ZSCORE vs the reference's numpy arr.mean() /
+    arr.std() (src/qpp.py:358-359, via ref_port.normalize_qpp) over the queries
+    with a non-empty list, values compared bit for bit; "%.6f" micro-units too."""
+    from qppfuse import engine
+    rng = np.random.default_rng(Q * 10 + R)
+    raw_h = rng.standard_normal((Q * R, 13)) * 10.0 ** rng.integers(-6, 6, (Q * R, 13))
+    raw_h[:, 11] = raw_h[:, 12]            # duplicated column, as QPPBridge writes it
+    raw_h[:, 3] = 0.25                     # constant column: std 0 -> scale 1.0
+    lens = np.ones(Q * R, np.int64)
+    if R > 1:
+        lens[rng.random(Q * R) < 0.1] = 0  # absent (query, retriever) lists
+    off = np.zeros(Q * R + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    raw = t(raw_h)
+    st = engine.qpp_colmeanstd(raw, t(off), R)
+    o = engine.qpp_normalize(raw, st, t(off), R, "zscore", -1, want_norm=True)
+    norm, micro = o["norm"].cpu().numpy(), o["micro"].cpu().numpy()
+    for r in range(R):
+        rows = [l for l in range(r, Q * R, R) if lens[l] > 0]
+        want = ref_port.normalize_qpp({str(l): raw_h[l].tolist() for l in rows}, "zscore")
+        got = norm[rows]
+        exp = np.array([want[str(l)] for l in rows], np.float64)
+        assert got.tobytes() == exp.tobytes(), r
+        assert [_fmt6(m) for m in micro[rows].ravel()[:200]] == \
+            [f"{v:.6f}" for v in exp.ravel()[:200]]
+    absent = np.where(lens == 0)[0]
+    assert (norm[absent] == 0).all()
+
+
+def test_normalize_qpp_api_zscore(gpu):
+    from qppfuse.qpp import _normalize_qpp
+    rng = np.random.default_rng(5)
+    res = {f"q{i}": (rng.standard_normal(13) * 3).tolist() for i in range(257)}
+    got = _normalize_qpp(res, "zscore")
+    want = ref_port.normalize_qpp(res, "zscore")
+    assert list(got) == list(want)
+    for q in res:
+        assert np.array(got[q]).tobytes() == np.array(want[q], np.float64).tobytes()
+    # the reference takes every method other than "minmax" as zscore (src/qpp.py:357-359)
+    assert _normalize_qpp(res, "other") == got
