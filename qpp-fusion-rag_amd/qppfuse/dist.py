@@ -4,7 +4,12 @@ Fusion is independent per query; QPP normalisation couples the queries of each
 retriever through per-column min / max (src/qpp.py:347-361).  Each rank reduces
 its shard to [min, -max] per (retriever, column) (qf_qpp_colminmax) and one
 element-wise MIN all-reduce (RCCL over xGMI with backend "nccl"; gloo in the CPU
-tests) combines them.  Fused lists stay on the rank that produced them.
+tests) combines them.  zscore normalisation (numpy's mean / std, whose pairwise
+sum depends on every query's position) cannot be combined from shard partials
+bit-exactly: allgather_qpp_raw gives every rank the whole raw predictor table
+(R*13 doubles + one presence flag per query — 0.5 MB per 1,000 queries at R = 5)
+and each rank computes the statistics itself.  Fused lists stay on the rank that
+produced them.
 """
 from __future__ import annotations
 
@@ -38,3 +43,28 @@ def allreduce_minmax(mm, group=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
     return mm
+
+
+def allgather_qpp_raw(raw, present, group=None):
+    """All ranks' raw predictor rows [q*R + r, 13] and presence flags [q*R + r]
+    (contiguous query shards, in rank order) concatenated on every rank."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return raw, present
+    world = dist.get_world_size(group)
+    n = torch.tensor([raw.shape[0]], dtype=torch.int64, device=raw.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    m = max(sizes)
+    pad = torch.zeros((m, raw.shape[1]), dtype=raw.dtype, device=raw.device)
+    pad[: raw.shape[0]] = raw
+    ppad = torch.zeros(m, dtype=torch.int64, device=raw.device)
+    ppad[: raw.shape[0]] = present.to(torch.int64)
+    rows = [torch.empty_like(pad) for _ in range(world)]
+    pres = [torch.empty_like(ppad) for _ in range(world)]
+    dist.all_gather(rows, pad, group=group)
+    dist.all_gather(pres, ppad, group=group)
+    return (torch.cat([t[:k] for t, k in zip(rows, sizes)]),
+            torch.cat([t[:k] for t, k in zip(pres, sizes)]).to(torch.bool))

@@ -73,3 +73,30 @@ def test_sharded_qpp_normalisation_equals_global():
         got = (raw[r::R] - lo[r]) / scale
         for q in range(Q):
             assert got[q].tolist() == [float(v) for v in want[str(q)]]
+
+
+def _gather_worker(rank, world, port, raw, Q, R, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qppfuse.dist import allgather_qpp_raw, shard_range
+    b, e = shard_range(Q, world, rank)
+    mine = torch.from_numpy(raw[b * R:e * R].copy())
+    pres = torch.from_numpy((np.arange(b * R, e * R) % 7 != 3))
+    full, fp = allgather_qpp_raw(mine, pres)
+    out[rank] = (full.numpy().copy(), fp.numpy().copy())
+    dist.destroy_process_group()
+
+
+def test_zscore_gathers_the_whole_table():
+    """zscore needs every query in order on each rank: the gathered table equals the
+    unsharded one, so per-rank device statistics equal the single-GPU ones."""
+    rng = np.random.default_rng(2)
+    Q, R, world = 41, 3, 2
+    raw = rng.normal(0, 5, (Q * R, 13))
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gather_worker, args=(world, _free_port(), raw, Q, R, out), nprocs=world, join=True)
+    for rank in range(world):
+        full, fp = out[rank]
+        assert full.tobytes() == raw.tobytes()
+        assert np.array_equal(fp, np.arange(Q * R) % 7 != 3)
