@@ -48,6 +48,10 @@ int qfio_runset_csr(const qfio_runset* rs, int64_t* list_off, uint32_t* docid, d
 int qfio_runset_strings(const qfio_runset* rs, int64_t* qid_off, char* qid_chars,
                         int64_t* docno_off, char* docno_chars, int64_t* iter_off,
                         char* iter_chars, int64_t* tag_off, char* tag_chars);
+/* strings i = chars[off[i], off[i+1]) of a table, each followed by '\n', into
+ * out (off[n] + n bytes): one decode + split gives Python str objects (no field
+ * of a whitespace-separated run file contains '\n') */
+int qfio_join_lines(const int64_t* off, const char* chars, int64_t n, char* out);
 /* rows of every file in file order (the DataFrames load_runs returns):
  * file_off[R+1], codes into qids / docnos / iters / tags, rank, score */
 int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, uint32_t* docid,

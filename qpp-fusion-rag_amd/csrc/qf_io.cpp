@@ -54,13 +54,6 @@ struct Mapped {
   }
 };
 
-struct Row {
-  std::string_view qid, iter, docno, tag;
-  int64_t rank;
-  double score;
-  int32_t micro;
-  bool micro_ok;
-};
 
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
@@ -105,8 +98,36 @@ inline bool parse_score(std::string_view t, double& v, int32_t& micro, bool& mic
   return end == buf + t.size();
 }
 
-// Parse [begin, end) of a mapped file (whole lines) into rows.
-bool parse_chunk(const char* p, const char* end, std::vector<Row>& rows, std::string& err) {
+// Rows with any non-blank field in [p, end) (pandas skips blank lines).
+size_t count_rows(const char* p, const char* end) {
+  size_t n = 0;
+  while (p < end) {
+    const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+    const char* e = nl ? nl : end;
+    const char* q = p;
+    while (q < e && (is_space(*q))) ++q;
+    n += q < e;
+    p = nl ? nl + 1 : end;
+  }
+  return n;
+}
+
+// Row columns, structure of arrays over all files in file order.
+struct Cols {
+  std::vector<std::string_view> q, d, it, tag;
+  std::vector<int64_t> rank;
+  std::vector<double> score;
+  std::vector<int32_t> micro;
+  void resize(size_t n) {
+    q.resize(n); d.resize(n); it.resize(n); tag.resize(n);
+    rank.resize(n); score.resize(n); micro.resize(n);
+  }
+};
+
+// Parse [begin, end) of a mapped file (whole lines) into rows o, o+1, ...;
+// returns the number of rows whose score is not an exact 6-decimal number.
+bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micro_bad,
+                 std::string& err) {
   while (p < end) {
     std::string_view f[7];
     int nf = 0;
@@ -126,24 +147,31 @@ bool parse_chunk(const char* p, const char* end, std::vector<Row>& rows, std::st
             " in line: " + std::string(line, std::min<size_t>(120, (size_t)(p - line)));
       return false;
     }
-    Row r;
-    r.qid = f[0];
-    r.iter = f[1];
-    r.docno = f[2];
-    r.tag = f[5];
-    char buf[32];
-    if (f[3].size() >= sizeof buf) { err = "bad rank field"; return false; }
-    memcpy(buf, f[3].data(), f[3].size());
-    buf[f[3].size()] = 0;
-    char* e2 = nullptr;
-    r.rank = strtoll(buf, &e2, 10);
-    if (e2 != buf + f[3].size()) { err = "bad rank field '" + std::string(f[3]) + "'"; return false; }
-    r.micro = 0;
-    if (!parse_score(f[4], r.score, r.micro, r.micro_ok)) {
+    c.q[o] = f[0];
+    c.it[o] = f[1];
+    c.d[o] = f[2];
+    c.tag[o] = f[5];
+    // rank: [+-]digits (strtoll's accepted form for plain integer text)
+    {
+      const std::string_view t = f[3];
+      size_t i = 0;
+      bool neg = false;
+      if (i < t.size() && (t[i] == '-' || t[i] == '+')) neg = t[i++] == '-';
+      int64_t v = 0;
+      const size_t d0 = i;
+      while (i < t.size() && t[i] >= '0' && t[i] <= '9' && i - d0 < 18) v = v * 10 + (t[i++] - '0');
+      if (i == d0 || i != t.size()) { err = "bad rank field '" + std::string(t) + "'"; return false; }
+      c.rank[o] = neg ? -v : v;
+    }
+    bool mok = false;
+    int32_t m = 0;
+    if (!parse_score(f[4], c.score[o], m, mok)) {
       err = "bad score field '" + std::string(f[4]) + "'";
       return false;
     }
-    rows.push_back(r);
+    c.micro[o] = m;
+    micro_bad += !mok;
+    ++o;
   }
   return true;
 }
@@ -221,20 +249,69 @@ void intern(const std::vector<std::string_view>& views, std::vector<std::string_
   std::vector<uint32_t> reps(U);  // row of each distinct string
   for (int b = 0; b < P; ++b)
     std::copy(ufirst[b].begin(), ufirst[b].end(), reps.begin() + (long)ubase[b]);
-  std::vector<uint32_t> order(U);
-  for (size_t k = 0; k < U; ++k) order[k] = (uint32_t)k;
-  __gnu_parallel::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    return views[reps[a]] < views[reps[b]];  // byte order == Python's str order for UTF-8
+  // Sort the distinct strings by byte order (== Python's str order for UTF-8).
+  // Keys are the first 16 bytes big-endian, zero-padded (no NUL in the text, so
+  // a proper prefix sorts first); only equal keys compare the strings.  Sorting
+  // 24-byte records keeps the sort in cache instead of chasing string pointers.
+  struct Key {
+    uint64_t k1, k2;
+    uint32_t u;
+  };
+  std::vector<Key> keys(U);
+#pragma omp parallel for schedule(static)
+  for (size_t k = 0; k < U; ++k) {
+    const std::string_view v = views[reps[k]];
+    unsigned char b[16] = {0};
+    memcpy(b, v.data(), std::min<size_t>(16, v.size()));
+    uint64_t k1 = 0, k2 = 0;
+    for (int i = 0; i < 8; ++i) {
+      k1 = (k1 << 8) | b[i];
+      k2 = (k2 << 8) | b[8 + i];
+    }
+    keys[k] = Key{k1, k2, (uint32_t)k};
+  }
+  __gnu_parallel::sort(keys.begin(), keys.end(), [&](const Key& a, const Key& b) {
+    if (a.k1 != b.k1) return a.k1 < b.k1;
+    if (a.k2 != b.k2) return a.k2 < b.k2;
+    return views[reps[a.u]] < views[reps[b.u]];
   });
   std::vector<uint32_t> rank(U);
   uniq.resize(U);
+#pragma omp parallel for schedule(static)
   for (size_t k = 0; k < U; ++k) {
-    rank[order[k]] = (uint32_t)k;
-    uniq[k] = views[reps[order[k]]];
+    rank[keys[k].u] = (uint32_t)k;
+    uniq[k] = views[reps[keys[k].u]];
   }
   id.resize(n);
 #pragma omp parallel for schedule(static)
   for (size_t i = 0; i < n; ++i) id[i] = rank[ubase[hs[i] >> 56] + local[i]];
+}
+
+// intern() for columns made of long runs of one value (qid, Q0, tag): only the
+// run heads are interned.
+void intern_runs(const std::vector<std::string_view>& views, std::vector<std::string_view>& uniq,
+                 std::vector<uint32_t>& id) {
+  const size_t n = views.size();
+  std::vector<uint8_t> head(n);
+#pragma omp parallel for schedule(static)
+  for (size_t i = 0; i < n; ++i) head[i] = i == 0 || views[i] != views[i - 1];
+  std::vector<size_t> hix;
+  for (size_t i = 0; i < n; ++i)
+    if (head[i]) hix.push_back(i);
+  if (hix.size() * 4 > n) {  // not run-structured
+    intern(views, uniq, id);
+    return;
+  }
+  std::vector<std::string_view> hv(hix.size());
+  for (size_t k = 0; k < hix.size(); ++k) hv[k] = views[hix[k]];
+  std::vector<uint32_t> hid;
+  intern(hv, uniq, hid);
+  id.resize(n);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (size_t k = 0; k < hix.size(); ++k) {
+    const size_t e = k + 1 < hix.size() ? hix[k + 1] : n;
+    for (size_t i = hix[k]; i < e; ++i) id[i] = hid[k];
+  }
 }
 
 }  // namespace
@@ -270,7 +347,9 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   if (n_threads > 0) omp_set_num_threads(n_threads);
   auto* rs = new qfio_runset();
   rs->n_files = n_files;
-  std::vector<std::vector<Row>> per_file(n_files);
+  // ---- map every file; chunk at line boundaries; count rows per chunk ----------
+  const int T = std::max(1, omp_get_max_threads());
+  std::vector<const char*> cut((size_t)n_files * (T + 1));
   for (int f = 0; f < n_files; ++f) {
     auto* m = new Mapped();
     rs->maps.push_back(m);
@@ -283,75 +362,62 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
     fstat(m->fd, &st);
     m->size = (size_t)st.st_size;
     if (m->size) {
-      m->data = (const char*)mmap(nullptr, m->size, PROT_READ, MAP_PRIVATE, m->fd, 0);
+      m->data = (const char*)mmap(nullptr, m->size, PROT_READ, MAP_PRIVATE | MAP_POPULATE,
+                                  m->fd, 0);
       if (m->data == MAP_FAILED) {
         m->data = nullptr;
         delete rs;
         return fail(QFIO_EIO, std::string("cannot map ") + paths[f]);
       }
-      madvise((void*)m->data, m->size, MADV_SEQUENTIAL);
     }
-    // chunk at line boundaries
-    const int T = std::max(1, omp_get_max_threads());
-    std::vector<const char*> cut(T + 1);
-    cut[0] = m->data;
-    cut[T] = m->data + m->size;
+    const char** c = &cut[(size_t)f * (T + 1)];
+    c[0] = m->data;
+    c[T] = m->data + m->size;
     for (int t = 1; t < T; ++t) {
-      const char* c = m->data + (m->size * (size_t)t) / (size_t)T;
-      while (c < cut[T] && c > m->data && c[-1] != '\n') ++c;
-      cut[t] = std::max(c, cut[t - 1]);
+      const char* x = m->data + (m->size * (size_t)t) / (size_t)T;
+      while (x < c[T] && x > m->data && x[-1] != '\n') ++x;
+      c[t] = std::max(x, c[t - 1]);
     }
-    std::vector<std::vector<Row>> parts(T);
-    std::vector<std::string> errs(T);
-    int bad = 0;
-#pragma omp parallel for schedule(static, 1) reduction(+ : bad)
-    for (int t = 0; t < T; ++t) {
-      parts[t].reserve((size_t)(cut[t + 1] - cut[t]) / 40 + 16);
-      if (!parse_chunk(cut[t], cut[t + 1], parts[t], errs[t])) bad += 1;
-    }
-    for (int t = 0; t < T; ++t)
-      if (!errs[t].empty()) {
-        const std::string e = std::string(paths[f]) + ": " + errs[t];
-        delete rs;
-        return fail(QFIO_EPARSE, e);
-      }
-    size_t n = 0;
-    for (auto& v : parts) n += v.size();
-    per_file[f].reserve(n);
-    for (auto& v : parts) per_file[f].insert(per_file[f].end(), v.begin(), v.end());
   }
-  // ---- flatten (file order), intern qids / docnos / iter / tag -----------------
-  rs->file_off.assign(n_files + 1, 0);
-  for (int f = 0; f < n_files; ++f) rs->file_off[f + 1] = rs->file_off[f] + (int64_t)per_file[f].size();
-  const size_t E = (size_t)rs->file_off[n_files];
+  const size_t NC = (size_t)n_files * T;
+  std::vector<size_t> nrow(NC + 1, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (size_t k = 0; k < NC; ++k) {
+    const size_t f = k / T, t = k % T;
+    nrow[k + 1] = count_rows(cut[f * (T + 1) + t], cut[f * (T + 1) + t + 1]);
+  }
+  for (size_t k = 0; k < NC; ++k) nrow[k + 1] += nrow[k];
+  const size_t E = nrow[NC];
   if (E >= 0xFFFFFFFFull) { delete rs; return fail(QFIO_EINVAL, "too many rows"); }
-  std::vector<std::string_view> vq(E), vd(E), vi(E), vt(E);
-  rs->row_rank.resize(E);
-  rs->row_score.resize(E);
-  std::vector<int32_t> row_micro(E);
-  int micro_bad = 0;
-  for (int f = 0; f < n_files; ++f) {
-    const int64_t o = rs->file_off[f];
-    const auto& rows = per_file[f];
-#pragma omp parallel for schedule(static) reduction(+ : micro_bad)
-    for (int64_t i = 0; i < (int64_t)rows.size(); ++i) {
-      const Row& r = rows[i];
-      vq[o + i] = r.qid;
-      vd[o + i] = r.docno;
-      vi[o + i] = r.iter;
-      vt[o + i] = r.tag;
-      rs->row_rank[o + i] = r.rank;
-      rs->row_score[o + i] = r.score;
-      row_micro[o + i] = r.micro;
-      micro_bad += !r.micro_ok;
-    }
-    std::vector<Row>().swap(per_file[f]);
+  rs->file_off.assign(n_files + 1, 0);
+  for (int f = 0; f <= n_files; ++f) rs->file_off[f] = (int64_t)nrow[(size_t)f * T];
+  // ---- parse every chunk straight into its rows ------------------------------
+  Cols cols;
+  cols.resize(E);
+  std::vector<std::string> errs(NC);
+  std::vector<size_t> mbad(NC, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (size_t k = 0; k < NC; ++k) {
+    const size_t f = k / T, t = k % T;
+    parse_chunk(cut[f * (T + 1) + t], cut[f * (T + 1) + t + 1], cols, nrow[k], mbad[k], errs[k]);
   }
+  for (size_t k = 0; k < NC; ++k)
+    if (!errs[k].empty()) {
+      const std::string e = std::string(paths[k / T]) + ": " + errs[k];
+      delete rs;
+      return fail(QFIO_EPARSE, e);
+    }
+  size_t micro_bad = 0;
+  for (size_t k = 0; k < NC; ++k) micro_bad += mbad[k];
   rs->micro_ok = micro_bad == 0;
-  intern(vq, rs->qids, rs->row_qid);
-  intern(vd, rs->docnos, rs->row_docid);
-  intern(vi, rs->iters, rs->row_iter);
-  intern(vt, rs->tags, rs->row_tag);
+  rs->row_rank = std::move(cols.rank);
+  rs->row_score = std::move(cols.score);
+  std::vector<int32_t> row_micro = std::move(cols.micro);
+  // ---- intern qids / docnos / iter / tag ---------------------------------------
+  intern_runs(cols.q, rs->qids, rs->row_qid);
+  intern(cols.d, rs->docnos, rs->row_docid);
+  intern_runs(cols.it, rs->iters, rs->row_iter);
+  intern_runs(cols.tag, rs->tags, rs->row_tag);
   if (rs->docnos.size() >= 0xFFFFFFFFull) { delete rs; return fail(QFIO_EINVAL, "too many docnos"); }
   // ---- CSR by (query, file), stable in file order -------------------------------
   const int64_t Q = (int64_t)rs->qids.size(), R = n_files;
@@ -365,6 +431,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->score.resize(E);
   rs->rank.resize(E);
   rs->micro.resize(rs->micro_ok ? E : 0);
+#pragma omp parallel for schedule(dynamic, 1)
   for (int f = 0; f < n_files; ++f)
     for (int64_t i = rs->file_off[f]; i < rs->file_off[f + 1]; ++i) {
       const int64_t d = pos[(int64_t)rs->row_qid[i] * R + f]++;
@@ -420,6 +487,17 @@ int qfio_runset_strings(const qfio_runset* rs, int64_t* qid_off, char* qid_chars
   copy_strings(rs->docnos, docno_off, docno_chars);
   copy_strings(rs->iters, iter_off, iter_chars);
   copy_strings(rs->tags, tag_off, tag_chars);
+  return QFIO_OK;
+}
+
+int qfio_join_lines(const int64_t* off, const char* chars, int64_t n, char* out) {
+  if (n < 0 || (n > 0 && (!off || !chars || !out))) return fail(QFIO_EINVAL, "qfio_join_lines: bad arguments");
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t a = off[i], len = off[i + 1] - a;
+    memcpy(out + a + i, chars + a, (size_t)len);
+    out[a + i + len] = '\n';
+  }
   return QFIO_OK;
 }
 

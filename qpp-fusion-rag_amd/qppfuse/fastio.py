@@ -3,7 +3,7 @@
 load_runs parses every run file in C++ (memory-mapped, multithreaded) straight
 into the packed RunSet the device kernels read, and also returns the
 DataFrames the reference's load_runs returns (src/fusion.py:46-76) — qid /
-docno / iter / runid as pandas categoricals over the interned strings, rank
+docno / iter / runid as object columns of the interned strings, rank
 int64, score float64, rows in file order — with the RunSet cached for them, so
 the fusions that follow skip packing.  write_run writes one fused run the way
 write_runfile does (src/fusion.py:480-492), formatting in C++ with Python's
@@ -43,6 +43,8 @@ def lib() -> C.CDLL:
         L.qfio_runset_strings.argtypes = [_vp] + [_vp] * 8
         L.qfio_runset_rows.restype = C.c_int
         L.qfio_runset_rows.argtypes = [_vp] + [_vp] * 7
+        L.qfio_join_lines.restype = C.c_int
+        L.qfio_join_lines.argtypes = [_vp, _vp, _i64, _vp]
         L.qfio_runset_free.restype = None
         L.qfio_runset_free.argtypes = [_vp]
         L.qfio_format_score.restype = C.c_size_t
@@ -69,17 +71,15 @@ def _p(a: np.ndarray):
 
 
 def _strings(off: np.ndarray, chars: np.ndarray) -> np.ndarray:
-    """Offsets + bytes -> object array of str (one C-speed decode + split)."""
+    """Offsets + bytes -> object array of str (C join with newlines, one decode + split)."""
     n = len(off) - 1
     if n == 0:
         return np.zeros(0, dtype=object)
-    total = int(off[-1])
-    blob = np.zeros(total + n, np.uint8)  # each string followed by a NUL
-    lens = np.diff(off)
-    blob[np.arange(total) + np.repeat(np.arange(n), lens)] = chars[:total]
-    parts = blob.tobytes().decode().split("\0")
+    blob = np.empty(int(off[-1]) + n, np.uint8)
+    _check(lib().qfio_join_lines(_p(np.ascontiguousarray(off, np.int64)), _p(chars), n, _p(blob)),
+           "join_lines")
     out = np.empty(n, dtype=object)
-    out[:] = parts[:n]
+    out[:] = blob.tobytes().decode().split("\n")[:n]
     return out
 
 
@@ -134,19 +134,12 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
     rs.canonical = bool(np.all(score[1:][same] <= score[:-1][same]) and
                         np.all(rank[1:][same] > rank[:-1][same])) if E > 1 else True
     rs._strtab = {"qid": (qo, qc.tobytes()), "docno": (do, dc.tobytes())}
-    qcat = pd.CategoricalDtype(pd.Index(qids, dtype=object))
-    dcat = pd.CategoricalDtype(pd.Index(docnos, dtype=object))
-    icat = pd.CategoricalDtype(pd.Index(iters, dtype=object))
-    tcat = pd.CategoricalDtype(pd.Index(tags, dtype=object))
     frames = {}
     for r, name in enumerate(names):
         a, b = int(fo[r]), int(fo[r + 1])
         frames[name] = pd.DataFrame({
-            "qid": pd.Categorical.from_codes(rq[a:b].astype(np.int64), dtype=qcat),
-            "iter": pd.Categorical.from_codes(ri[a:b].astype(np.int64), dtype=icat),
-            "docno": pd.Categorical.from_codes(rd[a:b].astype(np.int64), dtype=dcat),
-            "rank": rr[a:b], "score": rsc[a:b],
-            "runid": pd.Categorical.from_codes(rt[a:b].astype(np.int64), dtype=tcat)})
+            "qid": qids[rq[a:b]], "iter": iters[ri[a:b]], "docno": docnos[rd[a:b]],
+            "rank": rr[a:b], "score": rsc[a:b], "runid": tags[rt[a:b]]}, copy=False)
     return rs, frames
 
 

@@ -48,7 +48,8 @@ def load_runs(res_path: str, use_normalized: bool = True) -> Dict[str, pd.DataFr
 
     Parsed natively (qppfuse.fastio, csrc/qf_io.cpp) into the packed run set the
     kernels read — cached for these frames, so the fusions skip packing.  The
-    string columns are pandas categoricals over the interned values."""
+    string columns hold the interned str objects (dtype object, as pandas reads
+    them in the reference)."""
     from . import fastio
     suffix = ".norm.res" if use_normalized else ".res"
     files = [f for f in os.listdir(res_path) if f.endswith(suffix)]

@@ -1,0 +1,127 @@
+"""End-to-end drop-in timing (development tool; DESIGN.md "End to end").
+
+C2-shaped run files (3,452 queries x 5 retrievers x top-1000, `.norm.res` text)
+are generated once, then the reference's fusion entry points are timed through
+this package as scripts/05_fusion.py would call them:
+  load_runs (native parse) -> load_qpp_scores -> fuse_many (6 methods: H2D,
+  qf_fuse, D2H) -> write_runfile x 6 (native writer).
+python tools/e2e.py [--queries Q] [--dir DIR]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+from types import SimpleNamespace
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+NAMES = ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade"]
+METHODS = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+
+
+def ascii_table(prefix: bytes, ids: np.ndarray):
+    """(offsets, bytes) of prefix + decimal(id) for every id, vectorised."""
+    ids = ids.astype(np.int64)
+    nd = np.maximum(1, np.floor(np.log10(np.maximum(ids, 1))).astype(np.int64) + 1)
+    W = int(nd.max())
+    dig = np.zeros((len(ids), W), np.uint8)
+    v = ids.copy()
+    for k in range(W - 1, -1, -1):
+        dig[:, k] = 48 + v % 10
+        v //= 10
+    lens = nd + len(prefix)
+    off = np.zeros(len(ids) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    out = np.empty(int(off[-1]), np.uint8)
+    pos = off[:-1]
+    for i, ch in enumerate(prefix):
+        out[pos + i] = ch
+    keep = np.arange(W)[None, :] >= (W - nd)[:, None]
+    dst = (pos + len(prefix))[:, None] + (np.arange(W)[None, :] - (W - nd)[:, None])
+    out[dst[keep]] = dig[keep]
+    return off, out.tobytes()
+
+
+def generate(d: Path, Q: int, R: int, K: int):
+    from qppfuse import engine, fastio
+    off, docid, raw = engine.synth_runs(0, Q, R, K)
+    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+    nt = torch.full((Q,), 4, dtype=torch.int32, device=off.device)
+    tf = torch.rand((Q, 2), dtype=torch.float64, device=off.device)
+    qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
+    mm = engine.qpp_colminmax(qraw, off, R)
+    qmicro = engine.qpp_normalize(qraw, mm, off, R, "minmax", 5)["micro"].cpu().numpy()
+    off_h = off.cpu().numpy()
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    uniq, inv = np.unique(doc_h, return_inverse=True)
+    rs = SimpleNamespace(qids=None, docnos=None)
+    rs._strtab = {"qid": ascii_table(b"test", np.arange(Q)), "docno": ascii_table(b"doc", uniq)}
+    ud = inv.astype(np.uint32)
+    pos = (np.arange(len(doc_h)) - np.repeat(off_h[:-1], np.diff(off_h))).astype(np.uint16)
+    for r, name in enumerate(NAMES[:R]):
+        qb = off_h[r:-1:R][:Q]
+        cnt = np.diff(off_h)[r::R][:Q].astype(np.int32)
+        fastio.write_run(str(d / f"{name}.norm.res"), np.arange(Q), qb, cnt, ud, pos, sc_h, rs,
+                         name)
+    qd = d / "qpp"
+    qd.mkdir(exist_ok=True)
+    for r, name in enumerate(NAMES[:R]):
+        with open(qd / f"{name}.res.mmnorm.qpp", "w") as fh:
+            for q in range(Q):
+                m = qmicro[q * R + r]
+                fh.write(f"test{q}\t" + "\t".join(f"{v // 10**6}.{v % 10**6:06d}" for v in m) + "\n")
+    return int(off_h[-1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--queries", type=int, default=3452)
+    ap.add_argument("--dir", default=None)
+    ap.add_argument("--repeat", type=int, default=2)
+    a = ap.parse_args()
+    from qppfuse import fusion
+    torch.cuda.set_device(0)
+    d = Path(a.dir or tempfile.mkdtemp(prefix="qf_e2e_"))
+    d.mkdir(parents=True, exist_ok=True)
+    t0 = time.perf_counter()
+    E = generate(d, a.queries, 5, 1000)
+    gen_s = time.perf_counter() - t0
+    size = sum(f.stat().st_size for f in d.glob("*.norm.res"))
+    best = None
+    for _ in range(a.repeat):
+        fusion._PACK_CACHE.clear()
+        t = {}
+        t0 = time.perf_counter()
+        runs = fusion.load_runs(str(d))
+        t["load_runs_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        qpp = fusion.load_qpp_scores(str(d / "qpp"))
+        t["load_qpp_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        res = fusion.fuse_many(runs, METHODS, qpp, 5)
+        torch.cuda.synchronize()
+        t["fuse_6_methods_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for m in METHODS:
+            fusion.write_runfile(res[m], str(d / f"fused_{m}.res"), m)
+        t["write_6_runfiles_s"] = time.perf_counter() - t0
+        t["total_s"] = sum(t.values())
+        if best is None or t["total_s"] < best["total_s"]:
+            best = t
+    out_bytes = sum((d / f"fused_{m}.res").stat().st_size for m in METHODS)
+    best = {k: round(v, 4) for k, v in best.items()}
+    print(json.dumps({"queries": a.queries, "entries": E, "input_bytes": size,
+                      "output_bytes": out_bytes, "generate_s": round(gen_s, 2), **best,
+                      "e2e_fused_queries_per_s": round(a.queries * 6 / best["total_s"], 1),
+                      "cpu_threads": os.cpu_count()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
