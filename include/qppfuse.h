@@ -55,6 +55,13 @@ extern "C" {
                                 groupby-sum (Kahan) order; ties by docno.  Takes
                                 its weights (qf_learned_weights) in `weights`, so
                                 it cannot share a call with the W-* methods. */
+#define QF_PROBFUSE (1 << 7) /* probFuse (ProbFuse.py:136-187 build_probfuse_run):
+                                sum over runs of P_r[seg - 1] / seg, seg =
+                                ceil(rank * x / L) clipped to [1, x], rank = the
+                                file rank column; only via qf_fuse_probfuse */
+#define QF_WRRF_MUL (1 << 8) /* QPPrrf_argmax.py:53-76 build_rrf_run: sum over runs
+                                of w_r * (1 / (k + rank)), file rank column, rows
+                                in file order (weights 1.0 = its plain RRF) */
 #define QF_ALL_METHODS 0x3F  /* the six fusions of config.fusion.methods */
 
 /* ---- score column encodings --------------------------------------------- */
@@ -163,6 +170,20 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
             int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
             uint16_t* perm, double* fused, int64_t out_stride, void* stream);
+
+/*
+ * qf_fuse with the ProbFuse segment table (ProbFuse.py:136-187): `methods` may
+ * add QF_PROBFUSE to the qf_fuse methods; seg_prob[r * n_segments + k - 1] is
+ * P_k of run r (train_probfuse, ProbFuse.py:92-133; zeros for a run the model
+ * does not know), n_segments = x, seg_len = L.  Other arguments as qf_fuse.
+ */
+int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                     const uint32_t* docid, const void* score, int32_t score_kind,
+                     const int32_t* rank, const double* weights, int32_t methods,
+                     int32_t rrf_k, const double* seg_prob, int32_t n_segments,
+                     int32_t seg_len, int32_t max_entries, uint32_t* union_docid,
+                     int32_t* union_count, uint16_t* perm, double* fused, int64_t out_stride,
+                     void* stream);
 
 /*
  * LightGBM inference for learned fusion (src/fusion.py:415-429 ->

@@ -323,3 +323,94 @@ def learned_fusion_from_weights(runs: Dict[str, pd.DataFrame], weights_dict, n_r
     for _, row in aggregated.iterrows():
         fused[row["qid"]].append((row["docno"], row["weighted_score"]))
     return dict(fused)
+
+
+# ---- research fusion scripts: faithful loops --------------------
+
+def probfuse_pos_to_segment(pos, L, x):
+    """ProbFuse.py:30-39."""
+    import math
+    if pos <= 0:
+        pos = 1
+    k = math.ceil((pos * x) / float(L))
+    if k < 1:
+        k = 1
+    if k > x:
+        k = x
+    return int(k)
+
+
+def train_probfuse(runs_train, qrels_train_dict, x=25, L=100, variant="judged", eps=0.0):
+    """ProbFuse.py:92-133, row by row."""
+    P_probs = {}
+    for ranker, df in runs_train.items():
+        rel_counts, nonrel_counts, total_counts = [0] * x, [0] * x, [0] * x
+        for qid in sorted(df["qid"].unique()):
+            sub = df[df["qid"] == qid]
+            for _, row in sub.iterrows():
+                k = probfuse_pos_to_segment(int(row["rank"]), L, x) - 1
+                doc = str(row["docno"])
+                total_counts[k] += 1
+                if qid in qrels_train_dict and doc in qrels_train_dict[qid]:
+                    if qrels_train_dict[qid][doc] > 0:
+                        rel_counts[k] += 1
+                    else:
+                        nonrel_counts[k] += 1
+        probs = [0.0] * x
+        for k in range(x):
+            if variant.lower() == "all":
+                denom, num = total_counts[k], rel_counts[k]
+            else:
+                denom, num = rel_counts[k] + nonrel_counts[k], rel_counts[k]
+            probs[k] = float(num) / float(denom) if denom > 0 else eps
+        P_probs[ranker] = probs
+    return P_probs
+
+
+def build_probfuse_run(runs_test, P_probs, x=25, L=100, run_tag="probFuse"):
+    """ProbFuse.py:136-187, row by row."""
+    from collections import defaultdict
+    records = []
+    rankers = list(runs_test.keys())
+    all_qids = set()
+    for r in rankers:
+        all_qids.update(runs_test[r]["qid"].unique())
+    for qid in sorted(all_qids, key=lambda x: int(x) if x.isdigit() else x):
+        doc_scores = defaultdict(float)
+        for ranker in rankers:
+            df_q = runs_test[ranker][runs_test[ranker]["qid"] == qid]
+            for _, row in df_q.iterrows():
+                k = probfuse_pos_to_segment(int(row["rank"]), L, x)
+                prob = P_probs[ranker][k - 1] if ranker in P_probs else 0.0
+                doc_scores[str(row["docno"])] += prob / float(k) if k > 0 else 0.0
+        for rank, (docno, score) in enumerate(sorted(doc_scores.items(), key=lambda t: t[1],
+                                                     reverse=True), start=1):
+            records.append([qid, "Q0", docno, rank, score, run_tag])
+    return pd.DataFrame(records, columns=["qid", "iter", "docno", "rank", "score", "runid"])
+
+
+def build_rrf_run(runs, k=60, qpp_data=None, qpp_method_index=None):
+    """QPPrrf_argmax.py:53-76, row by row."""
+    from collections import defaultdict
+    records = []
+    rankers = list(runs.keys())
+    for qid in runs[rankers[0]]["qid"].unique():
+        doc_scores = defaultdict(float)
+        for ranker in rankers:
+            df_q = runs[ranker][runs[ranker]["qid"] == int(qid)]
+            if df_q.empty:
+                continue
+            weight = 1.0
+            if qpp_data and qpp_method_index is not None:
+                try:
+                    weight = qpp_data[str(qid)][ranker][qpp_method_index]
+                except KeyError:
+                    weight = 0.0
+            for _, row in df_q.iterrows():
+                doc_scores[row["docno"]] += weight * (1.0 / (k + row["rank"]))
+        if doc_scores:
+            for rank, (docno, score) in enumerate(sorted(doc_scores.items(), key=lambda t: t[1],
+                                                         reverse=True), start=1):
+                records.append([qid, "Q0", docno, rank, score,
+                                "Weighted-RRF" if qpp_data else "RRF"])
+    return pd.DataFrame(records, columns=["qid", "iter", "docno", "rank", "score", "runid"])

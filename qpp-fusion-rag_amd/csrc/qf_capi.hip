@@ -93,33 +93,63 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
                "qf_qpp_normalize");
 }
 
+static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                       const uint32_t* docid, const void* score, int32_t score_kind,
+                       const int32_t* rank, const double* weights, int32_t methods,
+                       int32_t rrf_k, const double* seg_prob, int32_t n_seg, int32_t seg_len,
+                       int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
+                       uint16_t* perm, double* fused, int64_t out_stride, void* stream,
+                       const char* fn) {
+  if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
+    return fail(QF_EINVAL, "%s: n_retrievers must be in [1, %d]", fn, kMaxR);
+  if (methods <= 0 ||
+      (methods & ~(QF_ALL_METHODS | QF_LEARNED | QF_PROBFUSE | QF_WRRF_MUL)))
+    return fail(QF_EINVAL, "%s: bad method mask 0x%x", fn, methods);
+  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_LEARNED | QF_WRRF_MUL)) && !weights)
+    return fail(QF_EINVAL, "%s: weighted method requested without weights", fn);
+  if ((methods & QF_LEARNED) && (methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_WRRF_MUL)))
+    return fail(QF_EINVAL, "%s: QF_LEARNED and the W-* methods need different weights", fn);
+  if ((methods & QF_PROBFUSE) && (!seg_prob || n_seg <= 0 || seg_len <= 0))
+    return fail(QF_EINVAL, "%s: QF_PROBFUSE needs the segment table, x > 0 and L > 0", fn);
+  if (score_kind != QF_SCORE_F64 && score_kind != QF_SCORE_MICRO)
+    return fail(QF_EINVAL, "%s: bad score_kind %d", fn, score_kind);
+  if (max_entries > qf::fuse_max_entries())
+    return fail(QF_ETOOBIG, "%s: %d entries in one query exceed the kernel limit %d", fn,
+                max_entries, qf::fuse_max_entries());
+  if (n_queries == 0) return QF_OK;
+  if (!list_off || !docid || !score || !union_docid || !union_count || !perm || !fused ||
+      out_stride < 0)
+    return fail(QF_EINVAL, "%s: null buffer", fn);
+  qf::FuseParams p{n_queries, n_retrievers, list_off,    docid,       score, rank,
+                   weights,   methods,      rrf_k,       union_docid, union_count,
+                   perm,      fused,        out_stride,  seg_prob,    n_seg, seg_len};
+  return check(qf::fuse_launch(p, score_kind, max_entries < 1 ? 1 : max_entries,
+                               (hipStream_t)stream),
+               fn);
+}
+
 int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
             const double* weights, int32_t methods, int32_t rrf_k, int32_t max_entries,
             uint32_t* union_docid, int32_t* union_count, uint16_t* perm, double* fused,
             int64_t out_stride, void* stream) {
-  if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
-    return fail(QF_EINVAL, "qf_fuse: n_retrievers must be in [1, %d]", kMaxR);
-  if (methods <= 0 || (methods & ~(QF_ALL_METHODS | QF_LEARNED)))
-    return fail(QF_EINVAL, "qf_fuse: bad method mask 0x%x", methods);
-  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_LEARNED)) && !weights)
-    return fail(QF_EINVAL, "qf_fuse: weighted method requested without weights");
-  if ((methods & QF_LEARNED) && (methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF)))
-    return fail(QF_EINVAL, "qf_fuse: QF_LEARNED and the W-* methods need different weights");
-  if (score_kind != QF_SCORE_F64 && score_kind != QF_SCORE_MICRO)
-    return fail(QF_EINVAL, "qf_fuse: bad score_kind %d", score_kind);
-  if (max_entries > qf::fuse_max_entries())
-    return fail(QF_ETOOBIG, "qf_fuse: %d entries in one query exceed the kernel limit %d",
-                max_entries, qf::fuse_max_entries());
-  if (n_queries == 0) return QF_OK;
-  if (!list_off || !docid || !score || !union_docid || !union_count || !perm || !fused ||
-      out_stride < 0)
-    return fail(QF_EINVAL, "qf_fuse: null buffer");
-  qf::FuseParams p{n_queries, n_retrievers, list_off,    docid, score, rank,       weights,
-                   methods,   rrf_k,        union_docid, union_count, perm, fused, out_stride};
-  return check(qf::fuse_launch(p, score_kind, max_entries < 1 ? 1 : max_entries,
-                               (hipStream_t)stream),
-               "qf_fuse");
+  if (methods & QF_PROBFUSE)
+    return fail(QF_EINVAL, "qf_fuse: QF_PROBFUSE needs qf_fuse_probfuse (segment table)");
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
+                     methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
+                     fused, out_stride, stream, "qf_fuse");
+}
+
+int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                     const uint32_t* docid, const void* score, int32_t score_kind,
+                     const int32_t* rank, const double* weights, int32_t methods,
+                     int32_t rrf_k, const double* seg_prob, int32_t n_segments,
+                     int32_t seg_len, int32_t max_entries, uint32_t* union_docid,
+                     int32_t* union_count, uint16_t* perm, double* fused, int64_t out_stride,
+                     void* stream) {
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
+                     methods, rrf_k, seg_prob, n_segments, seg_len, max_entries, union_docid,
+                     union_count, perm, fused, out_stride, stream, "qf_fuse_probfuse");
 }
 
 int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,

@@ -31,6 +31,7 @@
 namespace qf {
 
 constexpr int kRMax = 16;
+constexpr int kNMethods = 9;  // method bits QF_COMBSUM .. QF_WRRF_MUL
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 #ifdef QF_STAMPS
@@ -607,14 +608,14 @@ void join_kernel(FuseParams p) {
   QF_STAMP(7);
   // ---- fused score of every document, every requested method ------------------
   const int methods = p.methods, rrf_k = p.rrf_k;
-  int slot[7];
-  for (int t = 0, c = 0; t < 7; ++t) {
+  int slot[kNMethods];
+  for (int t = 0, c = 0; t < kNMethods; ++t) {
     slot[t] = c;
     c += (methods >> t) & 1;
   }
   for (int u = tid; u < U; u += BLOCK) {
     const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0, a6 = 0.0, c6 = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0, a6 = 0.0, c6 = 0.0, a7 = 0.0, a8 = 0.0;
     for (int k = gs; k < ge; ++k) {
       const double s = ScoreIn<KIND>::val(gsc[k]);
       const uint32_t q2 = gpr[k];
@@ -628,6 +629,19 @@ void join_kernel(FuseParams p) {
       if (methods & QF_WRRF) {                                      // src/fusion.py:374
         const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
         a5 += s_w[r] / (double)(rrf_k + rk);
+      }
+      if (methods & (QF_PROBFUSE | QF_WRRF_MUL)) {
+        const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;  // int(row["rank"])
+        if (methods & QF_PROBFUSE) {  // ProbFuse.py:30-39,172-179
+          // ceil(rank * x / L) in integers (exact: the float quotient of two
+          // integers below 2^26 is never rounded onto an integer), clipped to [1, x]
+          const int64_t pp = rk > 0 ? rk : 1;
+          int64_t k = (pp * p.n_seg + p.seg_len - 1) / p.seg_len;
+          k = k < 1 ? 1 : (k > p.n_seg ? p.n_seg : k);
+          a7 += p.seg_prob[r * p.n_seg + (int)k - 1] / (double)k;
+        }
+        if (methods & QF_WRRF_MUL)  // QPPrrf_argmax.py:71: weight * (1.0 / (k + rank))
+          a8 += s_w[r] * (1.0 / (double)(rrf_k + rk));
       }
       if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
         const double y = s * s_w[r] - c6;
@@ -647,6 +661,8 @@ void join_kernel(FuseParams p) {
     if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
     if (methods & QF_WRRF) out[slot[5] * st] = a5;
     if (methods & QF_LEARNED) out[slot[6] * st] = a6;
+    if (methods & QF_PROBFUSE) out[slot[7] * st] = a7;
+    if (methods & QF_WRRF_MUL) out[slot[8] * st] = a8;
   }
   if (tid == 0) p.union_count[q] = s_status ? s_status : U;
   QF_STAMP(14);
@@ -793,7 +809,7 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
 }
 // Method bit of output slot ms.
 __device__ __forceinline__ int slot_method(int methods, int ms) {
-  for (int t = 0, c = 0; t < 7; ++t)
+  for (int t = 0, c = 0; t < kNMethods; ++t)
     if ((methods >> t) & 1) {
       if (c == ms) return t;
       ++c;

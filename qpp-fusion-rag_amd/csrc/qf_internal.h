@@ -21,6 +21,8 @@ struct FuseParams {
   uint16_t* perm;
   double* fused;
   int64_t out_stride;
+  const double* seg_prob;  // QF_PROBFUSE: [R][n_seg] segment probabilities
+  int32_t n_seg, seg_len;  // x and L of ProbFuse.py
 };
 
 // IR evaluation (qf_eval): run m, query q reads its ranked list at

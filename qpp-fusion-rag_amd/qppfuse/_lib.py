@@ -17,9 +17,11 @@ QF_QSTATUS = {-1: "query exceeds the fusion kernel's entry limit",
               -4: "reserved docid 0xFFFFFFFF",
               -5: "a docno repeats within one run list (unsupported)"}
 
-COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF, LEARNED = (1 << i for i in range(7))
+COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF, LEARNED, PROBFUSE, WRRF_MUL = \
+    (1 << i for i in range(9))
 METHOD_BITS = {"combsum": COMBSUM, "combmnz": COMBMNZ, "rrf": RRF,
-               "wcombsum": WCOMBSUM, "wcombmnz": WCOMBMNZ, "wrrf": WRRF, "learned": LEARNED}
+               "wcombsum": WCOMBSUM, "wcombmnz": WCOMBMNZ, "wrrf": WRRF, "learned": LEARNED,
+               "probfuse": PROBFUSE, "wrrf_mul": WRRF_MUL}
 SCORE_F64, SCORE_MICRO = 0, 1
 NORM_NONE, NORM_MINMAX, NORM_ZSCORE = 0, 1, 2
 QPP_COLS = 13
@@ -39,6 +41,8 @@ SIGNATURES = {
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
                           _vp, _vp, _vp, _vp, _i64, _vp]),
+    "qf_fuse_probfuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp,
+                                   _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_eval": (C.c_int, [_i64, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp,
                           _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_gbdt_predict": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

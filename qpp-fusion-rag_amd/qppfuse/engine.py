@@ -15,7 +15,8 @@ import torch
 
 from . import _lib
 
-_MNAMES = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf", "learned"]
+_MNAMES = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf", "learned", "probfuse",
+           "wrrf_mul"]
 
 
 def require_device() -> torch.device:
@@ -73,8 +74,10 @@ def alloc_fuse_out(n_queries: int, n_entries: int, mask: int, device) -> FuseOut
 def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_retrievers: int,
          methods, rrf_k: int = 60, weights: Optional[torch.Tensor] = None,
          rank: Optional[torch.Tensor] = None, max_entries: Optional[int] = None,
-         out: Optional[FuseOut] = None) -> FuseOut:
-    """qf_fuse over every query of a packed run set (see include/qppfuse.h)."""
+         out: Optional[FuseOut] = None, seg_prob: Optional[torch.Tensor] = None,
+         n_segments: int = 0, seg_len: int = 0) -> FuseOut:
+    """qf_fuse over every query of a packed run set (see include/qppfuse.h); with
+    "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
@@ -90,6 +93,14 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
         raise ValueError("max_entries (largest per-query entry count) is required")
     if out is None:
         out = alloc_fuse_out(Q, E, mask, dev)
+    if mask & _lib.PROBFUSE:
+        if seg_prob is None or seg_prob.dtype != torch.float64 or seg_prob.numel() != R * n_segments:
+            raise ValueError("probfuse needs seg_prob: float64 [n_retrievers * n_segments]")
+        _lib.call("qf_fuse_probfuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
+                  _ptr(rank), _ptr(weights), mask, int(rrf_k), _ptr(seg_prob), int(n_segments),
+                  int(seg_len), int(max_entries), _ptr(out.union_docid), _ptr(out.union_count),
+                  _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], _stream())
+        return out
     _lib.call("qf_fuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
               _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
               _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused), out.fused.shape[1],

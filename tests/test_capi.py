@@ -17,7 +17,8 @@ def test_header_declares_expected_entry_points():
     fns = header_functions()
     for name in ["qf_fuse", "qf_minmax_per_query", "qf_qpp_raw", "qf_qpp_colminmax",
                  "qf_qpp_normalize", "qf_last_error", "qf_version", "qf_max_entries_per_query",
-                 "qf_synth_runs", "qf_eval", "qf_gbdt_predict", "qf_learned_weights"]:
+                 "qf_synth_runs", "qf_eval", "qf_gbdt_predict", "qf_learned_weights",
+                 "qf_qpp_colmeanstd", "qf_fuse_probfuse"]:
         assert name in fns
 
 
@@ -43,7 +44,14 @@ def test_argument_validation_without_device():
     with pytest.raises(ValueError, match="n_retrievers"):
         _lib.call("qf_fuse", 1, 0, None, None, None, 0, None, None, 1, 60, 10, *tail)
     with pytest.raises(ValueError, match="method mask"):
-        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, 0x80, 60, 10, *tail)
+        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, 0x200, 60, 10, *tail)
+    with pytest.raises(ValueError, match="segment table"):
+        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, _lib.PROBFUSE, 60, 10, *tail)
+    with pytest.raises(ValueError, match="segment table"):
+        _lib.call("qf_fuse_probfuse", 1, 2, None, None, None, 0, None, None, _lib.PROBFUSE, 60,
+                  None, 25, 100, 10, *tail)
+    with pytest.raises(ValueError, match="without weights"):
+        _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, None, _lib.WRRF_MUL, 60, 10, *tail)
     with pytest.raises(ValueError, match="different weights"):
         _lib.call("qf_fuse", 1, 2, None, None, None, 0, None, 8, _lib.LEARNED | _lib.WRRF, 60, 10,
                   *tail)
