@@ -3,8 +3,11 @@ import sys, json
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
+import os
 import numpy as np, torch
 from qppfuse import engine, _lib
+if os.environ.get("QF_LIB"):  # A/B a development build of the same sources
+    _lib.LIB_PATH = Path(os.environ["QF_LIB"])
 
 def timeit(fn, n=10):
     fn(); torch.cuda.synchronize()
