@@ -35,6 +35,24 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METHODS = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+NAMES = ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade", "R5", "R6", "R7"]
+# BASELINE.json configs (SURVEY.md §8 shorthand).  The default run — and the
+# driver's — is C2; the others measure the remaining configs' hot paths.
+WORKLOADS = {
+    "c2": dict(queries=3452, total=False, methods=METHODS, qpp=True, qpp_index=5,
+               desc="C2: BEIR-NQ-shaped, 3452 queries/GPU x 5 retrievers x top-1000; "
+                    "min-max + QPP(13) + 6 fusions, full sorted lists"),
+    "c3": dict(queries=1_000_000, total=True, methods=["combsum", "rrf"], qpp=False,
+               qpp_index=5,
+               desc="C3: synthetic 1M queries in all x 5 retrievers x top-1000, query-sharded; "
+                    "min-max + CombSUM + RRF, full sorted lists"),
+    "c4": dict(queries=11157, total=True, methods=["wcombsum"], qpp=True, qpp_index=-1,
+               desc="C4: HotpotQA+SciFact+NQ-shaped, 11157 queries in all x 5 x top-1000; "
+                    "min-max + QPP(13) + W-CombSUM with the mean of the 13 columns"),
+    "c5": dict(queries=3452, total=False, methods=["learned"], qpp=True, qpp_index=5,
+               desc="C5: C2 + learned fusion with the reference's NQ MultiOutput-LightGBM "
+                    "(tests/golden/lgbm fixture): min-max + QPP(13) + GBDT weights + fusion"),
+}
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md), 6.3 TB/s measured copy
 SEED = 20251212
 
@@ -42,13 +60,15 @@ SEED = 20251212
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--queries", type=int, default=3452, help="queries per GPU")
+    ap.add_argument("--queries", type=int, default=None,
+                    help="queries per GPU (default: the workload's; C3/C4 split their total)")
     ap.add_argument("--retrievers", type=int, default=5)
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--qpp-top-k", type=int, default=100)
-    ap.add_argument("--qpp-index", type=int, default=5)
+    ap.add_argument("--qpp-index", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=40,
                     help="queries timed through the Python port of the reference (0 = skip)")
     ap.add_argument("--native-sample", type=int, default=400,
@@ -56,7 +76,12 @@ def parse():
     ap.add_argument("--check", type=int, default=8, help="queries checked bit-exact vs oracle")
     ap.add_argument("--ndcg-sample", type=int, default=256,
                     help="queries whose NDCG@10 is recomputed on the CPU reference path")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.wl = WORKLOADS[a.workload]
+    if a.qpp_index is None:
+        a.qpp_index = a.wl["qpp_index"]
+    a.methods = list(a.wl["methods"])
+    return a
 
 
 def setup_dist(args):
@@ -84,9 +109,18 @@ class Pipeline:
         from qppfuse import engine
         self.engine = engine
         self.args, self.world, self.rank, self.dev = args, world, rank, dev
-        Q, R, K = args.queries, args.retrievers, args.k
+        R, K = args.retrievers, args.k
+        wl = args.wl
+        if args.queries is not None:
+            Q, self.q_begin = args.queries, rank * args.queries
+        elif wl["total"]:  # strong scaling: the workload's total split across ranks
+            from qppfuse.dist import shard_range
+            b, e = shard_range(wl["queries"], world, rank)
+            Q, self.q_begin = e - b, b
+        else:
+            Q, self.q_begin = wl["queries"], rank * wl["queries"]
         self.Q, self.R, self.K = Q, R, K
-        self.q_begin = rank * Q
+        self.methods = args.methods
         self.off, self.docid, self.raw = engine.synth_runs(self.q_begin, Q, R, K, seed=SEED)
         nt, tf = text_inputs(self.q_begin, Q)
         self.nt = torch.from_numpy(nt).to(dev)
@@ -95,7 +129,19 @@ class Pipeline:
         self.micro = torch.empty(E, dtype=torch.int32, device=dev)
         self.qraw = torch.empty((Q * R, 13), dtype=torch.float64, device=dev)
         self.mm = torch.empty(2 * R * 13, dtype=torch.float64, device=dev)
-        self.out = engine.alloc_fuse_out(Q, E, engine.methods_mask(METHODS), dev)
+        self.out = engine.alloc_fuse_out(Q, E, engine.methods_mask(self.methods), dev)
+        self.w = None
+        if "learned" in self.methods:
+            from qppfuse import lgbm
+            model = lgbm.load_fusion_model(ROOT / "tests" / "golden" / "lgbm" /
+                                           "nq_fusion_multioutput.json.gz")
+            self.packed = lgbm.pack_model(model)
+            names = NAMES[:R]
+            # X columns: model.retrievers order, 13 QPP values each (src/fusion.py:421-427)
+            self.xperm = torch.tensor([names.index(r) for r in model.retrievers],
+                                      dtype=torch.int64, device=dev)
+            self.run_to_booster = [model.retrievers.index(n) if n in model.retrievers else -1
+                                   for n in names]
         self.ev = []
         torch.cuda.synchronize()
 
@@ -105,17 +151,25 @@ class Pipeline:
         s = torch.cuda.current_stream().cuda_stream
         _lib.call("qf_minmax_per_query", self.raw.data_ptr(), self.off.data_ptr(),
                   self.Q * self.R, None, self.micro.data_ptr(), s)
-        e.qpp_raw(self.raw, self.off, self.R, a.qpp_top_k, self.nt, self.tf, out=self.qraw)
-        e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
-        if self.world > 1:  # the path's only exchange: ~1 KB over RCCL/xGMI
-            from qppfuse.dist import allreduce_minmax
-            allreduce_minmax(self.mm)
-        w = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
-                            want_micro=False)["weights"]
+        w = None
+        if a.wl["qpp"]:
+            e.qpp_raw(self.raw, self.off, self.R, a.qpp_top_k, self.nt, self.tf, out=self.qraw)
+            e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
+            if self.world > 1:  # the path's only exchange: ~1 KB over RCCL/xGMI
+                from qppfuse.dist import allreduce_minmax
+                allreduce_minmax(self.mm)
+            learned = "learned" in self.methods
+            o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
+                                want_micro=learned, want_weights=not learned)
+            w = o["weights"]
+            if learned:  # the .qpp values as features, GBDT, normalised weights
+                X = (o["micro"].view(self.Q, self.R, 13).index_select(1, self.xperm)
+                     .reshape(self.Q, -1).to(torch.float64) / 1e6)
+                w = e.learned_weights(e.gbdt_predict(X, self.packed), self.run_to_booster)
         if timed:
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0.record()
-        e.fuse(self.off, self.docid, self.micro, self.R, METHODS, 60, weights=w,
+        e.fuse(self.off, self.docid, self.micro, self.R, self.methods, 60, weights=w,
                max_entries=self.R * self.K, out=self.out)
         if timed:
             t1.record()
@@ -129,8 +183,9 @@ class Pipeline:
         """Algorithmic HBM bytes of one qf_fuse launch."""
         uc = self.out.union_count.cpu().numpy()[:self.Q].astype(np.int64)
         N = self.Q * self.R * self.K
-        M = len(METHODS)
-        reads = N * (4 + 4) + self.Q * self.R * 8 + (self.Q * self.R + 1) * 8
+        M = len(self.methods)
+        weighted = any(m.startswith("w") or m == "learned" for m in self.methods)
+        reads = N * (4 + 4) + (self.Q * self.R * 8 if weighted else 0) + (self.Q * self.R + 1) * 8
         writes = int(uc.sum()) * (4 + M * (2 + 8)) + self.Q * 4
         return reads + writes, float(uc.mean())
 
@@ -157,7 +212,7 @@ def ndcg_device(p: Pipeline):
     qdev = (t(qo), t(qd.view(np.int32)), t(qr))
     o = p.out
     run = lambda: evaluate_device(p.off, p.R, o.union_count, o.union_docid, o.perm, o.fused,
-                                  o.fused.shape[1], len(METHODS), p.Q, qdev,
+                                  o.fused.shape[1], len(p.methods), p.Q, qdev,
                                   int(np.diff(qo).max()), ["nDCG@10"], text_scores=True)
     run()
     torch.cuda.synchronize()
@@ -176,7 +231,9 @@ def ndcg_delta(p: Pipeline, dev_vals, nq: int):
     sc = h["micro"].astype(np.float64) / 1e6
     qo, qd, qr = synth_qrels(p.q_begin, nq, p.K)
     worst_q, worst_mean = 0.0, 0.0
-    for m, name in enumerate(METHODS):
+    for m, name in enumerate(p.methods):
+        if name not in METHODS:
+            continue
         ud_all, uc, perm, fused = coracle.fuse(h["off"], h["docid"], sc, p.R, name, 60,
                                                weights=h["w"])
         roff = np.zeros(nq + 1, np.int64)
@@ -199,7 +256,8 @@ def host_sample(p: Pipeline, nq: int):
     off = p.off[: nq * R + 1].cpu().numpy()
     return dict(off=off, docid=p.docid[:n].cpu().numpy().view(np.uint32),
                 raw=p.raw[:n].cpu().numpy(), micro=p.micro[:n].cpu().numpy(),
-                w=p.w[: nq * R].cpu().numpy(), nt=p.nt[:nq].cpu().numpy(),
+                w=None if p.w is None else p.w[: nq * R].cpu().numpy(),
+                nt=p.nt[:nq].cpu().numpy(),
                 tf=p.tf[:nq].cpu().numpy(), qraw=p.qraw[: nq * R].cpu().numpy())
 
 
@@ -209,7 +267,9 @@ def check_parity(p: Pipeline, nq: int):
     sc = h["micro"].astype(np.float64) / 1e6
     uc = p.out.union_count[:nq].cpu().numpy()
     ok = True
-    for m, name in enumerate(METHODS):
+    for m, name in enumerate(p.methods):
+        if name not in METHODS:  # learned fusion: checked by tests/test_gpu_learned.py
+            continue
         _, o_uc, o_perm, o_fused = coracle.fuse(h["off"], h["docid"], sc, p.R, name, 60,
                                                 weights=h["w"])
         f = p.out.fused[m, : nq * p.R * p.K].cpu().numpy()
@@ -229,7 +289,7 @@ def cpu_baseline_port(p: Pipeline, nq: int):
     from oracle import ref_port
     h = host_sample(p, nq)
     R, K = p.R, p.K
-    names = ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade", "R5", "R6", "R7"][:R]
+    names = NAMES[:R]
     qids = [f"test{p.q_begin + q}" for q in range(nq)]
     frames, raw_lists = {}, {}
     for r, name in enumerate(names):
@@ -251,7 +311,7 @@ def cpu_baseline_port(p: Pipeline, nq: int):
         d = ref_port.java_qpp(int(h["nt"][qi]), float(h["tf"][qi][0]), float(h["tf"][qi][1]),
                               sorted(scores, reverse=True)[:100])
         qpp[qid][name] = [d[n] for n in ref_port.QPP_NAMES]
-    for m in METHODS:
+    for m in p.methods:
         ref_port.fuse(frames, m, qpp, p.args.qpp_index, 60)
     dt = time.perf_counter() - t0
     return nq / dt, dt
@@ -262,7 +322,7 @@ def cpu_baseline_native(p: Pipeline, nq: int):
     h = host_sample(p, nq)
     sc = h["micro"].astype(np.float64) / 1e6
     t0 = time.perf_counter()
-    for m in METHODS:
+    for m in p.methods:
         coracle.fuse(h["off"], h["docid"], sc, p.R, m, 60, weights=h["w"])
     coracle.qpp_raw(h["raw"], h["off"], np.repeat(h["nt"], p.R), np.repeat(h["tf"][:, 0], p.R),
                     np.repeat(h["tf"][:, 1], p.R))
@@ -277,7 +337,8 @@ def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     from FETCH_SIZE and WRITE_SIZE passes (separate runs) of this same bench command
     at its default workload; it only applies to that workload.
     """
-    default = (args.queries, args.retrievers, args.k) == (3452, 5, 1000)
+    default = args.workload == "c2" and (args.queries, args.retrievers, args.k) in \
+        ((None, 5, 1000), (3452, 5, 1000))
     files = sorted((ROOT / "profiles").glob("r*_pmc.json"))
     if not default or not files:
         return None, None
@@ -312,38 +373,47 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_q = args.queries * world * args.steps
+    if world > 1:
+        qt = torch.tensor([p.Q], dtype=torch.int64, device=dev)
+        dist.all_reduce(qt)
+        total_q = int(qt.item()) * args.steps
+    else:
+        total_q = p.Q * args.steps
     value = total_q / elapsed
     fuse_ms = p.fuse_kernel_ms()
     fbytes, mean_u = p.fuse_bytes()
     achieved = fbytes / (fuse_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args)
-    parity = check_parity(p, min(args.check, args.queries)) if args.check > 0 else None
+    parity = check_parity(p, min(args.check, p.Q)) if args.check > 0 else None
     ndcg_vals, eval_ms = ndcg_device(p)
     result = None
     if rank == 0:
         cpu = None
-        if world == 1 and args.cpu_sample > 0:
-            v, dt = cpu_baseline_port(p, min(args.cpu_sample, args.queries))
+        ported = all(m in METHODS for m in p.methods)
+        if world == 1 and args.cpu_sample > 0 and ported:
+            nq = min(args.cpu_sample, p.Q)
+            v, dt = cpu_baseline_port(p, nq)
             cpu = {"value": round(v, 4), "unit": "fused queries/s", "cores": 1, "kind": "port",
-                   "sample": f"{min(args.cpu_sample, args.queries)} queries x {args.retrievers} "
-                             f"x top-{args.k}: 13 QPP predictors + 6 fusions through "
+                   "sample": f"{nq} queries x {args.retrievers} x top-{args.k}: 13 QPP "
+                             f"predictors + {len(p.methods)} fusion(s) through "
                              f"oracle/ref_port.py (pandas groupby/iterrows, the reference's "
                              f"per-row algorithm), 1 thread, {dt:.1f} s"}
             if args.native_sample > 0:
                 cpu["native_c_oracle_value"] = round(
-                    cpu_baseline_native(p, min(args.native_sample, args.queries)), 2)
+                    cpu_baseline_native(p, min(args.native_sample, p.Q)), 2)
         result = {
-            "metric": "fused queries/sec (5 retrievers x top-1000), all 6 fusions + 13 QPP",
+            "metric": "fused queries/sec (5 retrievers x top-1000), all 6 fusions + 13 QPP"
+                      if args.workload == "c2" else
+                      f"fused queries/sec (5 retrievers x top-1000), {args.workload.upper()}",
             "value": round(value, 2), "unit": "fused queries/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "strong" if args.wl["total"] and args.queries is None else "weak",
+            "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device counter-based generator, DESIGN.md)",
-            "config": {"workload": "C2: BEIR-NQ-shaped, 3452 queries/GPU x 5 retrievers x "
-                                   "top-1000; min-max + QPP(13) + 6 fusions, full sorted lists",
-                       "queries_per_gpu": args.queries, "retrievers": args.retrievers,
-                       "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": METHODS,
+            "config": {"workload": args.wl["desc"],
+                       "queries_per_gpu": p.Q, "retrievers": args.retrievers,
+                       "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": p.methods,
                        "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1)},
             "roofline": {"bound": "hbm", "kernel": "qf_fuse", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -352,13 +422,13 @@ def main():
                          "algorithmic_bytes_per_launch": fbytes,
                          "kernel_ms": round(fuse_ms, 4)},
             "cpu_baseline": cpu,
-            "parity_vs_oracle": {"queries": min(args.check, args.queries), "bit_exact": parity},
+            "parity_vs_oracle": {"queries": min(args.check, p.Q), "bit_exact": parity},
             "ndcg10": {m: round(float(np.nanmean(ndcg_vals[i])), 6)
-                       for i, m in enumerate(METHODS)},
+                       for i, m in enumerate(p.methods)},
             "ndcg10_eval_ms": round(eval_ms, 4),
         }
-        if world == 1 and args.ndcg_sample > 0:
-            nq = min(args.ndcg_sample, args.queries)
+        if world == 1 and args.ndcg_sample > 0 and ported:
+            nq = min(args.ndcg_sample, p.Q)
             dq, dm = ndcg_delta(p, ndcg_vals, nq)
             result["ndcg10_delta_vs_ref"] = {
                 "queries": nq, "max_abs_per_query": dq, "max_abs_mean": dm,
