@@ -61,6 +61,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="put every rank on GPU 0 (use with --dist-backend gloo)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--queries", type=int, default=None,
@@ -88,10 +91,15 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_one_gpu:  # N-rank rehearsal on a 1-GPU box (gloo): all ranks on GPU 0
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     return world, rank, torch.device("cuda", local)
 
 
@@ -149,15 +157,22 @@ class Pipeline:
         from qppfuse import _lib
         e, a = self.engine, self.args
         s = torch.cuda.current_stream().cuda_stream
-        _lib.call("qf_minmax_per_query", self.raw.data_ptr(), self.off.data_ptr(),
-                  self.Q * self.R, None, self.micro.data_ptr(), s)
+        minmax = lambda: _lib.call("qf_minmax_per_query", self.raw.data_ptr(),
+                                   self.off.data_ptr(), self.Q * self.R, None,
+                                   self.micro.data_ptr(), s)
         w = None
-        if a.wl["qpp"]:
+        if not a.wl["qpp"]:
+            minmax()
+        else:
             e.qpp_raw(self.raw, self.off, self.R, a.qpp_top_k, self.nt, self.tf, out=self.qraw)
             e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
-            if self.world > 1:  # the path's only exchange: ~1 KB over RCCL/xGMI
-                from qppfuse.dist import allreduce_minmax
-                allreduce_minmax(self.mm)
+            work = None
+            if self.world > 1:  # the path's only exchange: ~1 KB over RCCL/xGMI,
+                from qppfuse.dist import allreduce_minmax  # hidden behind the min-max kernel
+                work = allreduce_minmax(self.mm, async_op=True)
+            minmax()
+            if work is not None:
+                work.wait()
             learned = "learned" in self.methods
             o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
                                 want_micro=learned, want_weights=not learned)

@@ -37,12 +37,15 @@ def shard_by_entries(list_off: np.ndarray, n_retrievers: int, world: int) -> np.
     return np.maximum.accumulate(b)
 
 
-def allreduce_minmax(mm, group=None):
-    """In-place element-wise MIN over ranks of the [min, -max] buffer (a torch tensor)."""
+def allreduce_minmax(mm, group=None, async_op=False):
+    """In-place element-wise MIN over ranks of the [min, -max] buffer (a torch tensor).
+    async_op=True returns the work handle (None on one rank): launch independent
+    kernels, then handle.wait() before reading mm — the exchange hides behind them."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
-    return mm
+        work = dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group, async_op=async_op)
+        return work if async_op else mm
+    return None if async_op else mm
 
 
 def allgather_qpp_raw(raw, present, group=None):
