@@ -621,8 +621,10 @@ void join_kernel(FuseParams p) {
       const uint32_t q2 = gpr[k];
       const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
       if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // ranx min-max normalised score
-        const double den = s_den[r];
-        a0 += den > 0.0 ? (s - s_min[r]) / den : 0.0;
+        const double den = s_den[r], mn = s_min[r];
+        // A .norm.res list is already [0, 1] (min 0.000000, max 1.000000), where
+        // (s - 0.0) / 1.0 == s bit for bit (-0.0 included): skip the division.
+        a0 += den > 0.0 ? ((den == 1.0 && mn == 0.0) ? s : (s - mn) / den) : 0.0;
       }
       if (methods & QF_RRF) a1 += 1.0 / (double)(rrf_k + pos + 1);  // ranx rrf: rank = position
       if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += s_w[r] * s;  // src/fusion.py:273
