@@ -39,6 +39,10 @@ NAMES = ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade", "R5", "R6", "R7"]
 # BASELINE.json configs (SURVEY.md §8 shorthand).  The default run — and the
 # driver's — is C2; the others measure the remaining configs' hot paths.
 WORKLOADS = {
+    "c1": dict(queries=3452, total=False, methods=["combsum", "rrf"], qpp=False, qpp_index=5,
+               retrievers=3, k=100,
+               desc="C1: BEIR-NQ-shaped, 3452 queries/GPU x 3 retrievers (BM25/BGE/SPLADE) x "
+                    "top-100; min-max + CombSUM + RRF, full sorted lists"),
     "c2": dict(queries=3452, total=False, methods=METHODS, qpp=True, qpp_index=5,
                desc="C2: BEIR-NQ-shaped, 3452 queries/GPU x 5 retrievers x top-1000; "
                     "min-max + QPP(13) + 6 fusions, full sorted lists"),
@@ -68,8 +72,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--queries", type=int, default=None,
                     help="queries per GPU (default: the workload's; C3/C4 split their total)")
-    ap.add_argument("--retrievers", type=int, default=5)
-    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--retrievers", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--qpp-top-k", type=int, default=100)
     ap.add_argument("--qpp-index", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=40,
@@ -84,6 +88,10 @@ def parse():
     if a.qpp_index is None:
         a.qpp_index = a.wl["qpp_index"]
     a.methods = list(a.wl["methods"])
+    if a.retrievers is None:
+        a.retrievers = a.wl.get("retrievers", 5)
+    if a.k is None:
+        a.k = a.wl.get("k", 1000)
     return a
 
 
@@ -352,8 +360,8 @@ def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     from FETCH_SIZE and WRITE_SIZE passes (separate runs) of this same bench command
     at its default workload; it only applies to that workload.
     """
-    default = args.workload == "c2" and (args.queries, args.retrievers, args.k) in \
-        ((None, 5, 1000), (3452, 5, 1000))
+    default = args.workload == "c2" and args.queries in (None, 3452) and \
+        (args.retrievers, args.k) == (5, 1000)
     files = sorted((ROOT / "profiles").glob("r*_pmc.json"))
     if not default or not files:
         return None, None
@@ -419,7 +427,8 @@ def main():
         result = {
             "metric": "fused queries/sec (5 retrievers x top-1000), all 6 fusions + 13 QPP"
                       if args.workload == "c2" else
-                      f"fused queries/sec (5 retrievers x top-1000), {args.workload.upper()}",
+                      f"fused queries/sec ({args.retrievers} retrievers x top-{args.k}), "
+                      f"{args.workload.upper()}",
             "value": round(value, 2), "unit": "fused queries/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
