@@ -16,6 +16,35 @@ __global__ __launch_bounds__(256) void minmax_per_query_kernel(
   const int64_t l = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= n_lists) return;
   const int64_t a = list_off[l], b = list_off[l + 1];
+  constexpr int kRegRows = 16;  // lists of <= 1024 entries: one HBM read, held in registers
+  if (b - a <= 64 * kRegRows) {
+    double v[kRegRows];
+    double mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kRegRows; ++j) {  // every load in flight before the first use
+      const int64_t i = a + j * 64 + lane;
+      v[j] = i < b ? score[i] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < kRegRows; ++j)
+      if (a + j * 64 + lane < b) {
+        mn = fmin(mn, v[j]);
+        mx = fmax(mx, v[j]);
+      }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    const double range = mx > mn ? mx - mn : 1.0;
+#pragma unroll
+    for (int j = 0; j < kRegRows; ++j) {
+      const int64_t i = a + j * 64 + lane;
+      if (i < b) {
+        const double x = (v[j] - mn) / range;
+        if (out_norm) out_norm[i] = x;
+        if (out_micro) out_micro[i] = (int32_t)round6(x);
+      }
+    }
+    return;
+  }
   double mn = INFINITY, mx = -INFINITY;
   for (int64_t i = a + lane; i < b; i += 64) {
     const double s = score[i];
