@@ -94,15 +94,15 @@ __device__ __forceinline__ void block_min_max(uint64_t kmn, uint64_t kmx,
 //
 // Items are 32-bit words, held in registers wave-major (item i = (wid*rows +
 // j)*64 + lane) and scattered through LDS between passes:
-//   bits 13..30  window key: the kWindow most significant bits of (wkey - wmin),
+//   bits 14..31  window key: the kWindow most significant bits of (wkey - wmin),
 //                a non-decreasing function of key = ~orderable(score)
 //                (ascending key == descending score), see sort_one
-//   bits  0..12  u, the document's first-seen index
+//   bits  0..13  u, the document's first-seen index
 // The full key of an item is re-derived from fused[u] (the unsorted scores in
 // HBM/L2), which only the rare fix-up and the output need.
 constexpr int kDigit = 9;                // bits per LSD pass
 constexpr int kBuckets = 1 << kDigit;    // counters per wave, 16 bits each
-constexpr int kUBits = 13;
+constexpr int kUBits = 14;
 constexpr uint32_t kUMask = (1u << kUBits) - 1u;
 template <int ITEMS, int WAVES>
 struct SortCtx {
@@ -876,11 +876,13 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
 using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
+using JoinXL = JoinCfg<1024, 10, 14>; // N <= 10240 (e.g. 10 runs x top-1000; 143 KB LDS)
 using SortS = SortCfg<256, 4, 4>;     // U <= 1024
 using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
+using SortXL = SortCfg<1024, 10, 2>;  // U <= 10240
 
-int fuse_max_entries() { return JoinL::kNMax; }
+int fuse_max_entries() { return JoinXL::kNMax; }
 
 template <class J>
 static void launch_join(const FuseParams& p, int kind, hipStream_t st) {
@@ -912,9 +914,11 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     launch_sort<SortS>(p, 0, st);
   } else {
     if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
-    else launch_join<JoinL>(p, kind, st);
+    else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
+    else launch_join<JoinXL>(p, kind, st);
     launch_sort<SortM>(p, 0, st);
     launch_sort_large<SortL>(p, SortM::kUMax + 1, st, 1);  // the queries SortM left
+    if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
   }
   return hipGetLastError();
 }

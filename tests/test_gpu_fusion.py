@@ -148,7 +148,7 @@ def test_edge_cases_empty_lists_ties_single(gpu):
             assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
-@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680])
+@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680, 7681, 10240])
 def test_kernel_capacity_boundaries(gpu, n_entries):
     """Queries exactly at / just past each kernel configuration's capacity."""
     from qppfuse import engine
@@ -208,7 +208,7 @@ def _sort_case(kind, n, rng):
     return s
 
 
-@pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000])
+@pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000, 7681, 10240])
 @pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform",
                                   "huge_and_inf"])
 def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
