@@ -22,6 +22,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <cmath>
 #include <cstdint>
@@ -38,6 +39,19 @@
 namespace {
 
 thread_local std::string g_err;
+
+// QFIO_TIMING=1: phase times of qfio_load_runs on stderr (diagnostics).
+struct PhaseTimer {
+  bool on = getenv("QFIO_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[qfio] %-18s %8.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -347,6 +361,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   if (n_threads > 0) omp_set_num_threads(n_threads);
   auto* rs = new qfio_runset();
   rs->n_files = n_files;
+  PhaseTimer tm;
   // ---- map every file; chunk at line boundaries; count rows per chunk ----------
   const int T = std::max(1, omp_get_max_threads());
   std::vector<const char*> cut((size_t)n_files * (T + 1));
@@ -379,6 +394,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
       c[t] = std::max(x, c[t - 1]);
     }
   }
+  tm.mark("map");
   const size_t NC = (size_t)n_files * T;
   std::vector<size_t> nrow(NC + 1, 0);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -392,8 +408,10 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->file_off.assign(n_files + 1, 0);
   for (int f = 0; f <= n_files; ++f) rs->file_off[f] = (int64_t)nrow[(size_t)f * T];
   // ---- parse every chunk straight into its rows ------------------------------
+  tm.mark("count rows");
   Cols cols;
   cols.resize(E);
+  tm.mark("alloc columns");
   std::vector<std::string> errs(NC);
   std::vector<size_t> mbad(NC, 0);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -401,6 +419,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
     const size_t f = k / T, t = k % T;
     parse_chunk(cut[f * (T + 1) + t], cut[f * (T + 1) + t + 1], cols, nrow[k], mbad[k], errs[k]);
   }
+  tm.mark("parse");
   for (size_t k = 0; k < NC; ++k)
     if (!errs[k].empty()) {
       const std::string e = std::string(paths[k / T]) + ": " + errs[k];
@@ -415,9 +434,12 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   std::vector<int32_t> row_micro = std::move(cols.micro);
   // ---- intern qids / docnos / iter / tag ---------------------------------------
   intern_runs(cols.q, rs->qids, rs->row_qid);
+  tm.mark("intern qid");
   intern(cols.d, rs->docnos, rs->row_docid);
+  tm.mark("intern docno");
   intern_runs(cols.it, rs->iters, rs->row_iter);
   intern_runs(cols.tag, rs->tags, rs->row_tag);
+  tm.mark("intern iter/tag");
   if (rs->docnos.size() >= 0xFFFFFFFFull) { delete rs; return fail(QFIO_EINVAL, "too many docnos"); }
   // ---- CSR by (query, file), stable in file order -------------------------------
   const int64_t Q = (int64_t)rs->qids.size(), R = n_files;
@@ -440,6 +462,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
       rs->rank[d] = rs->row_rank[i];
       if (rs->micro_ok) rs->micro[d] = row_micro[i];
     }
+  tm.mark("csr");
   *out = rs;
   return QFIO_OK;
 }
