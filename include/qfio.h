@@ -36,7 +36,9 @@ const char* qfio_last_error(void);
 int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
                    qfio_runset** out);
 /* sizes[8]: n_queries, n_docnos, n_entries, qid bytes, docno bytes,
- * micro_ok (every score is an exact 6-decimal number), n_iter | n_tag << 32,
+ * flags (bit 0 micro_ok: every score is an exact 6-decimal number; bit 1: every
+ * rank equals position + 1; bit 2: every list is score-descending with strictly
+ * rising ranks), n_iter | n_tag << 32,
  * iter bytes | tag bytes << 32 */
 void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes);
 /* CSR: list_off[Q*R+1], docid[E], score[E], micro[E] (nullable; only if

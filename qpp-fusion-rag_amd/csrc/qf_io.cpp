@@ -341,6 +341,7 @@ struct qfio_runset {
   std::vector<int32_t> micro;
   std::vector<int64_t> rank;
   bool micro_ok = true;
+  bool rank_is_position = true, canonical = true;
   // per-file rows in file order (for DataFrames): codes and values
   std::vector<int64_t> file_off;  // [n_files + 1]
   std::vector<uint32_t> row_qid, row_docid, row_iter, row_tag;
@@ -462,6 +463,19 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
       rs->rank[d] = rs->row_rank[i];
       if (rs->micro_ok) rs->micro[d] = row_micro[i];
     }
+  // list properties the device path keys on (qppfuse/runset.py _analyse): the
+  // rank column is position + 1; every list is score-descending with rising ranks
+  int not_pos = 0, not_canon = 0;
+#pragma omp parallel for schedule(static) reduction(+ : not_pos, not_canon)
+  for (int64_t l = 0; l < Q * R; ++l) {
+    const int64_t a = rs->list_off[l], b = rs->list_off[l + 1];
+    for (int64_t i = a; i < b; ++i) {
+      not_pos += rs->rank[i] != i - a + 1;
+      if (i > a) not_canon += !(rs->score[i] <= rs->score[i - 1] && rs->rank[i] > rs->rank[i - 1]);
+    }
+  }
+  rs->rank_is_position = not_pos == 0;
+  rs->canonical = not_canon == 0;
   tm.mark("csr");
   *out = rs;
   return QFIO_OK;
@@ -478,7 +492,7 @@ void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes /* [8] */) {
   sizes[2] = (int64_t)rs->docid.size();
   sizes[3] = qb;
   sizes[4] = db;
-  sizes[5] = rs->micro_ok ? 1 : 0;
+  sizes[5] = (rs->micro_ok ? 1 : 0) | (rs->rank_is_position ? 2 : 0) | (rs->canonical ? 4 : 0);
   sizes[6] = (int64_t)rs->iters.size() | ((int64_t)rs->tags.size() << 32);
   sizes[7] = ib | (tb << 32);
 }

@@ -99,7 +99,8 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
     try:
         sz = np.zeros(8, np.int64)
         L.qfio_runset_sizes(h, _p(sz))
-        Q, D, E, qb, db, micro_ok = (int(x) for x in sz[:6])
+        Q, D, E, qb, db, flags = (int(x) for x in sz[:6])
+        micro_ok = flags & 1
         n_iter, n_tag = int(sz[6]) & 0xFFFFFFFF, int(sz[6]) >> 32
         ib, tb = int(sz[7]) & 0xFFFFFFFF, int(sz[7]) >> 32
         R = len(paths)
@@ -127,19 +128,22 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
     iters, tags = _strings(io, ic), _strings(to, tc)
     rs = RunSet(qids=list(qids), rankers=list(names), docnos=docnos, list_off=list_off,
                 docid=docid, score=score, rank=rank, micro=micro)
-    lid = np.repeat(np.arange(Q * R, dtype=np.int64), np.diff(list_off))
-    same = lid[1:] == lid[:-1]
-    pos = np.arange(E, dtype=np.int64) - list_off[lid] if E else np.zeros(0, np.int64)
-    rs.rank_is_position = bool(np.array_equal(rank, pos + 1))
-    rs.canonical = bool(np.all(score[1:][same] <= score[:-1][same]) and
-                        np.all(rank[1:][same] > rank[:-1][same])) if E > 1 else True
+    rs.rank_is_position = bool(flags & 2)
+    rs.canonical = bool(flags & 4)
     rs._strtab = {"qid": (qo, qc.tobytes()), "docno": (do, dc.tobytes())}
+
+    def column(strings, codes):
+        # a column of one value (the usual iter "Q0" / a file's tag) is a broadcast
+        if len(codes) and codes[0] == codes[-1] and (codes == codes[0]).all():
+            return np.full(len(codes), strings[codes[0]], dtype=object)
+        return strings[codes]
+
     frames = {}
     for r, name in enumerate(names):
         a, b = int(fo[r]), int(fo[r + 1])
         frames[name] = pd.DataFrame({
-            "qid": qids[rq[a:b]], "iter": iters[ri[a:b]], "docno": docnos[rd[a:b]],
-            "rank": rr[a:b], "score": rsc[a:b], "runid": tags[rt[a:b]]}, copy=False)
+            "qid": qids[rq[a:b]], "iter": column(iters, ri[a:b]), "docno": docnos[rd[a:b]],
+            "rank": rr[a:b], "score": rsc[a:b], "runid": column(tags, rt[a:b])}, copy=False)
     return rs, frames
 
 

@@ -154,3 +154,24 @@ def test_load_runs_returns_frames_and_caches_the_pack(tmp_path):
                             if f.endswith(".norm.res")]
     rs = fusion._pack(frames)
     assert rs.n_entries == sum(len(df) for df in frames.values())
+
+
+@pytest.mark.parametrize("case", ["shifted_ranks", "unsorted_scores", "canonical"])
+def test_list_flags_match_pack(tmp_path, case):
+    """rank_is_position / canonical computed by the native loader == pack_frames'."""
+    lines = []
+    for q in range(4):
+        for i in range(6):
+            rank = i + (2 if case == "shifted_ranks" else 1)
+            score = 1.0 - i / 10
+            if case == "unsorted_scores" and q == 2 and i == 3:
+                score = 0.95
+            lines.append(f"{q} Q0 d{q}_{i} {rank} {score:.6f} t\n")
+    p = tmp_path / "A.norm.res"
+    p.write_text("".join(lines))
+    rs, _ = fastio.parse_runs([str(p)], ["A"])
+    ref = pack_frames(_pandas_frames([str(p)], ["A"]))
+    assert (rs.rank_is_position, rs.canonical) == (ref.rank_is_position, ref.canonical)
+    assert (rs.rank_is_position, rs.canonical) == {
+        "shifted_ranks": (False, True), "unsorted_scores": (True, False),
+        "canonical": (True, True)}[case]
