@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--gather-topk", type=int, default=0,
+                    help="per step, gather every rank's fused top-k to rank 0 (0 = fused "
+                         "lists stay on their rank, as each rank writes its own qid range)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="put every rank on GPU 0 (use with --dist-backend gloo)")
     ap.add_argument("--steps", type=int, default=20)
@@ -194,6 +197,10 @@ class Pipeline:
             t0.record()
         e.fuse(self.off, self.docid, self.micro, self.R, self.methods, 60, weights=w,
                max_entries=self.R * self.K, out=self.out)
+        if a.gather_topk > 0:  # the final fused top-k of every shard onto rank 0 (RCCL)
+            from qppfuse.dist import gather_fused_topk
+            d, sc = e.fused_topk(self.out, self.off, self.R, a.gather_topk)
+            self.gathered = gather_fused_topk(d, sc, dst=0)
         if timed:
             t1.record()
             self.ev.append((t0, t1))
@@ -438,7 +445,8 @@ def main():
             "config": {"workload": args.wl["desc"],
                        "queries_per_gpu": p.Q, "retrievers": args.retrievers,
                        "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": p.methods,
-                       "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1)},
+                       "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1),
+                       "gather_topk_to_rank0": args.gather_topk},
             "roofline": {"bound": "hbm", "kernel": "qf_fuse", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -186,6 +186,18 @@ int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* lis
                      void* stream);
 
 /*
+ * Fused top-k of every (query, method slot) from qf_fuse's outputs, packed for
+ * the multi-GPU gather of the final fused lists (qppfuse.dist.gather_fused_topk):
+ * out_docid / out_score[(q * n_methods + m) * k + i] = rank i (< min(k, U_q)) of
+ * method slot m — docid union_docid[base + perm[...]], its fused score; the rest
+ * of each row is docid 0xFFFFFFFF / score NaN.  base = list_off[q * R].
+ */
+int qf_fused_topk(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                  const int32_t* union_count, const uint32_t* union_docid, const uint16_t* perm,
+                  const double* fused, int64_t out_stride, int32_t n_methods, int32_t k,
+                  uint32_t* out_docid, double* out_score, void* stream);
+
+/*
  * LightGBM inference for learned fusion (src/fusion.py:415-429 ->
  * MultiOutputLGBM / PerRetrieverLGBM .predict, src/models/lightgbm_models.py):
  * out[row*n_boosters + b] = raw prediction of booster b on X[row*n_features ..]

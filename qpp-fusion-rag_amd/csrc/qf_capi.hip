@@ -152,6 +152,21 @@ int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* lis
                      union_count, perm, fused, out_stride, stream, "qf_fuse_probfuse");
 }
 
+int qf_fused_topk(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                  const int32_t* union_count, const uint32_t* union_docid, const uint16_t* perm,
+                  const double* fused, int64_t out_stride, int32_t n_methods, int32_t k,
+                  uint32_t* out_docid, double* out_score, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || n_methods <= 0 || k < 0 || out_stride < 0)
+    return fail(QF_EINVAL, "qf_fused_topk: bad sizes");
+  if (n_queries > 0 && k > 0 &&
+      (!list_off || !union_count || !union_docid || !perm || !fused || !out_docid || !out_score))
+    return fail(QF_EINVAL, "qf_fused_topk: null buffer");
+  return check(qf::topk_launch(n_queries, n_retrievers, list_off, union_count, union_docid, perm,
+                               fused, out_stride, n_methods, k, out_docid, out_score,
+                               (hipStream_t)stream),
+               "qf_fused_topk");
+}
+
 int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,
             const int32_t* q_count, const uint32_t* docid, const uint16_t* perm,
             const double* score, int64_t out_stride, int32_t n_runs, int32_t text_scores,

@@ -923,6 +923,53 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
   return hipGetLastError();
 }
 
+// ---- fused top-k compaction (the multi-GPU gather's payload) -------------------
+// out[(q*M + m)*k + i] = docid / score of rank i of method slot m of query q, for
+// i < min(k, U_q); the rest of the row is padded (docid 0xFFFFFFFF, score NaN).
+// One wave per (query, method) row, coalesced in i.
+__global__ __launch_bounds__(256) void topk_kernel(int64_t n_queries, int32_t R,
+                                                   const int64_t* __restrict__ list_off,
+                                                   const int32_t* __restrict__ union_count,
+                                                   const uint32_t* __restrict__ union_docid,
+                                                   const uint16_t* __restrict__ perm,
+                                                   const double* __restrict__ fused,
+                                                   int64_t out_stride, int32_t M, int32_t k,
+                                                   uint32_t* __restrict__ out_docid,
+                                                   double* __restrict__ out_score) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // q * M + m
+  if (row >= n_queries * M) return;
+  const int64_t q = row / M;
+  const int m = (int)(row % M);
+  const int64_t base = list_off[q * R];
+  const int uc = union_count[q];
+  const int n = uc < 0 ? 0 : (uc < k ? uc : k);
+  const uint16_t* pm = perm + (int64_t)m * out_stride + base;
+  const double* fz = fused + (int64_t)m * out_stride + base;
+  for (int i = lane; i < k; i += 64) {
+    uint32_t d = 0xFFFFFFFFu;
+    double sc = __longlong_as_double(0x7FF8000000000000ll);
+    if (i < n) {
+      d = union_docid[base + pm[i]];
+      sc = fz[i];
+    }
+    out_docid[row * k + i] = d;
+    out_score[row * k + i] = sc;
+  }
+}
+
+hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
+                       const int32_t* union_count, const uint32_t* union_docid,
+                       const uint16_t* perm, const double* fused, int64_t out_stride, int32_t M,
+                       int32_t k, uint32_t* out_docid, double* out_score, hipStream_t st) {
+  const int64_t rows = n_queries * M;
+  if (rows == 0 || k == 0) return hipSuccess;
+  hipLaunchKernelGGL(topk_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, n_queries,
+                     R, list_off, union_count, union_docid, perm, fused, out_stride, M, k,
+                     out_docid, out_score);
+  return hipGetLastError();
+}
+
 #ifdef QF_STAMPS
 extern "C" int qf_debug_stamps(unsigned long long* host, int n, int clear) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) != hipSuccess)

@@ -82,6 +82,10 @@ hipError_t learned_weights_launch(const LearnedWeightParams& p, hipStream_t st);
 int fuse_max_entries();
 hipError_t eval_launch(const EvalParams& p, hipStream_t st);
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);
+hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
+                       const int32_t* union_count, const uint32_t* union_docid,
+                       const uint16_t* perm, const double* fused, int64_t out_stride, int32_t M,
+                       int32_t k, uint32_t* out_docid, double* out_score, hipStream_t st);
 hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t Q, int32_t R,
                           int32_t top_k, const int32_t* nt, const double* tf, double* out,
                           hipStream_t st);

@@ -71,3 +71,32 @@ def allgather_qpp_raw(raw, present, group=None):
     dist.all_gather(pres, ppad, group=group)
     return (torch.cat([t[:k] for t, k in zip(rows, sizes)]),
             torch.cat([t[:k] for t, k in zip(pres, sizes)]).to(torch.bool))
+
+
+def gather_fused_topk(docid, score, dst: int = 0, group=None):
+    """The final fused top-k of every rank's query shard, concatenated in rank
+    order on rank `dst` (None elsewhere): docid [Q_r, M, k] and score tensors
+    from engine.fused_topk.  Shards may differ in size by the shard_range
+    remainder: rows are padded to the largest shard for the collective
+    (dist.gather over RCCL/xGMI; gloo in the CPU tests) and trimmed after."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return docid, score
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    n = torch.tensor([docid.shape[0]], dtype=torch.int64, device=docid.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    pad = lambda t, v: torch.cat([t, t.new_full((m - t.shape[0],) + tuple(t.shape[1:]), v)]) \
+        if t.shape[0] < m else t
+    d, s = pad(docid, -1), pad(score, float("nan"))
+    dl = [torch.empty_like(d) for _ in range(world)] if rank == dst else None
+    sl = [torch.empty_like(s) for _ in range(world)] if rank == dst else None
+    dist.gather(d, dl, dst=dst, group=group)
+    dist.gather(s, sl, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return (torch.cat([t[:k] for t, k in zip(dl, sizes)]),
+            torch.cat([t[:k] for t, k in zip(sl, sizes)]))

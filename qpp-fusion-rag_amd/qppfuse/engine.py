@@ -132,6 +132,21 @@ def qpp_raw(score: torch.Tensor, list_off: torch.Tensor, n_retrievers: int, top_
     return out
 
 
+def fused_topk(out: FuseOut, list_off: torch.Tensor, n_retrievers: int, k: int):
+    """qf_fused_topk: (docid int32 view of uint32 [Q, M, k], score float64 [Q, M, k]);
+    rows shorter than k padded with docid 0xFFFFFFFF (-1) and NaN."""
+    dev = require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    M = out.fused.shape[0]
+    docid = torch.empty((Q, M, k), dtype=torch.int32, device=dev)
+    score = torch.empty((Q, M, k), dtype=torch.float64, device=dev)
+    _lib.call("qf_fused_topk", Q, R, _ptr(list_off), _ptr(out.union_count), _ptr(out.union_docid),
+              _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], M, int(k), _ptr(docid),
+              _ptr(score), _stream())
+    return docid, score
+
+
 def qpp_colminmax(raw: torch.Tensor, list_off: torch.Tensor, n_retrievers: int,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[2*R*13]: column minima then negated maxima (MIN all-reduce combines shards)."""

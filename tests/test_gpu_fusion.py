@@ -231,3 +231,26 @@ def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
     np.testing.assert_array_equal(perm, want)
     # defaultdict(float) accumulation: 0.0 + 1.0 * s, so -0.0 comes out as +0.0
     assert fused.tobytes() == (0.0 + s[want]).tobytes()
+
+
+@pytest.mark.parametrize("k", [1, 10, 1000, 3000])
+def test_fused_topk_compaction(gpu, k):
+    """qf_fused_topk packs rank i < min(k, U_q) of every (query, method) row."""
+    from qppfuse import engine
+    Q, R, K = 6, 3, 700
+    off, docid, raw = engine.synth_runs(0, Q, R, K, seed=3)
+    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+    ms = ["combsum", "rrf"]
+    out = engine.fuse(off, docid, micro, R, ms, max_entries=R * K)
+    d, s = engine.fused_topk(out, off, R, k)
+    d, s = d.cpu().numpy().view(np.uint32), s.cpu().numpy()
+    off_h, uc = off.cpu().numpy(), out.union_count.cpu().numpy()
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fz = out.fused.cpu().numpy()
+    for q in range(Q):
+        b, n = off_h[q * R], min(k, uc[q])
+        for m in range(len(ms)):
+            np.testing.assert_array_equal(d[q, m, :n], ud[b + perm[m, b:b + n].astype(np.int64)])
+            assert s[q, m, :n].tobytes() == fz[m, b:b + n].tobytes()
+            assert (d[q, m, n:] == 0xFFFFFFFF).all() and np.isnan(s[q, m, n:]).all()
