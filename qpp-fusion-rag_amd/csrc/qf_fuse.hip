@@ -121,7 +121,8 @@ __device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, ui
 }
 
 // One stable counting-scatter pass on a kDigit-bit digit of the items.  Within a
-// wave a row's items are ranked by a ballot match of their digits; the row's
+// wave a row's items are ranked by a ballot match of their digits (per bit:
+// v_bfe, v_cmp into a ballot, one v_bitop3 per 32-lane half); the row's
 // leader lane claims a run of slots with one LDS atomicAdd (LDS ops of a wave
 // execute in program order, so rows stay ordered); the (wave, digit) offsets
 // are one block-wide exclusive scan in [digit][wave] order.  Leaves the
@@ -159,8 +160,9 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
         uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)d, (uint32_t)b, 1u);
         asm("" : "+v"(m));  // keep the ballot on m (one v_cmp), not a re-derived bit test
         const uint64_t bb = ballot(m != 0u);
-        mlo |= (uint32_t)bb ^ m;
-        mhi |= (uint32_t)(bb >> 32) ^ m;
+        // mismatch |= ballot ^ m, one v_bitop3 per half (0xF6: a | (b ^ c))
+        mlo = __builtin_amdgcn_bitop3_b32(mlo, (uint32_t)bb, m, 0xF6);
+        mhi = __builtin_amdgcn_bitop3_b32(mhi, (uint32_t)(bb >> 32), m, 0xF6);
       }
       const uint32_t plo = ~mlo, phi = ~mhi;
       const uint32_t before = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
@@ -715,14 +717,17 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
   const int rows = (U + 64 * WAVES - 1) / (64 * WAVES);
   // ---- the join kernel's unsorted scores -> LDS, their key range -----------------
   uint64_t fk[ITEMS];
+  double fv[ITEMS];  // the scores themselves (the linearised window key needs them)
   uint64_t kmn = ~0ull, kmx = 0ull;
   uint32_t dmn = ~0u, dmx = 0u;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rows + j) * 64 + lane;
     fk[j] = 0;
+    fv[j] = 0.0;
     if (j < rows && i < U) {
-      fk[j] = ~f64_asc_key(io[i]);  // ascending sort on ~key == descending score
+      fv[j] = io[i];
+      fk[j] = ~f64_asc_key(fv[j]);  // ascending sort on ~key == descending score
       kmn = min(kmn, fk[j]);
       kmx = max(kmx, fk[j]);
       if (by_docid) {
@@ -800,7 +805,9 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const int i = (wid * rows + j) * 64 + lane;
-      item[j] = ((uint32_t)((wkey(fk[j]) - wmin) >> lo) << kUBits) | (uint32_t)i;
+      // wkey(fk[j]) straight from the score (-0.0 and +0.0 give the same (v - smin) + delta)
+      const uint64_t wk = lin ? ~f64_asc_key((fv[j] - smin) + delta) : fk[j];
+      item[j] = ((uint32_t)((wk - wmin) >> lo) << kUBits) | (uint32_t)i;
     }
   }
   QF_STAMP(0);

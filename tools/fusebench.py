@@ -1,0 +1,18 @@
+"""Only the C2 six-method qf_fuse launch, repeated (development: PMC passes)."""
+import sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
+import torch
+from qppfuse import engine
+Q, R, K = 3452, 5, 1000
+dev = torch.device("cuda", 0)
+off, docid, raw = engine.synth_runs(0, Q, R, K)
+_, micro = engine.minmax_per_query(raw, off, want_norm=False)
+w = torch.rand(Q * R, dtype=torch.float64, device=dev)
+M = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+out = engine.alloc_fuse_out(Q, Q * R * K, engine.methods_mask(M), dev)
+for _ in range(5):
+    engine.fuse(off, docid, micro, R, M, weights=w, max_entries=R * K, out=out)
+torch.cuda.synchronize()
+print("ok")
