@@ -484,6 +484,7 @@ void join_kernel(FuseParams p) {
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
   int status = 0;
   uint32_t rj[ITEMS];
+  int r = 0;  // entry e's list; e grows with j, so the search resumes where it stopped
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
@@ -492,7 +493,6 @@ void join_kernel(FuseParams p) {
     if (e < N) {
       const uint32_t d = dk[j];
       if (d == kEmpty) status = QF_QSTATUS_BADDOC;
-      int r = 0;
       while (base + e >= s_off[r + 1]) ++r;
       rj[j] = (uint32_t)r;
       uint32_t h = (d * 0x9E3779B1u) >> (32 - C::kTB);
