@@ -360,6 +360,23 @@ def cpu_baseline_native(p: Pipeline, nq: int):
     return nq / dt
 
 
+VALU_PEAK_PER_SIMD_NS = 0.5208  # tools/valu_peak.hip on MI355X (profiles/r01_valu.json)
+N_SIMDS = 1024
+
+
+def pmc_valu(args, kernel_substr="qf_fuse (sum of its kernels)"):
+    """VALU instructions per qf_fuse launch (SQ_INSTS_VALU) from the committed summary."""
+    default = args.workload == "c2" and args.queries in (None, 3452) and \
+        (args.retrievers, args.k) == (5, 1000)
+    files = sorted((ROOT / "profiles").glob("r*_pmc.json"))
+    if not default or not files:
+        return None
+    for name, d in json.loads(files[-1].read_text()).items():
+        if kernel_substr in name and d.get("insts_valu"):
+            return d["insts_valu"]
+    return None
+
+
 def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     """HBM bytes per qf_fuse launch from the newest committed rocprofv3 PMC summary.
 
@@ -414,6 +431,7 @@ def main():
     fbytes, mean_u = p.fuse_bytes()
     achieved = fbytes / (fuse_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args)
+    valu = pmc_valu(args)
     parity = check_parity(p, min(args.check, p.Q)) if args.check > 0 else None
     ndcg_vals, eval_ms = ndcg_device(p)
     result = None
@@ -452,7 +470,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": fbytes,
-                         "kernel_ms": round(fuse_ms, 4)},
+                         "kernel_ms": round(fuse_ms, 4),
+                         # the roof it actually meets: VALU issue
+                         "valu_issue_frac": None if valu is None else round(
+                             valu / N_SIMDS / (fuse_ms * 1e6) / VALU_PEAK_PER_SIMD_NS, 4),
+                         "valu_insts_per_launch": valu},
             "cpu_baseline": cpu,
             "parity_vs_oracle": {"queries": min(args.check, p.Q), "bit_exact": parity},
             "ndcg10": {m: round(float(np.nanmean(ndcg_vals[i])), 6)
