@@ -260,47 +260,58 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
     if (sh < (fallback ? hb_full : nb)) continue;
     if (fallback || exact) return;
     // -- A: find the runs to fix (read-only) ----------------------------------------
+    // First every row's predecessor window and, where the windows tie, both scores
+    // are loaded (all rows' loads in flight at once), then compared: one memory
+    // latency per wave, not one per row.
     {
       int rp = sx.rows;
       asm volatile("" : "+s"(rp));
       bool any = false;
+      double vk[ITEMS], vp[ITEMS];
+      uint32_t tie = 0u;
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const int i = (sx.wid * rp + j) * 64 + sx.lane;
         const uint32_t wk = item[j] >> kUBits;
         uint32_t wp = wave_up1(wk);
+        vk[j] = vp[j] = 0.0;
         if (j < rp && i < sx.U && i > 0) {
-          uint32_t ip = 0;
-          if (sx.lane == 0) {
-            ip = sx.sitem[i - 1];
-            wp = ip >> kUBits;
+          const uint32_t ip = sx.sitem[i - 1];
+          if (sx.lane == 0) wp = ip >> kUBits;
+          if (wp == wk) {  // same window as the predecessor: fetch both scores
+            tie |= 1u << j;
+            vk[j] = sx.sval[item[j] & kUMask];
+            vp[j] = sx.sval[ip & kUMask];
           }
-          if (wp == wk) {  // same window as the predecessor: compare full keys
-            if (sx.lane != 0) ip = sx.sitem[i - 1];
-            const uint64_t k = full_key(sx, item[j]), kp = full_key(sx, ip);
-            if (kp > k) {  // bad: walk back to the run start
-              any = true;
-              int st = i - 1;
-              uint64_t kc = kp;
-              bool first = true;
-              while (st > 0) {
-                const uint32_t iq = sx.sitem[st - 1];
-                if ((iq >> kUBits) != wk) break;
-                const uint64_t kq = full_key(sx, iq);
-                if (kq > kc) { first = false; break; }  // an earlier bad item owns the run
-                kc = kq;
-                --st;
-                if (i - st > kRunMax) break;
-              }
-              if (first) {
-                if (i - st > kRunMax) {
-                  atomicOr(&sx.flag[0], 1);
-                } else {
-                  const int slot = atomicAdd(&sx.flag[1], 1);
-                  if (slot < kListCap) sx.hist[slot] = (uint32_t)st;
-                  else atomicOr(&sx.flag[0], 1);
-                }
-              }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        if (!((tie >> j) & 1u)) continue;
+        const int i = (sx.wid * rp + j) * 64 + sx.lane;
+        const uint32_t wk = item[j] >> kUBits;
+        const uint64_t k = ~f64_asc_key(vk[j]), kp = ~f64_asc_key(vp[j]);
+        if (kp > k) {  // bad: walk back to the run start
+          any = true;
+          int st = i - 1;
+          uint64_t kc = kp;
+          bool first = true;
+          while (st > 0) {
+            const uint32_t iq = sx.sitem[st - 1];
+            if ((iq >> kUBits) != wk) break;
+            const uint64_t kq = full_key(sx, iq);
+            if (kq > kc) { first = false; break; }  // an earlier bad item owns the run
+            kc = kq;
+            --st;
+            if (i - st > kRunMax) break;
+          }
+          if (first) {
+            if (i - st > kRunMax) {
+              atomicOr(&sx.flag[0], 1);
+            } else {
+              const int slot = atomicAdd(&sx.flag[1], 1);
+              if (slot < kListCap) sx.hist[slot] = (uint32_t)st;
+              else atomicOr(&sx.flag[0], 1);
             }
           }
         }
