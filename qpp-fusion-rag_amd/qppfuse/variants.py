@@ -6,8 +6,11 @@ with k the rank's segment (build_probfuse_run, ProbFuse.py:136-187).
 QPPrrf_argmax.py — (weighted) RRF with weight * (1 / (k + rank)) per row
 (build_rrf_run, QPPrrf_argmax.py:53-76) and argmax-QPP ranker selection
 (build_adaptive_run, QPPrrf_argmax.py:33-51).
+10_oracle_baseline.py — the oracle upper bound: per query the ranker with the
+best per-query metric (compute_oracle_run, :152-201), its evaluation and the
+selection statistics (:204-254).
 
-The fusions run on the device through the same join + sort kernels as the main
+The fusions and the per-query metrics run on the device through the same join + sort kernels as the main
 path (qf_fuse_probfuse with QF_PROBFUSE, qf_fuse with QF_WRRF_MUL): the per-row
 contribution differs, the first-seen accumulation order (runs in dict order,
 rows in file order) and the stable score-descending sort are the reference's.
@@ -31,7 +34,8 @@ from .runset import pack_frames
 
 __all__ = ["pos_to_segment", "load_runs", "train_probfuse", "build_probfuse_run",
            "write_runfile", "load_qpp_estimates", "load_argmax_runs", "build_rrf_run",
-           "build_adaptive_run"]
+           "build_adaptive_run", "load_all_runs", "parse_metric", "compute_per_query_scores",
+           "compute_oracle_run", "evaluate_run", "analyze_oracle_selections"]
 
 
 # ------------------------------------------------------------- probFuse ------
@@ -250,3 +254,139 @@ def build_adaptive_run(qpp_data, runs, qpp_method_index=0) -> pd.DataFrame:
         out["rank"] = out.groupby("qid").cumcount() + 1
         return out
     return pd.DataFrame(columns=["qid", "iter", "docno", "rank", "score", "runid"])
+
+
+# ------------------------------------------------- 10_oracle_baseline --------
+
+def load_all_runs(runs_dir, use_normalized: bool = False):
+    """{ranker: {qid: [(docid, score)]}} with every list sorted by score descending
+    (stable), as 10_oracle_baseline.py:56-88 loads *.res or *.norm.res."""
+    from pathlib import Path
+    from .data_utils import load_run_file
+    runs_dir = Path(runs_dir)
+    suffix = ".norm.res" if use_normalized else ".res"
+    files = sorted(f for f in runs_dir.glob(f"*{suffix}")
+                   if use_normalized or ".norm." not in f.name)
+    runs = {}
+    for f in files:
+        name = f.name.replace(".norm.res", "") if use_normalized else f.stem
+        runs[name] = {qid: [(d, s) for d, s, _ in sorted(docs, key=lambda t: -t[1])]
+                      for qid, docs in load_run_file(f).items()}
+    return runs
+
+
+def parse_metric(metric_str: str) -> str:
+    """Selection metric name (10_oracle_baseline.py:91-115): ndcg[@k] (k=10),
+    map/ap, [m]rr[@k] (k=10), recall[@k] / r@k (k=10); the ir_measures object's
+    string form ("nDCG@10", "AP", "RR@10", "R@10") is what qppfuse.evaluation takes."""
+    m = metric_str.lower().strip()
+    cut = (lambda: int(m.split("@")[1])) if "@" in m else (lambda: 10)
+    if "ndcg" in m:
+        return f"nDCG@{cut()}"
+    if m in ("map", "ap"):
+        return "AP"
+    if "rr" in m or "mrr" in m:
+        return f"RR@{cut()}"
+    if "recall" in m or m.startswith("r@"):
+        return f"R@{cut()}"
+    raise ValueError(f"Unknown metric: {metric_str}")
+
+
+def _pack_lists(lists):
+    """[{docno: score}] -> docnos (sorted), off, docid, score; each list score-descending."""
+    all_docs = np.asarray(sorted({d for dd in lists for d in dd}), dtype=object)
+    off = np.zeros(len(lists) + 1, dtype=np.int64)
+    ids, scs = [], []
+    for i, dd in enumerate(lists):
+        names = np.asarray(list(dd.keys()), dtype=object)
+        sc = np.fromiter(dd.values(), dtype=np.float64, count=len(dd))
+        o = np.argsort(-sc, kind="stable")
+        ids.append(np.searchsorted(all_docs, names).astype(np.uint32)[o])
+        scs.append(sc[o])
+        off[i + 1] = off[i] + len(dd)
+    cat = lambda parts, dt: np.concatenate(parts) if parts else np.zeros(0, dt)
+    return all_docs, off, cat(ids, np.uint32), cat(scs, np.float64)
+
+
+def compute_per_query_scores(runs, qrels, metric):
+    """{ranker: {qid: value}} (10_oracle_baseline.py:118-149): every (ranker, qid)
+    list of every ranker goes to ONE qf_eval launch; a query without qrels (or
+    without documents) gets no value, as ir_measures.iter_calc yields none."""
+    import torch
+    from .evaluation import evaluate_device, pack_qrels
+    name = metric if isinstance(metric, str) else str(metric)
+    keys, lists = [], []
+    for ranker, run in runs.items():
+        for qid, docs in run.items():
+            keys.append((ranker, str(qid)))
+            lists.append({str(d): float(s) for d, s in docs})  # the last repeat wins
+    out = {r: {} for r in runs}
+    if not lists:
+        return out
+    dev = engine.require_device()
+    docnos, off, docid, score = _pack_lists(lists)
+    qs = pack_qrels({str(q): r for q, r in qrels.items()}, [q for _, q in keys], docnos)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    v = evaluate_device(t(off), 1, None, t(docid.view(np.int32)), None, t(score), 0, 1,
+                        len(lists), qs.to_device(dev), qs.max_per_query, [name],
+                        text_scores=False)[0, :, 0].cpu().numpy()
+    for (ranker, qid), x in zip(keys, v):
+        if not np.isnan(x):
+            out[ranker][qid] = float(x)
+    return out
+
+
+def _select_best(runs, qrels, per_query_scores):
+    """The selection loop of compute_oracle_run (10_oracle_baseline.py:171-199):
+    sorted qids judged in qrels, rankers in dict order, strictly greater wins,
+    best_score starts at -1."""
+    all_qids = set(qrels.keys())
+    for run in runs.values():
+        all_qids.update(run.keys())
+    all_qids &= set(qrels.keys())
+    oracle_run, selections = {}, {}
+    for qid in sorted(all_qids):
+        best, best_ranker = -1, None
+        for ranker in runs:
+            if qid in per_query_scores[ranker]:
+                sc = per_query_scores[ranker][qid]
+                if sc > best:
+                    best, best_ranker = sc, ranker
+        if best_ranker and qid in runs[best_ranker]:
+            oracle_run[qid] = runs[best_ranker][qid]
+            selections[qid] = best_ranker
+    return oracle_run, selections
+
+
+def compute_oracle_run(runs, qrels, metric):
+    """(oracle_run {qid: [(docid, score)]}, selections {qid: ranker})."""
+    return _select_best(runs, qrels, compute_per_query_scores(runs, qrels, metric))
+
+
+def evaluate_run(run, qrels, metrics) -> Dict[str, float]:
+    """{metric: mean over the evaluated queries} (10_oracle_baseline.py:204-214) on device."""
+    from .evaluation import IREvaluator
+    names = [m if isinstance(m, str) else str(m) for m in metrics]
+    return {k: float(v) for k, v in IREvaluator(names).evaluate(run, qrels).items()}
+
+
+def analyze_oracle_selections(selections, per_query_scores):
+    """Selection counts / percentages and the mean relative gain of the selected
+    ranker over the mean of the others (10_oracle_baseline.py:217-254)."""
+    counts = defaultdict(int)
+    for ranker in selections.values():
+        counts[ranker] += 1
+    total = len(selections)
+    gains = []
+    for qid, best_ranker in selections.items():
+        best = per_query_scores[best_ranker].get(qid, 0)
+        others = [per_query_scores[r].get(qid, 0) for r in per_query_scores if r != best_ranker]
+        if others:
+            avg = np.mean(others)
+            if avg > 0:
+                gains.append((best - avg) / avg * 100)
+    return {"selection_counts": dict(counts),
+            "selection_percentages": {r: c / total * 100 for r, c in counts.items()},
+            "n_queries": total,
+            "avg_improvement_over_others": np.mean(gains) if gains else 0,
+            "max_improvement": max(gains) if gains else 0}

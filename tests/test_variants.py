@@ -112,3 +112,126 @@ def test_rrf_mul_run_bit_exact(gpu, weighted):
     got = build_rrf_run(runs, 60, qpp, 3 if weighted else None)
     want = ref_port.build_rrf_run(runs, 60, qpp, 3 if weighted else None)
     _assert_same_frame(got, want)
+
+
+# ---------------------------------------------- 10_oracle_baseline.py -------
+
+@pytest.mark.parametrize("s,want", [
+    ("ndcg@10", "nDCG@10"), ("nDCG@5", "nDCG@5"), ("ndcg", "nDCG@10"), ("map", "AP"),
+    ("AP", "AP"), ("mrr@10", "RR@10"), ("rr", "RR@10"), ("RR@3", "RR@3"), ("recall@100", "R@100"),
+    ("recall", "R@10"), ("r@5", "R@5"), (" NDCG@20 ", "nDCG@20")])
+def test_parse_metric(s, want):
+    from qppfuse.variants import parse_metric
+    assert parse_metric(s) == want
+
+
+def test_parse_metric_unknown():
+    from qppfuse.variants import parse_metric
+    with pytest.raises(ValueError, match="Unknown metric"):
+        parse_metric("p@10")
+
+
+def test_oracle_selection_rules():
+    """compute_oracle_run's loop (10_oracle_baseline.py:171-199): judged qids only, in
+    sorted order; strictly greater wins (first ranker in dict order on ties); a 0.0
+    score still beats the initial -1; a query missing from every ranker is dropped."""
+    from qppfuse.variants import _select_best
+    runs = {"A": {"1": [("a", 1.0)], "2": [("b", 1.0)], "3": [("c", 1.0)], "9": [("z", 1.0)]},
+            "B": {"1": [("d", 1.0)], "2": [("e", 1.0)], "4": [("f", 1.0)]}}
+    qrels = {"1": {"a": 1}, "2": {"b": 1}, "3": {"x": 1}, "4": {"f": 1}, "5": {"y": 1}}
+    scores = {"A": {"1": 0.5, "2": 0.25, "3": 0.0}, "B": {"1": 0.5, "2": 0.75, "4": 1.0}}
+    oracle_run, sel = _select_best(runs, qrels, scores)
+    assert sel == {"1": "A", "2": "B", "3": "A", "4": "B"}
+    assert list(oracle_run) == ["1", "2", "3", "4"]
+    assert oracle_run["2"] == [("e", 1.0)]
+
+
+def test_analyze_oracle_selections():
+    from qppfuse.variants import analyze_oracle_selections
+    sel = {"1": "A", "2": "B", "3": "A"}
+    pq = {"A": {"1": 0.6, "3": 0.5}, "B": {"1": 0.3, "2": 0.4}, "C": {"1": 0.3, "2": 0.2}}
+    a = analyze_oracle_selections(sel, pq)
+    assert a["selection_counts"] == {"A": 2, "B": 1}
+    assert a["selection_percentages"] == {"A": 2 / 3 * 100, "B": 1 / 3 * 100}
+    assert a["n_queries"] == 3
+    # q1: (0.6 - 0.3) / 0.3; q2: (0.4 - 0.1) / 0.1; q3: others average 0 -> skipped
+    gains = [(0.6 - 0.3) / 0.3 * 100, (0.4 - np.mean([0.0, 0.2])) / np.mean([0.0, 0.2]) * 100]
+    assert a["avg_improvement_over_others"] == pytest.approx(np.mean(gains))
+    assert a["max_improvement"] == pytest.approx(max(gains))
+
+
+def test_load_all_runs(tmp_path):
+    from qppfuse.variants import load_all_runs
+    (tmp_path / "BM25.res").write_text("1 Q0 a 2 0.5 t\n1 Q0 b 1 0.9 t\n2 Q0 c 1 0.1 t\n")
+    (tmp_path / "BM25.norm.res").write_text("1 Q0 a 1 1.0 t\n")
+    (tmp_path / "Dense.res").write_text("1 Q0 b 1 0.3 t\n1 Q0 a 2 0.3 t\n")
+    raw = load_all_runs(tmp_path)
+    assert list(raw) == ["BM25", "Dense"]
+    assert raw["BM25"] == {"1": [("b", 0.9), ("a", 0.5)], "2": [("c", 0.1)]}
+    assert raw["Dense"]["1"] == [("b", 0.3), ("a", 0.3)]  # stable on equal scores
+    assert load_all_runs(tmp_path, use_normalized=True) == {"BM25": {"1": [("a", 1.0)]}}
+
+
+def _oracle_metric(run, qrels, measure):
+    """Per-query values of one {qid: [(docno, score)]} run from the trec_eval restatement."""
+    from oracle import _loader as coracle
+    names = sorted({d for v in run.values() for d, _ in v} |
+                   {d for v in qrels.values() for d in v})
+    idx = {d: i for i, d in enumerate(names)}
+    qids = list(run)
+    off, docs, scs = [0], [], []
+    for q in qids:
+        dd = {}
+        for d, s in run[q]:
+            dd[d] = s
+        docs += [idx[d] for d in dd]
+        scs += list(dd.values())
+        off.append(len(docs))
+    qo, qd, qr = [0], [], []
+    for q in qids:
+        j = sorted((idx[d], r) for d, r in qrels.get(q, {}).items())
+        qd += [a for a, _ in j]
+        qr += [b for _, b in j]
+        qo.append(len(qd))
+    v = coracle.evaluate(np.array(off, np.int64), np.array(docs, np.uint32), np.array(scs),
+                         np.array(qo, np.int64), np.array(qd, np.uint32), np.array(qr, np.int32),
+                         [measure])[:, 0]
+    return {q: float(x) for q, x in zip(qids, v) if not np.isnan(x)}
+
+
+def _oracle_runs(seed, n_q=30, rankers=("BM25", "BGE", "Splade")):
+    rng = np.random.default_rng(seed)
+    runs, qrels = {}, {}
+    for q in range(n_q):
+        if q % 9 != 4:
+            qrels[str(q)] = {f"d{int(d)}": int(rng.integers(0, 3))
+                             for d in rng.choice(300, int(rng.integers(1, 8)), replace=False)}
+    for ri, r in enumerate(rankers):
+        runs[r] = {}
+        for q in range(n_q + 3):
+            if (q + ri) % 8 == 7:
+                continue
+            m = int(rng.integers(1, 120))
+            docs = [f"d{int(d)}" for d in rng.choice(300, m, replace=False)]
+            sc = rng.choice([1.0, 0.75, 0.5, 0.25], m) if q % 3 == 0 else rng.random(m)
+            runs[r][str(q)] = sorted(zip(docs, sc.tolist()), key=lambda t: -t[1])
+    return runs, qrels
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("metric", ["ndcg@10", "map", "mrr@10", "recall@100"])
+def test_oracle_baseline_on_device(gpu, metric):
+    from qppfuse.variants import (_select_best, compute_oracle_run, compute_per_query_scores,
+                                  evaluate_run, parse_metric)
+    runs, qrels = _oracle_runs(8)
+    name = parse_metric(metric)
+    got = compute_per_query_scores(runs, qrels, name)
+    want = {r: _oracle_metric(run, qrels, name) for r, run in runs.items()}
+    assert got == want
+    oracle_run, sel = compute_oracle_run(runs, qrels, name)
+    assert (oracle_run, sel) == _select_best(runs, qrels, want)
+    ms = ["nDCG@5", "nDCG@10", "RR@10", "R@100", "AP"]
+    ev = evaluate_run(oracle_run, qrels, ms)
+    for m in ms:
+        col = list(_oracle_metric(oracle_run, qrels, m).values())
+        assert ev[m] == pytest.approx(np.mean(col), rel=1e-12)
