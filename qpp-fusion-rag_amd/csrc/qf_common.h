@@ -108,14 +108,21 @@ __host__ __device__ __forceinline__ void kahan_add(Kahan& k, double v) {
   k.s = velvel;
   k.simple += v;
 }
-__host__ __device__ __forceinline__ double kahan_final(const Kahan& k) {
+// computeFinalSum in two halves, so that a serial chain can keep the first and
+// leave the second to lane-parallel code: the compensated sum, then the
+// fall-back to the simple sum when it is NaN and the simple sum infinite.
+__host__ __device__ __forceinline__ double kahan_final_sum(const Kahan& k) {
 #ifdef QF_JDK18_FINAL_SUM
-  const double tmp = k.s - k.c;  // JDK >= 18 (JDK-8214761)
+  return k.s - k.c;  // JDK >= 18 (JDK-8214761)
 #else
-  const double tmp = k.s + k.c;  // JDK 11..17
+  return k.s + k.c;  // JDK 11..17
 #endif
-  if (isnan(tmp) && isinf(k.simple)) return k.simple;
-  return tmp;
+}
+__host__ __device__ __forceinline__ double kahan_final_pick(double tmp, double simple) {
+  return (isnan(tmp) && isinf(simple)) ? simple : tmp;
+}
+__host__ __device__ __forceinline__ double kahan_final(const Kahan& k) {
+  return kahan_final_pick(kahan_final_sum(k), k.simple);
 }
 
 // Order-preserving map of a double to uint64 (ascending), with -0.0 folded

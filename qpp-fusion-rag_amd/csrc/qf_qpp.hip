@@ -11,8 +11,11 @@
 // (SigmaMax, CumNQC).  Java's sequential summation order is reproduced
 // exactly: every sum Java forms left to right is a serial chain here too, and
 // every DoubleStream.average() is the JDK's compensated (Kahan) sum.  The
-// chains of the 8 lists run batched in one wave (lane = list x chain), so the
-// serial work costs one lane each, not a whole wave.
+// chains of the 8 lists run batched (lane = list, or list x chain), so the
+// serial work costs one lane each, not a whole wave; the chains that need only
+// rsv (prefix sums, SigmaX) run on two waves at once, and everything that is not
+// a chain (computeFinalSum's check, the divisions, UEF's weight sums) is taken
+// off them.
 #include "qf_common.h"
 #include "qf_internal.h"
 
@@ -41,6 +44,29 @@ __constant__ double kUefWeight[20] = {
     0x1.e21e1180c5dabp-3,
     0x1.d9dcd21439834p-3,
     0x1.d244c78367a0dp-3};
+// Their left-to-right sums from 0.0 (the loop's `weightSum += w`): kUefWeightSum[n-1]
+// is the sum of the first n weights, so no chain of the kernel has to form it.
+__constant__ double kUefWeightSum[20] = {
+    0x1.0000000000000p+0,
+    0x1.a1849cc1a9a9ep+0,
+    0x1.10c24e60d4d4fp+1,
+    0x1.47e2b732def3dp+1,
+    0x1.79671bc097091p+1,
+    0x1.a6ff4e36345c8p+1,
+    0x1.d1a9f8e0df073p+1,
+    0x1.fa0b20114971bp+1,
+    0x1.1049a3594432dp+2,
+    0x1.22c9ad1b21972p+2,
+    0x1.34a3e09e62f78p+2,
+    0x1.45ef75973c5bap+2,
+    0x1.56beb5960f325p+2,
+    0x1.6720535a7c706p+2,
+    0x1.7720535a7c706p+2,
+    0x1.86c8ae19d29cap+2,
+    0x1.9621c47d17f01p+2,
+    0x1.a532b5091e1eep+2,
+    0x1.b4019b99bfeb0p+2,
+    0x1.c293c1d5db280p+2};
 
 // x^0.33 for x >= 0 as exp(0.33 ln x): within a few ulp of pow (Java's Math.pow is
 // itself a 1-ulp approximation), at a third of ocml pow's instructions.
@@ -67,17 +93,20 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // of one instruction instead of a whole wave's.
 constexpr int kQppLists = 8;
 constexpr int kQppBlock = 64 * kQppLists;
-constexpr int kChains = 8;   // cum, smv, wig, skew, snqc, uw, w, SigmaX-x
+constexpr int kChains = 6;   // cum, smv, wig, skew, snqc, uw
 constexpr int kRow = 65;     // padded LDS row (doubles)
+constexpr int kQppK = 50;    // k = min(50, n), QPPBridge.java:141
 
 __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     int32_t R, int32_t top_k, const int32_t* __restrict__ num_terms,
     const double* __restrict__ text_feat, double* __restrict__ out) {
   __shared__ double s_x[kQppLists][kRow];           // rsv (float32-rounded)
-  __shared__ double s_pm[kQppLists][kRow];          // prefix means
+  __shared__ double s_pf[kQppLists][kRow];          // prefix sums (Kahan s + c)
+  __shared__ double s_ps[kQppLists][kRow];          // prefix sums (simple)
   __shared__ double s_t[kQppLists][kChains][kRow];  // per-element terms of the chains
-  __shared__ double s_res[kQppLists][kChains + 1];  // chain sums; [8] = SigmaX
+  __shared__ double s_res[kQppLists][kChains];      // chain sums
+  __shared__ double s_sigmax[kQppLists];
   __shared__ unsigned long long s_fmask[kQppLists];
   __shared__ int s_k[kQppLists];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -95,19 +124,60 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
   // float32 rounding of the JSON value (Gson getAsFloat), then widened.
   const double x = act ? (double)(float)score[a + lane] : 0.0;
   s_x[w][lane] = x;
-  if (lane == 0) s_k[w] = k;
+  // col 4: SigmaX (:299-319) takes {x >= 0.5 x0} in order
+  const double thr = __shfl(x, 0, 64) * 0.5;
+  const uint64_t fmask = ballot(act && x >= thr);
+  if (lane == 0) {
+    s_k[w] = k;
+    s_fmask[w] = fmask;
+  }
   __syncthreads();
 
-  // ---- B (wave 0, lane = list): Java's compensated prefix means
-  // (DoubleStream.average of rsv[0..i]), one serial chain per list
+  // ---- B (lane = list): the serial chains that need only rsv, on two waves at once.
+  // The serial loops run to kQppK unrolled, their LDS loads issued unconditionally
+  // (rows are kRow long; values past k unused) and only the arithmetic predicated,
+  // so a chain does not wait one LDS latency per element; every sum keeps its order.
   if (w == 0 && lane < kQppLists) {
+    // Java's compensated prefix sums (DoubleStream.average of rsv[0..i]): the
+    // chain keeps only the Kahan state; computeFinalSum and the division by
+    // i + 1 run lane-parallel in C
     const int kl = s_k[lane];
     Kahan kp;
     kahan_init(kp);
-    for (int j = 0; j < kl; ++j) {
-      kahan_add(kp, s_x[lane][j]);
-      s_pm[lane][j] = kahan_final(kp) / (double)(j + 1);
+#pragma unroll
+    for (int j = 0; j < kQppK; ++j) {
+      const double v = s_x[lane][j];
+      if (j < kl) {
+        kahan_add(kp, v);
+        s_pf[lane][j] = kahan_final_sum(kp);
+        s_ps[lane][j] = kp.simple;
+      }
     }
+  } else if (w == 1 && lane < kQppLists) {
+    // SigmaX: compensated mean over F, then the compensated mean of (x - mean)^2
+    const int kl = s_k[lane];
+    const uint64_t fm = s_fmask[lane];
+    const int nf = __popcll(fm);
+    double sigmax = 0.0;
+    if (kl >= 2 && nf >= 2) {
+      Kahan kf;
+      kahan_init(kf);
+#pragma unroll
+      for (int j = 0; j < kQppK; ++j) {
+        const double v = s_x[lane][j];
+        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kf, v);
+      }
+      const double mf = kahan_final(kf) / (double)nf;
+      Kahan kfv;
+      kahan_init(kfv);
+#pragma unroll
+      for (int j = 0; j < kQppK; ++j) {
+        const double dv = s_x[lane][j] - mf;
+        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
+      }
+      sigmax = sqrt(kahan_final(kfv) / (double)nf);
+    }
+    s_sigmax[lane] = sigmax;
   }
   __syncthreads();
 
@@ -117,15 +187,20 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
   const int64_t q = lv ? l / R : 0;
   const int nt_raw = lv ? num_terms[q] : 1;
   const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
-  const double mean_i = act ? s_pm[w][lane] : 0.0;
-  const double mu = k > 0 ? s_pm[w][k - 1] : 0.0;  // Arrays.stream(rsvs).average()
+  double mean_i = 0.0;
+  if (act) {  // computeFinalSum of prefix i, / (i + 1)
+    const double tmp = s_pf[w][lane], simple = s_ps[w][lane];
+    mean_i = kahan_final_pick(tmp, simple) / (double)(lane + 1);
+  }
+  const double mu = k > 0 ? readlane_f64(mean_i, k - 1) : 0.0;  // Arrays.stream(rsvs).average()
   Kahan kv;
   kahan_init(kv);
   double sq = 0.0;
-  for (int j = 0; j < k; ++j) {
+#pragma unroll
+  for (int j = 0; j < kQppK; ++j) {
     const double del = s_x[w][j] - mean_i;
     const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
-    if (j <= lane) {
+    if (j < k && j <= lane) {
       sq += d2;
       kahan_add(kv, d2);
     }
@@ -143,9 +218,7 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
   const double muhat = mu <= 0.0 ? 1.0 : mu;                  // SMV
   const double baseline = 1.0 / (0.01 > mu ? 0.01 : mu);      // WIG
   const double std_full = sqrt(var_full);                     // RSD
-  const double x0 = s_x[w][0];
-  const double thr = x0 * 0.5;                                // SigmaX
-  double t_smv = 0.0, t_snqc = 0.0, t_skew = 0.0, t_wig = 0.0, t_uw = 0.0, t_w = 0.0;
+  double t_smv = 0.0, t_snqc = 0.0, t_skew = 0.0, t_wig = 0.0, t_uw = 0.0;
   if (act) {
     if (x > 0.0) {
       t_smv = x * fabs(log(x / muhat));
@@ -155,10 +228,7 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     }
     t_skew = cube((x - mu) / std_full);
     t_wig = x - baseline;
-    if (lane < 20) {  // UEF DCG weights (:349-363)
-      t_w = kUefWeight[lane];
-      t_uw = x * t_w;
-    }
+    if (lane < 20) t_uw = x * kUefWeight[lane];  // UEF (:349-363)
   }
   // Java adds the x <= 0 terms of SMV / SNQC as "skip": adding +0.0 is the same.
   // col 9: CumNQC (:400-410) sums the NQC of prefix sizes 2..n in order.
@@ -168,51 +238,24 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
   s_t[w][3][lane] = t_skew;
   s_t[w][4][lane] = t_snqc;
   s_t[w][5][lane] = t_uw;
-  s_t[w][6][lane] = t_w;
-  s_t[w][7][lane] = x;
-  // col 4: SigmaX (:299-319) takes {x >= thr} in order
-  const uint64_t fmask = ballot(act && x >= thr);
-  if (lane == 0) s_fmask[w] = fmask;
   const double mx = wave_max(act ? x : -INFINITY);
   const double mn = wave_min(act ? x : INFINITY);
   __syncthreads();
 
   // ---- D (wave 0, lane = list * 8 + chain): the left-to-right sums, all chains
-  // of all lists at once; chain 7 is SigmaX's compensated mean over F
-  if (w == 0) {
+  // of all lists at once
+  if (w == 0 && (lane & 7) < kChains) {
     const int ll = lane >> 3, c = lane & 7;
     const int kl = s_k[ll];
-    const int len = (c == 5 || c == 6) ? (kl < 20 ? kl : 20) : kl;
-    const uint64_t fm = s_fmask[ll];
+    const int len = c == 5 ? (kl < 20 ? kl : 20) : kl;
     const double* row = s_t[ll][c];
     double acc = 0.0;
-    Kahan kf;
-    kahan_init(kf);
-    for (int j = 0; j < len; ++j) {
+#pragma unroll
+    for (int j = 0; j < kQppK; ++j) {
       const double v = row[j];
-      acc += v;
-      if (c == 7 && ((fm >> j) & 1ull)) kahan_add(kf, v);
+      if (j < len) acc += v;
     }
-    const int nf = __popcll(fm);
-    const double mf = kahan_final(kf) / (double)nf;
-    s_res[ll][c] = c == 7 ? mf : acc;
-    // SigmaX variance: compensated mean of (x - mf)^2 over F, in order
-    const double mfl = __shfl(mf, ll * 8 + 7, 64);
-    if (c == 0) {
-      double sigmax = 0.0;
-      if (kl >= 2 && nf >= 2) {
-        const double* xr = s_t[ll][7];
-        Kahan kfv;
-        kahan_init(kfv);
-        for (int j = 0; j < kl; ++j)
-          if ((fm >> j) & 1ull) {
-            const double dv = xr[j] - mfl;
-            kahan_add(kfv, dv * dv);
-          }
-        sigmax = sqrt(kahan_final(kfv) / (double)nf);
-      }
-      s_res[ll][8] = sigmax;
-    }
+    s_res[ll][c] = acc;
   }
   __syncthreads();
 
@@ -223,8 +266,9 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     return;
   }
   const double cum = s_res[w][0], smv = s_res[w][1], wig = s_res[w][2], skew = s_res[w][3];
-  const double snqc = s_res[w][4], util = s_res[w][5], wsum = s_res[w][6];
-  const double sigmax = s_res[w][8];
+  const double snqc = s_res[w][4], util = s_res[w][5];
+  const double wsum = kUefWeightSum[(k < 20 ? k : 20) - 1];
+  const double sigmax = s_sigmax[w];
   const double cumnqc = k < 2 ? 0.0 : cum / (double)(k - 1);
   double res[kQppCols];
   res[0] = nqc;
