@@ -504,7 +504,8 @@ void join_kernel(FuseParams p) {
       if (g + 1 < s_off[r + 1]) {
         if (p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) {
           const raw_t nx = lane == 63 ? ScoreIn<KIND>::raw(p.score, g + 1) : nxt;
-          if (ScoreIn<KIND>::val(nx) > ScoreIn<KIND>::val(sc[j])) status = QF_QSTATUS_UNSORTED;
+          // raw compare: m / 1e6 is strictly increasing in the micro-units m
+          if (nx > sc[j]) status = QF_QSTATUS_UNSORTED;
         }
         if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
           status = QF_QSTATUS_RANKORDER;
@@ -712,22 +713,27 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
   // ---- the join kernel's unsorted scores -> LDS, their key range -----------------
   uint64_t fk[ITEMS];
   double fv[ITEMS];  // the scores themselves (the linearised window key needs them)
+  uint32_t ud[ITEMS];  // learned fusion: the docids (their range for the docid passes)
   uint64_t kmn = ~0ull, kmx = 0ull;
   uint32_t dmn = ~0u, dmx = 0u;
+  // every row's load in flight before the first use (one HBM latency, not one per row)
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = (wid * rows + j) * 64 + lane;
+    fv[j] = (j < rows && i < U) ? io[i] : 0.0;
+    ud[j] = (by_docid && j < rows && i < U) ? udoc[i] : 0u;
+  }
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (wid * rows + j) * 64 + lane;
     fk[j] = 0;
-    fv[j] = 0.0;
     if (j < rows && i < U) {
-      fv[j] = io[i];
       fk[j] = ~f64_asc_key(fv[j]);  // ascending sort on ~key == descending score
       kmn = min(kmn, fk[j]);
       kmx = max(kmx, fk[j]);
       if (by_docid) {
-        const uint32_t d = udoc[i];
-        dmn = min(dmn, d);
-        dmx = max(dmx, d);
+        dmn = min(dmn, ud[j]);
+        dmx = max(dmx, ud[j]);
       }
     }
   }
