@@ -67,8 +67,9 @@ struct ScoreIn<1> {
   static __device__ __forceinline__ raw_t raw(const void* p, int64_t i) {
     return ((const int32_t*)p)[i];
   }
-  // m / 1e6 is the nearest double to the "%.6f" text, i.e. pandas' parse.
-  static __device__ __forceinline__ double val(raw_t r) { return (double)r / 1e6; }
+  // m / 1e6 is the nearest double to the "%.6f" text, i.e. pandas' parse
+  // (correctly rounded without a division: qf_common.h micro_to_f64).
+  static __device__ __forceinline__ double val(raw_t r) { return micro_to_f64(r); }
   static __device__ __forceinline__ double load(const void* p, int64_t i) { return val(raw(p, i)); }
 };
 
@@ -623,11 +624,11 @@ void join_kernel(FuseParams p) {
         // (s - 0.0) / 1.0 == s bit for bit (-0.0 included): skip the division.
         a0 += den > 0.0 ? ((den == 1.0 && mn == 0.0) ? s : (s - mn) / den) : 0.0;
       }
-      if (methods & QF_RRF) a1 += 1.0 / (double)(rrf_k + pos + 1);  // ranx rrf: rank = position
+      if (methods & QF_RRF) a1 += recip_int(rrf_k + pos + 1);  // ranx rrf: rank = position
       if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += s_w[r] * s;  // src/fusion.py:273
       if (methods & QF_WRRF) {                                      // src/fusion.py:374
         const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
-        a5 += s_w[r] / (double)(rrf_k + rk);
+        a5 += div_int(s_w[r], rrf_k + rk);
       }
       if (methods & (QF_PROBFUSE | QF_WRRF_MUL)) {
         const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;  // int(row["rank"])
@@ -637,10 +638,10 @@ void join_kernel(FuseParams p) {
           const int64_t pp = rk > 0 ? rk : 1;
           int64_t k = (pp * p.n_seg + p.seg_len - 1) / p.seg_len;
           k = k < 1 ? 1 : (k > p.n_seg ? p.n_seg : k);
-          a7 += p.seg_prob[r * p.n_seg + (int)k - 1] / (double)k;
+          a7 += div_int(p.seg_prob[r * p.n_seg + (int)k - 1], (int)k);
         }
         if (methods & QF_WRRF_MUL)  // QPPrrf_argmax.py:71: weight * (1.0 / (k + rank))
-          a8 += s_w[r] * (1.0 / (double)(rrf_k + rk));
+          a8 += s_w[r] * recip_int(rrf_k + rk);
       }
       if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
         const double y = s * s_w[r] - c6;

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
   double mean_i = 0.0;
   if (act) {  // computeFinalSum of prefix i, / (i + 1)
     const double tmp = s_pf[w][lane], simple = s_ps[w][lane];
-    mean_i = kahan_final_pick(tmp, simple) / (double)(lane + 1);
+    mean_i = div_int(kahan_final_pick(tmp, simple), lane + 1);
   }
   const double mu = k > 0 ? readlane_f64(mean_i, k - 1) : 0.0;  // Arrays.stream(rsvs).average()
   Kahan kv;
@@ -205,8 +205,8 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
       kahan_add(kv, d2);
     }
   }
-  const double nqc_i = sq / (double)(lane + 1);
-  const double var_i = kahan_final(kv) / (double)(lane + 1);
+  const double nqc_i = div_int(sq, lane + 1);
+  const double var_i = div_int(kahan_final(kv), lane + 1);
   const double sigma_i = sqrt(var_i);
   const double nqc = k > 0 ? readlane_f64(nqc_i, k - 1) : 0.0;  // col 0: NQC (:202-216)
   const double var_full = k > 0 ? readlane_f64(var_i, k - 1) : 0.0;
