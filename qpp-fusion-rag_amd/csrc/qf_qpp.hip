@@ -68,9 +68,10 @@ __constant__ double kUefWeightSum[20] = {
     0x1.b4019b99bfeb0p+2,
     0x1.c293c1d5db280p+2};
 
-// x^0.33 for x >= 0 as exp(0.33 ln x): within a few ulp of pow (Java's Math.pow is
-// itself a 1-ulp approximation), at a third of ocml pow's instructions.
-__device__ __forceinline__ double pow033(double x) { return exp(0.33 * log(x)); }
+// SNQC's pow(pow(1, 0.33) * pow(y, 0.33), 0.33) = y^(0.33 * 0.33) for y >= 0, as one
+// exp(0.1089 ln y): within a few ulp of the nested pows (Java's Math.pow is itself a
+// 1-ulp approximation; pow(1.0, 0.33) == 1.0 exactly), at a sixth of their instructions.
+__device__ __forceinline__ double snqc_term(double y) { return exp((0.33 * 0.33) * log(y)); }
 
 // x^3 with one rounding of the square carried (fma): ~1 ulp, like pow(x, 3.0).
 __device__ __forceinline__ double cube(double x) {
@@ -223,8 +224,7 @@ __global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
     if (x > 0.0) {
       t_smv = x * fabs(log(x / muhat));
       const double del = x - mu;
-      const double prod = 1.0 * pow033((del * del) / x);  // pow(1.0, 0.33) == 1.0
-      t_snqc = pow033(prod);
+      t_snqc = snqc_term((del * del) / x);
     }
     t_skew = cube((x - mu) / std_full);
     t_wig = x - baseline;
