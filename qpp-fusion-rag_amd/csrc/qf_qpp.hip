@@ -300,13 +300,24 @@ __global__ __launch_bounds__(256) void qpp_colminmax_kernel(
   const int rc = blockIdx.x;  // r * 13 + c
   const int r = rc / kQppCols, c = rc % kQppCols;
   double vmin = INFINITY, vmax = -INFINITY;
-  for (int64_t q = threadIdx.x; q < Q; q += blockDim.x) {
-    const int64_t l = q * R + r;
-    if (list_off[l + 1] > list_off[l]) {
-      const double v = raw[l * kQppCols + c];
-      vmin = fmin(vmin, v);
-      vmax = fmax(vmax, v);
+  // 8 queries per thread per step, their loads in flight together
+  constexpr int kU = 8;
+  for (int64_t q0 = threadIdx.x; q0 < Q; q0 += (int64_t)blockDim.x * kU) {
+    double v[kU];
+    bool pr[kU];
+#pragma unroll
+    for (int t = 0; t < kU; ++t) {
+      const int64_t q = q0 + (int64_t)t * blockDim.x;
+      const int64_t l = q * R + r;
+      pr[t] = q < Q && list_off[l + 1] > list_off[l];
+      v[t] = q < Q ? raw[l * kQppCols + c] : 0.0;
     }
+#pragma unroll
+    for (int t = 0; t < kU; ++t)
+      if (pr[t]) {
+        vmin = fmin(vmin, v[t]);
+        vmax = fmax(vmax, v[t]);
+      }
   }
   vmin = wave_min(vmin);
   vmax = wave_max(vmax);
@@ -495,23 +506,34 @@ __global__ __launch_bounds__(256) void qpp_normalize_kernel(
   if (l >= Q * R) return;
   const int r = (int)(l % R);
   const bool present = list_off[l + 1] > list_off[l];
-  double wsum = 0.0, wsel = 0.0;
+  // every load in flight before the first use (one memory latency per thread)
+  double xs[kQppCols], m0[kQppCols], m1[kQppCols];
+#pragma unroll
   for (int c = 0; c < kQppCols; ++c) {
-    const double x = raw[l * kQppCols + c];
+    xs[c] = raw[l * kQppCols + c];
+    m0[c] = mode != 0 ? mm[r * kQppCols + c] : 0.0;
+    m1[c] = mode != 0 ? mm[R * kQppCols + r * kQppCols + c] : 0.0;
+  }
+  double wsum = 0.0, wsel = 0.0;
+#pragma unroll
+  for (int c = 0; c < kQppCols; ++c) {
+    const double x = xs[c];
     double v = x;
     if (mode == 1) {
-      const double vmin = mm[r * kQppCols + c];
-      const double vmax = -mm[R * kQppCols + r * kQppCols + c];
+      const double vmin = m0[c];
+      const double vmax = -m1[c];
       const double scale = vmax > vmin ? vmax - vmin : 1.0;
       v = scale > 0.0 ? (x - vmin) / scale : 0.0;
     } else if (mode == 2) {  // zscore: mm = [mean, scale] (qpp_colmeanstd)
-      v = (x - mm[r * kQppCols + c]) / mm[R * kQppCols + r * kQppCols + c];
+      v = (x - m0[c]) / m1[c];
     }
     if (!present) v = 0.0;
     const long long m = round6(v);
     if (norm_out) norm_out[l * kQppCols + c] = v;
     if (micro_out) micro_out[l * kQppCols + c] = m;
-    const double back = (double)m / 1e6;  // float("%.6f") of the written text
+    // float("%.6f") of the written text: m / 1e6 (division-free where checked exact)
+    const double back = (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m)
+                                                               : (double)m / 1e6;
     wsum += back;                          // Python sum(): left to right
     if (c == qpp_index) wsel = back;
   }
