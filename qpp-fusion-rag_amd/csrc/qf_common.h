@@ -152,6 +152,12 @@ __device__ __forceinline__ double div_small(double w, int n) {
   const double q = w * y;
   return fma(fma(-q, d, w), y, q);
 }
+// a / b given y = 1 / b (IEEE, once per list) for 2^-900 <= a, b normal: the
+// min-max scaling's quotient, one multiply and two fmas per element.
+__device__ __forceinline__ double div_by_recip(double a, double b, double y) {
+  const double q = a * y;
+  return fma(fma(-q, b, a), y, q);
+}
 // 1 / n and w / n for any int n and double w: the division-free forms where
 // they are checked exact, IEEE division elsewhere (n out of range, w zero,
 // subnormal, huge, infinite or NaN — a zero w's sign is lost on the fast path).

@@ -34,11 +34,15 @@ __global__ __launch_bounds__(256) void minmax_per_query_kernel(
     mn = wave_min(mn);
     mx = wave_max(mx);
     const double range = mx > mn ? mx - mn : 1.0;
+    const double y = 1.0 / range;  // one IEEE division per list
+    const bool fast = range >= 0x1p-900 && range <= 0x1p900;
 #pragma unroll
     for (int j = 0; j < kRegRows; ++j) {
       const int64_t i = a + j * 64 + lane;
       if (i < b) {
-        const double x = (v[j] - mn) / range;
+        const double d = v[j] - mn;
+        const double x = (fast && d >= 0x1p-900 && d <= 0x1p900) ? div_by_recip(d, range, y)
+                                                                 : d / range;
         if (out_norm) out_norm[i] = x;
         if (out_micro) out_micro[i] = (int32_t)round6(x);
       }
@@ -54,8 +58,12 @@ __global__ __launch_bounds__(256) void minmax_per_query_kernel(
   mn = wave_min(mn);
   mx = wave_max(mx);
   const double range = mx > mn ? mx - mn : 1.0;
+  const double y = 1.0 / range;
+  const bool fast = range >= 0x1p-900 && range <= 0x1p900;
   for (int64_t i = a + lane; i < b; i += 64) {
-    const double v = (score[i] - mn) / range;
+    const double d = score[i] - mn;
+    const double v = (fast && d >= 0x1p-900 && d <= 0x1p900) ? div_by_recip(d, range, y)
+                                                             : d / range;
     if (out_norm) out_norm[i] = v;
     if (out_micro) out_micro[i] = (int32_t)round6(v);
   }

@@ -4,13 +4,15 @@
 //   recip:  1 / n for every n in [1, 2^24]   (qf_common.h recip_small)
 //   quot:   w / n for 2^32 pseudo-random (w, n), w of every magnitude, n <= 2^24
 //           (qf_common.h div_small)
-// Prints the mismatch count of each; the library relies on all three being 0.
+//   unit:   a / b for 2^32 pseudo-random doubles b of every magnitude and a in [0, b]
+//           with y = 1 / b computed once (qf_common.h div_by_recip: min-max scaling)
+// Prints the mismatch count of each; the library relies on all four being 0.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
 #include "../qpp-fusion-rag_amd/csrc/qf_common.h"
 
-__device__ unsigned long long g_bad[3];
+__device__ unsigned long long g_bad[4];
 
 __global__ void micro(long long base) {
   const long long m = base + (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -43,16 +45,35 @@ __global__ void quot(unsigned seed) {
     atomicAdd(&g_bad[2], 1ull);
 }
 
+__global__ void unit(unsigned seed) {
+  uint64_t h = ((uint64_t)seed << 32) ^ ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+  const int ex = (int)((h >> 52) % 1601) - 800;
+  const double b = ldexp(1.0 + (double)(h & ((1ull << 52) - 1)) * 0x1p-52, ex);
+  uint64_t g = h * 0x9E3779B97F4A7C15ull;
+  g ^= g >> 31; g *= 0xbf58476d1ce4e5b9ull; g ^= g >> 29;
+  // a = b * t, t in (0, 1]: uniform mantissa, and every 4th a tiny fraction of b
+  double t = (double)((g >> 11) | 1) * 0x1p-53;
+  if ((g & 3) == 0) t = ldexp(t, -(int)((g >> 2) % 60));
+  const double a = b * t;
+  const double y = 1.0 / b;
+  if (!(a >= 0x1p-900)) return;  // the fast path's domain
+  const double want = a / b;
+  if (__double_as_longlong(want) != __double_as_longlong(qf::div_by_recip(a, b, y)))
+    atomicAdd(&g_bad[3], 1ull);
+}
+
 int main() {
-  unsigned long long zero[3] = {0, 0, 0}, bad[3];
+  unsigned long long zero[4] = {0, 0, 0, 0}, bad[4];
   hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof zero);
   for (long long b = 0; b < (1ll << 32); b += (1ll << 30))
     hipLaunchKernelGGL(micro, dim3(1 << 22), dim3(256), 0, 0, b);
   hipLaunchKernelGGL(recip, dim3((1 << 24) / 256 + 1), dim3(256), 0, 0, 0);
   for (unsigned s = 0; s < 16; ++s) hipLaunchKernelGGL(quot, dim3(1 << 20), dim3(256), 0, 0, s);
+  for (unsigned s = 0; s < 16; ++s) hipLaunchKernelGGL(unit, dim3(1 << 20), dim3(256), 0, 0, s);
   hipDeviceSynchronize();
   hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof bad);
-  printf("{\"micro_all_int32\": %llu, \"recip_1_to_2^24\": %llu, \"quot_2^32_random\": %llu}\n",
-         bad[0], bad[1], bad[2]);
-  return (bad[0] | bad[1] | bad[2]) ? 1 : 0;
+  printf("{\"micro_all_int32\": %llu, \"recip_1_to_2^24\": %llu, \"quot_2^32_random\": %llu, "
+         "\"unit_2^32_random\": %llu}\n", bad[0], bad[1], bad[2], bad[3]);
+  return (bad[0] | bad[1] | bad[2] | bad[3]) ? 1 : 0;
 }
