@@ -425,7 +425,7 @@ void join_kernel(FuseParams p) {
   using raw_t = typename L::raw_t;
   __shared__ __attribute__((aligned(16))) unsigned char smem[L::kBytes];
   __shared__ int64_t s_off[kRMax + 1];
-  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax];
+  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax], s_rden[kRMax];
   __shared__ int s_cnt[ITEMS * WAVES], s_gof[ITEMS * WAVES];
   __shared__ int s_U, s_status;
   uint32_t* tkey = (uint32_t*)smem;
@@ -461,6 +461,7 @@ void join_kernel(FuseParams p) {
     }
     s_min[tid] = mn;
     s_den[tid] = mx - mn;
+    s_rden[tid] = 1.0 / (mx - mn);  // one IEEE division per list (div_by_recip)
   }
   for (int i = tid * 4; i < TS; i += BLOCK * 4)
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
@@ -622,7 +623,15 @@ void join_kernel(FuseParams p) {
         const double den = s_den[r], mn = s_min[r];
         // A .norm.res list is already [0, 1] (min 0.000000, max 1.000000), where
         // (s - 0.0) / 1.0 == s bit for bit (-0.0 included): skip the division.
-        a0 += den > 0.0 ? ((den == 1.0 && mn == 0.0) ? s : (s - mn) / den) : 0.0;
+        double x = 0.0;
+        if (den > 0.0) {
+          const double d = s - mn;
+          x = (den == 1.0 && mn == 0.0) ? s
+              : (den >= 0x1p-900 && den <= 0x1p900 && d >= 0x1p-900 && d <= 0x1p900)
+                  ? div_by_recip(d, den, s_rden[r])
+                  : d / den;
+        }
+        a0 += x;
       }
       if (methods & QF_RRF) a1 += recip_int(rrf_k + pos + 1);  // ranx rrf: rank = position
       if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += s_w[r] * s;  // src/fusion.py:273
