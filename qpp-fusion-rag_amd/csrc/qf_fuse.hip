@@ -260,6 +260,7 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
     sh += kDigit;
     if (sh < (fallback ? hb_full : nb)) continue;
     if (fallback || exact) return;
+    QF_STAMP_INIT();
     // -- A: find the runs to fix (read-only) ----------------------------------------
     // First every row's predecessor window and, where the windows tie, both scores
     // are loaded (all rows' loads in flight at once), then compared: one memory
@@ -319,7 +320,9 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
       }
       if (any) atomicOr(&sx.flag[0], 2);
     }
+    QF_STAMP(5);
     __syncthreads();
+    QF_STAMP(6);
     const int f = sx.flag[0];  // block-uniform
     if (f == 0) return;        // no bad item: already in full-key order
     if (!(f & 1)) {
@@ -344,6 +347,7 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
       }
       __syncthreads();
     }
+    QF_STAMP(7);
     if (sx.flag[0] & 1) {  // a run too long: finish with full LSD passes
       fallback = true;
       sh = 0;

@@ -40,7 +40,12 @@ for ms in (["rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"
     st = buf.reshape(NB, NS)[:nb, :14].astype(np.float64)
     st = st[st[:, 0] > 0]  # blocks that ran (not padding / other pass)
     tot = st[:, :3].sum(1).mean()
-    out["+".join(ms)] = {"cycles_per_block": round(tot),
+    fx = buf.reshape(NB, NS)[Q:nb, 5:8].astype(np.float64)  # sort blocks only (join uses 3-7)
+    fx = fx[fx[:, 1] > 0]
+    fixup = {"fix:scan": round(float(fx[:, 0].mean())), "fix:barrier": round(float(fx[:, 1].mean())),
+             "fix:runs+bar": round(float(fx[:, 2].mean())),
+             "fix:blocks_with_runs": round(float((fx[:, 2] > 2000).mean()), 3)} if len(fx) else {}
+    out["+".join(ms)] = {"cycles_per_block": round(tot), **fixup,
                          **{n: round(float(st[:, i].mean())) for i, n in enumerate(names)}}
     js = buf.reshape(NB, NS)[:Q].astype(np.float64)
     jn = {3: "join:load+init", 4: "join:insert", 5: "join:reps+scans", 6: "join:placement",
