@@ -98,7 +98,7 @@ constexpr int kChains = 6;   // cum, smv, wig, skew, snqc, uw
 constexpr int kRow = 65;     // padded LDS row (doubles)
 constexpr int kQppK = 50;    // k = min(50, n), QPPBridge.java:141
 
-__global__ __launch_bounds__(kQppBlock) void qpp_raw_kernel(
+__global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     int32_t R, int32_t top_k, const int32_t* __restrict__ num_terms,
     const double* __restrict__ text_feat, double* __restrict__ out) {
