@@ -396,12 +396,19 @@ def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     return None, None
 
 
+def progress(msg: str):
+    """One line on stderr per phase (long runs are not silent; stdout stays one JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
     from qppfuse import _lib
     _lib.lib()
+    progress(f"rank {rank}/{world}: generating {args.workload} inputs")
     p = Pipeline(args, world, rank, dev)
+    progress(f"rank {rank}: {p.Q} queries x {p.R} x top-{p.K} resident; warmup {args.warmup}")
     for _ in range(args.warmup):
         p.step()
     torch.cuda.synchronize()
@@ -409,6 +416,7 @@ def main():
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
+    progress(f"rank {rank}: timing {args.steps} steps")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         p.step(timed=True)
@@ -432,6 +440,7 @@ def main():
     achieved = fbytes / (fuse_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args)
     valu = pmc_valu(args)
+    progress(f"rank {rank}: {elapsed / args.steps * 1e3:.3f} ms/step; parity + NDCG checks")
     parity = check_parity(p, min(args.check, p.Q)) if args.check > 0 else None
     ndcg_vals, eval_ms = ndcg_device(p)
     result = None
@@ -440,6 +449,7 @@ def main():
         ported = all(m in METHODS for m in p.methods)
         if world == 1 and args.cpu_sample > 0 and ported:
             nq = min(args.cpu_sample, p.Q)
+            progress(f"CPU baseline on {nq} queries")
             v, dt = cpu_baseline_port(p, nq)
             cpu = {"value": round(v, 4), "unit": "fused queries/s", "cores": 1, "kind": "port",
                    "sample": f"{nq} queries x {args.retrievers} x top-{args.k}: 13 QPP "

@@ -125,6 +125,13 @@ __host__ __device__ __forceinline__ double kahan_final(const Kahan& k) {
   return kahan_final_pick(kahan_final_sum(k), k.simple);
 }
 
+// Linear workgroup id of a grid made by grid_for() (qf_internal.h): the grid
+// folds into y beyond 65,536 workgroups, x-fastest, so consecutive ids keep the
+// XCD round-robin.
+__device__ __forceinline__ int64_t block_id() {
+  return (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+}
+
 // ---- correctly rounded quotients without a division --------------------------
 // Markstein: with y = RN(1/b) and q within one ulp of a/b, the residual
 // a - q*b is exact in one fma and RN(q + residual*y) = RN(a/b).  The join uses

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(64 * kEvalWaves) void eval_kernel(EvalParams p) {
   __shared__ int s_rel[kEvalWaves][kEvalMaxRel];
   __shared__ int s_ideal[kEvalWaves][kEvalMaxRel];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * kEvalWaves + w;
+  const int64_t gw = block_id() * kEvalWaves + w;
   if (gw >= p.n_queries * (int64_t)p.n_runs) return;
   const int m = (int)(gw / p.n_queries);
   const int64_t q = gw % p.n_queries;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(64 * kEvalWaves) void eval_kernel(EvalParams p) {
 hipError_t eval_launch(const EvalParams& p, hipStream_t st) {
   const int64_t waves = p.n_queries * (int64_t)p.n_runs;
   if (waves == 0) return hipSuccess;
-  hipLaunchKernelGGL(eval_kernel, dim3((unsigned)((waves + kEvalWaves - 1) / kEvalWaves)),
+  hipLaunchKernelGGL(eval_kernel, grid_for((waves + kEvalWaves - 1) / kEvalWaves),
                      dim3(64 * kEvalWaves), 0, st, p);
   return hipGetLastError();
 }

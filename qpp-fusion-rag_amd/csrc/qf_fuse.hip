@@ -42,8 +42,8 @@ __device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
 #define QF_STAMP(slot)                                                          \
   do {                                                                          \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                 \
-    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                          \
-      g_stamps[blockIdx.x * kStampSlots + (slot)] += _t - _st_prev;             \
+    if (threadIdx.x == 0 && block_id() < kStampBlocks)                          \
+      g_stamps[block_id() * kStampSlots + (slot)] += _t - _st_prev;              \
     _st_prev = _t;                                                              \
   } while (0)
 #else
@@ -439,7 +439,7 @@ void join_kernel(FuseParams p) {
   };
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t q = blockIdx.x;
+  const int64_t q = block_id();
   if (q >= p.n_queries) return;
   QF_STAMP_INIT();
   const int R = p.R;
@@ -847,8 +847,9 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
   // block -> (query, method slot): slot-major groups of 8 queries, so that the
   // blocks resident together on an XCD (blockIdx % 8) read adjacent queries.
   const int M = __popc(p.methods);
-  const int64_t grp8 = (int64_t)(blockIdx.x >> 3);
-  const int64_t q = (grp8 / M) * 8 + (blockIdx.x & 7);
+  const int64_t bid = block_id();
+  const int64_t grp8 = bid >> 3;
+  const int64_t q = (grp8 / M) * 8 + (bid & 7);
   const int ms = (int)(grp8 % M);
   if (q >= p.n_queries) return;
   const int U = p.union_count[q];
@@ -907,7 +908,7 @@ int fuse_max_entries() { return JoinXL::kNMax; }
 
 template <class J>
 static void launch_join(const FuseParams& p, int kind, hipStream_t st) {
-  dim3 grid((unsigned)p.n_queries), block(J::kBlock);
+  const dim3 grid = grid_for(p.n_queries), block(J::kBlock);
   if (kind == 1) hipLaunchKernelGGL((join_kernel<J, 1>), grid, block, 0, st, p);
   else hipLaunchKernelGGL((join_kernel<J, 0>), grid, block, 0, st, p);
 }
@@ -916,7 +917,7 @@ template <class S>
 static void launch_sort(const FuseParams& p, int umin, hipStream_t st) {
   const int M = __builtin_popcount((unsigned)p.methods);
   const int64_t groups = (p.n_queries + 7) / 8;
-  hipLaunchKernelGGL((fuse_kernel<S>), dim3((unsigned)(groups * 8 * M)), dim3(S::kBlock), 0, st,
+  hipLaunchKernelGGL((fuse_kernel<S>), grid_for(groups * 8 * M), dim3(S::kBlock), 0, st,
                      p, umin);
 }
 
@@ -958,7 +959,7 @@ __global__ __launch_bounds__(256) void topk_kernel(int64_t n_queries, int32_t R,
                                                    uint32_t* __restrict__ out_docid,
                                                    double* __restrict__ out_score) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // q * M + m
+  const int64_t row = block_id() * 4 + (threadIdx.x >> 6);  // q * M + m
   if (row >= n_queries * M) return;
   const int64_t q = row / M;
   const int m = (int)(row % M);
@@ -985,7 +986,7 @@ hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
                        int32_t k, uint32_t* out_docid, double* out_score, hipStream_t st) {
   const int64_t rows = n_queries * M;
   if (rows == 0 || k == 0) return hipSuccess;
-  hipLaunchKernelGGL(topk_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, n_queries,
+  hipLaunchKernelGGL(topk_kernel, grid_for((rows + 3) / 4), dim3(256), 0, st, n_queries,
                      R, list_off, union_count, union_docid, perm, fused, out_stride, M, k,
                      out_docid, out_score);
   return hipGetLastError();

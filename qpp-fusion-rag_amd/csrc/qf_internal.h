@@ -6,6 +6,16 @@
 
 namespace qf {
 
+// A grid of n_blocks workgroups.  A dispatch holds at most 2^32 - 1 work-items per
+// dimension (a C3-sized synth or a 10-million-query join exceeds that in x alone),
+// so beyond 65,536 workgroups the grid folds into y; kernels take block_id() and
+// return for ids >= n_blocks (the last y row may overshoot).
+inline dim3 grid_for(int64_t n_blocks) {
+  if (n_blocks <= 65536) return dim3((unsigned)(n_blocks > 0 ? n_blocks : 1));
+  return dim3(65536u, (unsigned)((n_blocks + 65535) / 65536));
+}
+
+
 struct FuseParams {
   int64_t n_queries;
   int32_t R;

@@ -27,7 +27,7 @@
 namespace qf {
 
 __global__ __launch_bounds__(256) void gbdt_predict_kernel(GbdtParams p) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t idx = block_id() * blockDim.x + threadIdx.x;
   if (idx >= p.n_rows * p.n_boosters) return;
   const int64_t row = idx / p.n_boosters;
   const int b = (int)(idx % p.n_boosters);
@@ -77,7 +77,7 @@ __device__ __forceinline__ double np_pairwise_sum(const double* a, int n) {
 }
 
 __global__ __launch_bounds__(256) void learned_weights_kernel(LearnedWeightParams p) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t q = block_id() * blockDim.x + threadIdx.x;
   if (q >= p.n_queries) return;
   double c[kMaxBoosters];
   for (int b = 0; b < p.n_boosters; ++b) {
@@ -96,13 +96,13 @@ __global__ __launch_bounds__(256) void learned_weights_kernel(LearnedWeightParam
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st) {
   const int64_t n = p.n_rows * p.n_boosters;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(gbdt_predict_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(gbdt_predict_kernel, grid_for((n + 255) / 256), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 
 hipError_t learned_weights_launch(const LearnedWeightParams& p, hipStream_t st) {
   if (p.n_queries == 0) return hipSuccess;
-  hipLaunchKernelGGL(learned_weights_kernel, dim3((unsigned)((p.n_queries + 255) / 256)),
+  hipLaunchKernelGGL(learned_weights_kernel, grid_for((p.n_queries + 255) / 256),
                      dim3(256), 0, st, p);
   return hipGetLastError();
 }

@@ -13,7 +13,7 @@ __global__ __launch_bounds__(256) void minmax_per_query_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     double* __restrict__ out_norm, int32_t* __restrict__ out_micro) {
   const int lane = threadIdx.x & 63;
-  const int64_t l = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t l = block_id() * 4 + (threadIdx.x >> 6);
   if (l >= n_lists) return;
   const int64_t a = list_off[l], b = list_off[l + 1];
   constexpr int kRegRows = 16;  // lists of <= 1024 entries: one HBM read, held in registers
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void minmax_per_query_kernel(
 hipError_t minmax_launch(const double* score, const int64_t* list_off, int64_t n_lists,
                          double* out_norm, int32_t* out_micro, hipStream_t st) {
   if (n_lists == 0) return hipSuccess;
-  hipLaunchKernelGGL(minmax_per_query_kernel, dim3((unsigned)((n_lists + 3) / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(minmax_per_query_kernel, grid_for((n_lists + 3) / 4), dim3(256), 0,
                      st, score, list_off, n_lists, out_norm, out_micro);
   return hipGetLastError();
 }
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void synth_kernel(int64_t q_begin, int64_t n_q
                                                      int64_t* __restrict__ list_off,
                                                      uint32_t* __restrict__ docid,
                                                      double* __restrict__ score) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t idx = block_id() * blockDim.x + threadIdx.x;
   const int64_t total = n_queries * R * (int64_t)K;
   if (idx == 0) list_off[n_queries * R] = total;
   if (idx >= total) return;
@@ -150,7 +150,7 @@ hipError_t synth_launch(int64_t q_begin, int64_t n_queries, int32_t R, int32_t K
                         hipStream_t st) {
   const int64_t total = n_queries * R * (int64_t)K;
   const int64_t blocks = total > 0 ? (total + 255) / 256 : 1;
-  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, q_begin, n_queries, R,
+  hipLaunchKernelGGL(synth_kernel, grid_for(blocks), dim3(256), 0, st, q_begin, n_queries, R,
                      K, seed, p_shared, list_off, docid, score);
   return hipGetLastError();
 }

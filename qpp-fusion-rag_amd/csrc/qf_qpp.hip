@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   __shared__ unsigned long long s_fmask[kQppLists];
   __shared__ int s_k[kQppLists];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t l = (int64_t)blockIdx.x * kQppLists + w;
+  const int64_t l = block_id() * kQppLists + w;
   const bool lv = l < n_lists;  // every wave stays for the barriers
   int k = 0;
   int64_t a = 0;
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(256) void qpp_normalize_kernel(
     const double* __restrict__ raw, const double* __restrict__ mm,
     const int64_t* __restrict__ list_off, int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
     double* __restrict__ norm_out, int64_t* __restrict__ micro_out, double* __restrict__ w_out) {
-  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // list index q*R + r
+  const int64_t l = block_id() * blockDim.x + threadIdx.x;  // list index q*R + r
   if (l >= Q * R) return;
   const int r = (int)(l % R);
   const bool present = list_off[l + 1] > list_off[l];
@@ -545,8 +545,8 @@ hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t 
                           hipStream_t st) {
   const int64_t L = Q * R;
   if (L == 0) return hipSuccess;
-  const unsigned grid = (unsigned)((L + kQppLists - 1) / kQppLists);
-  hipLaunchKernelGGL(qpp_raw_kernel, dim3(grid), dim3(kQppBlock), 0, st, score, list_off, L, R,
+  hipLaunchKernelGGL(qpp_raw_kernel, grid_for((L + kQppLists - 1) / kQppLists), dim3(kQppBlock), 0,
+                     st, score, list_off, L, R,
                      top_k, nt, tf, out);
   return hipGetLastError();
 }
@@ -571,7 +571,7 @@ hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64
                                 hipStream_t st) {
   const int64_t L = Q * R;
   if (L == 0) return hipSuccess;
-  hipLaunchKernelGGL(qpp_normalize_kernel, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(qpp_normalize_kernel, grid_for((L + 255) / 256), dim3(256), 0, st,
                      raw, mm, list_off, Q, R, mode, qpp_index, norm_out, micro_out, w_out);
   return hipGetLastError();
 }

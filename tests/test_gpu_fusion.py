@@ -254,3 +254,41 @@ def test_fused_topk_compaction(gpu, k):
             np.testing.assert_array_equal(d[q, m, :n], ud[b + perm[m, b:b + n].astype(np.int64)])
             assert s[q, m, :n].tobytes() == fz[m, b:b + n].tobytes()
             assert (d[q, m, n:] == 0xFFFFFFFF).all() and np.isnan(s[q, m, n:]).all()
+
+
+def test_grids_beyond_65536_workgroups(gpu):
+    """Launches of more than 65,536 workgroups fold into a 2-D grid (a dispatch holds at
+    most 2^32 - 1 work-items per dimension): the join (one workgroup per query), the six
+    sorts, the min-max and the synthetic generator all run 2-D here, bit-exact."""
+    from qppfuse import engine
+    Q, R, K = 140_000, 2, 2
+    off, docid, raw = engine.synth_runs(0, Q, R, K, seed=5)
+    norm, micro = engine.minmax_per_query(raw, off)  # 70,000 workgroups
+    rng = np.random.default_rng(9)
+    w = torch.from_numpy(rng.random(Q * R).round(6)).to(gpu)
+    out = engine.fuse(off, docid, micro, R, ALL, rrf_k=60, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    raw_h = raw.cpu().numpy()
+    o_norm = coracle.minmax_per_query(raw_h, off_h)
+    assert norm.cpu().numpy().tobytes() == o_norm.tobytes()
+    sample = np.random.default_rng(2).choice(len(o_norm), 2000, replace=False)
+    mh = micro.cpu().numpy()
+    assert [f"{m // 10**6}.{m % 10**6:06d}" for m in mh[sample]] == \
+        [f"{x:.6f}" for x in o_norm[sample]]
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    uc = out.union_count.cpu().numpy()
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fused = out.fused.cpu().numpy()
+    E = Q * R * K
+    qb = np.repeat(off_h[0:-1:R][:Q], R * K)
+    valid = (np.arange(E) - qb) < np.repeat(uc, R * K)
+    for m, name in enumerate(ALL):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60,
+                                                   weights=w.cpu().numpy())
+        np.testing.assert_array_equal(uc, o_uc)
+        np.testing.assert_array_equal(ud[valid], o_ud[valid])
+        np.testing.assert_array_equal(perm[m][valid], o_perm[valid], err_msg=name)
+        assert fused[m][valid].tobytes() == o_fused[valid].tobytes(), name
