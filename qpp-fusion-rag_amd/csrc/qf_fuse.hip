@@ -392,6 +392,85 @@ __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
   }
 }
 
+// ---- one document's fused scores --------------------------------------------
+// Per-list constants of one query (ranx min-max end points, QPP weights, offsets).
+struct ListConsts {
+  const int64_t* off;  // [R + 1] absolute list offsets
+  const double* w;     // [R] weights (1.0 without)
+  const double* mn;    // [R] list minimum (ranx min-max)
+  const double* den;   // [R] max - min
+  const double* rden;  // [R] 1 / (max - min)
+};
+// Adds a document's contributions in retriever order — the reference's
+// left-to-right sums, bit for bit — for every requested method at once, and
+// stores them unsorted at fused[slot][at]: the workspace join of very large
+// queries.  The LDS join spells the same sums out inline (through this helper
+// the C2 join spills 32 more bytes per thread; tests/test_gpu_fusion.py checks
+// both paths against the oracle).
+struct DocSums {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0, a6 = 0.0, c6 = 0.0, a7 = 0.0, a8 = 0.0;
+  __device__ __forceinline__ void add(const FuseParams& p, int methods, const ListConsts& lc,
+                                      double s, int r, int pos) {
+    if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // ranx min-max normalised score
+      const double den = lc.den[r], mn = lc.mn[r];
+      // A .norm.res list is already [0, 1] (min 0.000000, max 1.000000), where
+      // (s - 0.0) / 1.0 == s bit for bit (-0.0 included): skip the division.
+      double x = 0.0;
+      if (den > 0.0) {
+        const double d = s - mn;
+        x = (den == 1.0 && mn == 0.0) ? s
+            : (den >= 0x1p-900 && den <= 0x1p900 && d >= 0x1p-900 && d <= 0x1p900)
+                ? div_by_recip(d, den, lc.rden[r])
+                : d / den;
+      }
+      a0 += x;
+    }
+    if (methods & QF_RRF) a1 += recip_int(p.rrf_k + pos + 1);  // ranx rrf: rank = position
+    if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += lc.w[r] * s;  // src/fusion.py:273
+    if (methods & QF_WRRF) {                                       // src/fusion.py:374
+      const int rk = p.rank ? p.rank[lc.off[r] + pos] : pos + 1;
+      a5 += div_int(lc.w[r], p.rrf_k + rk);
+    }
+    if (methods & (QF_PROBFUSE | QF_WRRF_MUL)) {
+      const int rk = p.rank ? p.rank[lc.off[r] + pos] : pos + 1;  // int(row["rank"])
+      if (methods & QF_PROBFUSE) {  // ProbFuse.py:30-39,172-179
+        // ceil(rank * x / L) in integers (exact: the float quotient of two
+        // integers below 2^26 is never rounded onto an integer), clipped to [1, x]
+        const int64_t pp = rk > 0 ? rk : 1;
+        int64_t k = (pp * p.n_seg + p.seg_len - 1) / p.seg_len;
+        k = k < 1 ? 1 : (k > p.n_seg ? p.n_seg : k);
+        a7 += div_int(p.seg_prob[r * p.n_seg + (int)k - 1], (int)k);
+      }
+      if (methods & QF_WRRF_MUL)  // QPPrrf_argmax.py:71: weight * (1.0 / (k + rank))
+        a8 += lc.w[r] * recip_int(p.rrf_k + rk);
+    }
+    if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
+      const double y = s * lc.w[r] - c6;
+      const double t = a6 + y;
+      c6 = (t - a6) - y;
+      if (c6 != c6) c6 = 0.0;  // +-inf contributions (pandas GH#53606)
+      a6 = t;
+    }
+  }
+  // cnt: the document's list count (CombMNZ: sum x count, src/fusion.py:327).
+  // Output slot of method bit t: the requested methods below it (scalar popcounts).
+  __device__ __forceinline__ void store(const FuseParams& p, int methods, double cnt,
+                                        int64_t at) const {
+    double* out = p.fused + at;
+    const int64_t st = p.out_stride;
+    auto slot = [&](int t) -> int64_t { return __popc((unsigned)methods & ((1u << t) - 1u)); };
+    if (methods & QF_COMBSUM) out[slot(0) * st] = a0;
+    if (methods & QF_COMBMNZ) out[slot(1) * st] = a0 * cnt;
+    if (methods & QF_RRF) out[slot(2) * st] = a1;
+    if (methods & QF_WCOMBSUM) out[slot(3) * st] = a2;
+    if (methods & QF_WCOMBMNZ) out[slot(4) * st] = a2 * cnt;
+    if (methods & QF_WRRF) out[slot(5) * st] = a5;
+    if (methods & QF_LEARNED) out[slot(6) * st] = a6;
+    if (methods & QF_PROBFUSE) out[slot(7) * st] = a7;
+    if (methods & QF_WRRF_MUL) out[slot(8) * st] = a8;
+  }
+};
+
 // ============================================================================
 // join_kernel
 // ============================================================================
@@ -894,6 +973,301 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
   }
 }
 
+
+// ============================================================================
+// join_sort_xl_kernel — queries beyond the LDS join (JoinXL::kNMax < N <= 65,535,
+// e.g. 16 runs x top-4000): the same algorithm with its tables in a global
+// workspace, one 1,024-thread workgroup per query.
+//   1. insert every entry into a hash table (docid, retriever mask, first
+//      entry: atomicCAS / atomicOr / atomicMin), remembering each entry's slot;
+//   2. number documents u in first-seen order (a document's representative is
+//      its smallest entry index; block scans over the entries in order);
+//   3. group offsets (scan of the masks' popcounts), each entry's place in its
+//      group in retriever order, and DocSums over every group — the same sums
+//      as the LDS join, bit for bit;
+//   4. per method slot, a bitonic sort of (key = ~orderable(score), tie = u —
+//      or docid for learned fusion) — unique pairs, so the order equals the
+//      stable sort of the LDS path: passes with stride >= kXlTile run in the
+//      workspace, the rest on kXlTile-item tiles in LDS.
+// A persistent grid of G workgroups lists the large queries of each strided
+// chunk (one parallel load of their sizes) and runs them in turn, so batches
+// without large queries cost one short launch — and fuse_launch only makes it
+// when max_entries says a large query may exist.
+// ============================================================================
+constexpr int kXlBlock = 1024;
+constexpr int kXlTile = 4096;  // bitonic items per LDS tile (64 KB of keys + ties)
+constexpr int kXlNMax = 65535; // perm entries and u are uint16
+constexpr int kXlGrid = 64;    // workgroups (each with ~4.5 MB of workspace at kXlNMax)
+
+struct XlWs {
+  uint32_t *tkey, *tmask, *tfirst, *tu;  // [TS] hash table
+  uint32_t *eslot, *umask, *ugo, *gent;  // [NMAX] entry slot, document masks / group
+                                         // starts, grouped entries (e | r << 16)
+  uint64_t *skey, *stie;                 // [P] sort keys and ties
+  double* sval;                          // [P] unsorted scores (their sign kept)
+};
+static __host__ __device__ inline int64_t xl_ws_bytes(int ts, int nmax, int np) {
+  const int64_t a = 16 * (int64_t)ts + 16 * (int64_t)nmax + 24 * (int64_t)np;
+  return (a + 255) & ~(int64_t)255;
+}
+__device__ __forceinline__ XlWs xl_ws(unsigned char* b, int ts, int nmax, int np) {
+  XlWs w;
+  uint32_t* t = (uint32_t*)b;
+  w.tkey = t; w.tmask = t + ts; w.tfirst = t + 2 * ts; w.tu = t + 3 * ts;
+  uint32_t* e = t + 4 * ts;
+  w.eslot = e; w.umask = e + nmax; w.ugo = e + 2 * nmax; w.gent = e + 3 * nmax;
+  uint64_t* k = (uint64_t*)(((uintptr_t)(e + 4 * nmax) + 7) & ~(uintptr_t)7);
+  w.skey = k; w.stie = k + np; w.sval = (double*)(k + 2 * np);
+  return w;
+}
+
+// Phase boundary of the workspace kernel: agent-scope fence (the tables are
+// written with L2 atomics and read back through L1) + barrier.
+__device__ __forceinline__ void xl_sync() {
+  __threadfence();
+  __syncthreads();
+}
+
+// Exclusive scan of v over the 1,024 threads; *total gets the sum.
+__device__ __forceinline__ uint32_t xl_scan(uint32_t v, uint32_t* s_wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan_dpp(v);
+  if (lane == 63) s_wsum[wid] = inc;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (int w = 0; w < kXlBlock / 64; ++w) {
+    const uint32_t x = s_wsum[w];
+    before += w < wid ? x : 0u;
+    all += x;
+  }
+  __syncthreads();  // s_wsum is reused by the next call
+  *total = all;
+  return before + inc - v;
+}
+
+__device__ __forceinline__ void xl_cmpswap(uint64_t& ka, uint64_t& ta, uint64_t& kb,
+                                           uint64_t& tb, bool asc) {
+  const bool gt = ka > kb || (ka == kb && ta > tb);
+  if (gt == asc) {
+    const uint64_t k = ka, t = ta;
+    ka = kb; ta = tb; kb = k; tb = t;
+  }
+}
+
+template <int KIND>
+__device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, int pb,
+                       int64_t* s_off, double* s_w, double* s_min, double* s_den,
+                       double* s_rden, uint32_t* s_wsum, int* s_status, uint64_t* t_key,
+                       uint64_t* t_tie) {
+  const int tid = threadIdx.x;
+  const int R = p.R, TS = 1 << tb;
+  if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
+  if (tid == 0) *s_status = 0;
+  __syncthreads();
+  const int64_t base = s_off[0];
+  const int N = (int)(s_off[R] - base);  // JoinXL::kNMax < N <= kXlNMax (the lister's test)
+  if (tid < R) {  // as the LDS join
+    const int64_t a = s_off[tid], b = s_off[tid + 1];
+    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
+    double mx = 0.0, mn = 0.0;
+    if (b > a) {
+      mx = ScoreIn<KIND>::load(p.score, a);
+      mn = ScoreIn<KIND>::load(p.score, b - 1);
+    }
+    s_min[tid] = mn;
+    s_den[tid] = mx - mn;
+    s_rden[tid] = 1.0 / (mx - mn);
+  }
+  for (int i = tid; i < TS; i += kXlBlock) {
+    w.tkey[i] = kEmpty;
+    w.tmask[i] = 0u;
+    w.tfirst[i] = kEmpty;
+  }
+  xl_sync();
+  // ---- 1. insert --------------------------------------------------------------
+  int status = 0, r = 0;
+  for (int e = tid; e < N; e += kXlBlock) {
+    const int64_t g = base + e;
+    while (g >= s_off[r + 1]) ++r;
+    const uint32_t d = p.docid[g];
+    if (d == kEmpty) status = QF_QSTATUS_BADDOC;
+    uint32_t h = (d * 0x9E3779B1u) >> (32 - tb);
+    while (true) {
+      const uint32_t prev = atomicCAS(&w.tkey[h], kEmpty, d);
+      if (prev == kEmpty || prev == d) break;
+      h = (h + 1) & (TS - 1);
+    }
+    const uint32_t old = atomicOr(&w.tmask[h], 1u << r);
+    if ((old >> r) & 1u) status = QF_QSTATUS_DUPDOC;
+    atomicMin(&w.tfirst[h], (uint32_t)e);
+    w.eslot[e] = h;
+    if (g + 1 < s_off[r + 1]) {
+      if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
+          ScoreIn<KIND>::raw(p.score, g + 1) > ScoreIn<KIND>::raw(p.score, g))
+        status = QF_QSTATUS_UNSORTED;
+      if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
+        status = QF_QSTATUS_RANKORDER;
+    }
+  }
+  if (status) atomicMin(s_status, status);
+  xl_sync();
+  if (*s_status) {  // uniform
+    if (tid == 0) p.union_count[q] = *s_status;
+    __syncthreads();
+    return;
+  }
+  // ---- 2. first-seen numbering ---------------------------------------------------
+  uint32_t U = 0;
+  for (int c0 = 0; c0 < N; c0 += kXlBlock) {
+    const int e = c0 + tid;
+    uint32_t h = 0;
+    bool rep = false;
+    if (e < N) {
+      h = w.eslot[e];
+      rep = w.tfirst[h] == (uint32_t)e;
+    }
+    uint32_t tot;
+    const uint32_t u = U + xl_scan(rep ? 1u : 0u, s_wsum, &tot);
+    if (rep) {
+      w.tu[h] = u;
+      w.umask[u] = w.tmask[h];
+      p.union_docid[base + u] = w.tkey[h];
+    }
+    U += tot;
+  }
+  xl_sync();
+  // ---- 3. groups and sums -------------------------------------------------------
+  uint32_t go = 0;
+  for (int c0 = 0; c0 < (int)U; c0 += kXlBlock) {
+    const int u = c0 + tid;
+    const uint32_t pc = u < (int)U ? (uint32_t)__popc(w.umask[u]) : 0u;
+    uint32_t tot;
+    const uint32_t x = go + xl_scan(pc, s_wsum, &tot);
+    if (u < (int)U) w.ugo[u] = x;
+    go += tot;
+  }
+  xl_sync();
+  r = 0;
+  for (int e = tid; e < N; e += kXlBlock) {
+    while (base + e >= s_off[r + 1]) ++r;
+    const uint32_t u = w.tu[w.eslot[e]];
+    const uint32_t k = w.ugo[u] + (uint32_t)__popc(w.umask[u] & ((1u << r) - 1u));
+    w.gent[k] = (uint32_t)e | ((uint32_t)r << 16);
+  }
+  xl_sync();
+  const int methods = p.methods;
+  const ListConsts lc{s_off, s_w, s_min, s_den, s_rden};
+  for (int u = tid; u < (int)U; u += kXlBlock) {
+    const int gs = (int)w.ugo[u], ge = u + 1 < (int)U ? (int)w.ugo[u + 1] : N;
+    DocSums acc;
+    for (int k = gs; k < ge; ++k) {
+      const uint32_t v = w.gent[k];
+      const int e = (int)(v & 0xFFFFu), rr = (int)(v >> 16);
+      acc.add(p, methods, lc, ScoreIn<KIND>::load(p.score, base + e), rr,
+              (int)(base + e - s_off[rr]));
+    }
+    acc.store(p, methods, (double)(ge - gs), base + u);
+  }
+  xl_sync();
+  // ---- 4. sort every method slot ------------------------------------------------
+  const int NP = 1 << pb, T = NP < kXlTile ? NP : kXlTile;
+  const int M = __popc(methods);
+  for (int ms = 0; ms < M; ++ms) {
+    const bool by_docid = slot_method(methods, ms) == 6;
+    double* io = p.fused + (int64_t)ms * p.out_stride + base;
+    uint16_t* pm = p.perm + (int64_t)ms * p.out_stride + base;
+    for (int i = tid; i < NP; i += kXlBlock) {
+      uint64_t k = ~0ull, t = ~0ull;  // padding sorts last
+      if (i < (int)U) {
+        const double v = io[i];
+        w.sval[i] = v;
+        k = ~f64_asc_key(v);
+        t = by_docid ? ((uint64_t)p.union_docid[base + i] << 16) | (uint64_t)i : (uint64_t)i;
+      }
+      w.skey[i] = k;
+      w.stie[i] = t;
+    }
+    xl_sync();
+    // stages k (and strides j < T) inside LDS tiles of T items
+    auto tile_pass = [&](int kk, int j0) {
+      for (int t0 = 0; t0 < NP; t0 += T) {
+        for (int i = tid; i < T; i += kXlBlock) {
+          t_key[i] = w.skey[t0 + i];
+          t_tie[i] = w.stie[t0 + i];
+        }
+        __syncthreads();
+        for (int k2 = (kk ? kk : 2); k2 <= (kk ? kk : T); k2 <<= 1) {
+          for (int j = kk ? j0 : k2 >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < T / 2; t += kXlBlock) {
+              const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+              xl_cmpswap(t_key[i], t_tie[i], t_key[i + j], t_tie[i + j],
+                         ((t0 + i) & k2) == 0);
+            }
+            __syncthreads();
+          }
+        }
+        for (int i = tid; i < T; i += kXlBlock) {
+          w.skey[t0 + i] = t_key[i];
+          w.stie[t0 + i] = t_tie[i];
+        }
+        __syncthreads();
+      }
+      xl_sync();
+    };
+    tile_pass(0, 0);  // every stage k <= T
+    for (int kk = 2 * T; kk <= NP; kk <<= 1) {
+      for (int j = kk >> 1; j >= T; j >>= 1) {
+        for (int t = tid; t < NP / 2; t += kXlBlock) {
+          const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+          uint64_t ka = w.skey[i], ta = w.stie[i], kb = w.skey[i + j], tb2 = w.stie[i + j];
+          xl_cmpswap(ka, ta, kb, tb2, (i & kk) == 0);
+          w.skey[i] = ka; w.stie[i] = ta; w.skey[i + j] = kb; w.stie[i + j] = tb2;
+        }
+        xl_sync();
+      }
+      tile_pass(kk, T >> 1);
+    }
+    for (int i = tid; i < (int)U; i += kXlBlock) {
+      const uint32_t u = (uint32_t)(w.stie[i] & 0xFFFFu);
+      pm[i] = (uint16_t)u;
+      io[i] = w.sval[u];
+    }
+    xl_sync();
+  }
+  if (tid == 0) p.union_count[q] = (int)U;
+  __syncthreads();
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kXlBlock) void join_sort_xl_kernel(FuseParams p, int nmin,
+                                                                unsigned char* ws, int64_t ws_each,
+                                                                int tb, int pb) {
+  __shared__ int64_t s_off[kRMax + 1];
+  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax], s_rden[kRMax];
+  __shared__ uint32_t s_wsum[kXlBlock / 64];
+  __shared__ int s_status, s_n;
+  __shared__ int64_t s_list[kXlBlock];
+  __shared__ uint64_t t_key[kXlTile], t_tie[kXlTile];
+  const int tid = threadIdx.x;
+  const XlWs w = xl_ws(ws + (int64_t)blockIdx.x * ws_each, 1 << tb, kXlNMax, 1 << pb);
+  const int64_t span = (int64_t)gridDim.x * kXlBlock;
+  for (int64_t c0 = 0; c0 < p.n_queries; c0 += span) {
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    const int64_t q = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
+    if (q < p.n_queries) {
+      const int64_t n = p.list_off[q * p.R + p.R] - p.list_off[q * p.R];
+      if (n > nmin && n <= kXlNMax) s_list[atomicAdd(&s_n, 1)] = q;
+    }
+    __syncthreads();
+    const int n = s_n;
+    for (int t = 0; t < n; ++t)
+      xl_one<KIND>(p, s_list[t], w, tb, pb, s_off, s_w, s_min, s_den, s_rden, s_wsum,
+                   &s_status, t_key, t_tie);
+    __syncthreads();
+  }
+}
+
 // ---- launch -----------------------------------------------------------------
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
 using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
@@ -904,7 +1278,7 @@ using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
 using SortXL = SortCfg<1024, 10, 2>;  // U <= 10240
 
-int fuse_max_entries() { return JoinXL::kNMax; }
+int fuse_max_entries() { return kXlNMax; }
 
 template <class J>
 static void launch_join(const FuseParams& p, int kind, hipStream_t st) {
@@ -941,6 +1315,25 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     launch_sort<SortM>(p, 0, st);
     launch_sort_large<SortL>(p, SortM::kUMax + 1, st, 1);  // the queries SortM left
     if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
+  }
+  if (max_entries > JoinXL::kNMax) {  // queries the LDS join marked QF_QSTATUS_TOOBIG
+    int tb = 1, pb = 0;
+    while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
+    while ((1 << pb) < max_entries) ++pb;
+    const int64_t each = xl_ws_bytes(1 << tb, kXlNMax, 1 << pb);
+    const int64_t g = p.n_queries < kXlGrid ? p.n_queries : kXlGrid;
+    void* ws = nullptr;
+    hipError_t e = hipMallocAsync(&ws, (size_t)(each * g), st);
+    if (e != hipSuccess) return e;
+    if (kind == 1)
+      hipLaunchKernelGGL((join_sort_xl_kernel<1>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
+                         JoinXL::kNMax, (unsigned char*)ws, each, tb, pb);
+    else
+      hipLaunchKernelGGL((join_sort_xl_kernel<0>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
+                         JoinXL::kNMax, (unsigned char*)ws, each, tb, pb);
+    e = hipGetLastError();
+    const hipError_t f = hipFreeAsync(ws, st);
+    return e != hipSuccess ? e : f;
   }
   return hipGetLastError();
 }

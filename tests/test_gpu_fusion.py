@@ -148,14 +148,14 @@ def test_edge_cases_empty_lists_ties_single(gpu):
             assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
-@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680, 7681, 10240])
+@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680, 7681, 10240, 10241, 65535])
 def test_kernel_capacity_boundaries(gpu, n_entries):
     """Queries exactly at / just past each kernel configuration's capacity."""
     from qppfuse import engine
     R = 2
     rng = np.random.default_rng(n_entries)
     a = n_entries // 2
-    docs = rng.choice(50_000, size=n_entries, replace=False).astype(np.uint32)
+    docs = rng.choice(max(50_000, 2 * n_entries), size=n_entries, replace=False).astype(np.uint32)
     docs[a:a + a // 3] = docs[: a // 3]  # overlap between the two lists
     s1 = np.sort(rng.integers(0, 10**6, a))[::-1] / 1e6
     s2 = np.sort(rng.integers(0, 10**6, n_entries - a))[::-1] / 1e6
@@ -208,7 +208,8 @@ def _sort_case(kind, n, rng):
     return s
 
 
-@pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000, 7681, 10240])
+@pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000, 7681, 10240, 10241,
+                               40000])
 @pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform",
                                   "huge_and_inf"])
 def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
@@ -292,3 +293,75 @@ def test_grids_beyond_65536_workgroups(gpu):
         np.testing.assert_array_equal(ud[valid], o_ud[valid])
         np.testing.assert_array_equal(perm[m][valid], o_perm[valid], err_msg=name)
         assert fused[m][valid].tobytes() == o_fused[valid].tobytes(), name
+
+
+@pytest.mark.parametrize("kind", ["f64", "micro"])
+def test_workspace_path_for_very_large_queries(gpu, kind):
+    """Queries beyond the LDS join (more than 10,240 entries, up to 65,535) run the
+    workspace join + bitonic sort (join_sort_xl_kernel); small queries of the same
+    call still take the LDS kernels.  Every method bit-exact vs the oracle."""
+    from qppfuse import engine
+    R = 4
+    rng = np.random.default_rng(11 if kind == "f64" else 12)
+    sizes = [300, 5000, 0, 16383, 1, 2600]  # per-list K of each query
+    lists, ranks = [], []
+    for K in sizes:
+        pool = rng.choice(1 << 30, size=max(1, 2 * K), replace=False).astype(np.uint32)
+        for r in range(R):
+            k = K if r != 2 else K // 2  # ragged lists
+            docs = rng.choice(pool, size=k, replace=False)
+            sc = np.sort(rng.integers(0, 3000 + r * 7919, k))[::-1] / 1e6  # ties
+            lists.append((docs, sc))
+            ranks.append(np.arange(1, k + 1, dtype=np.int32))
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    n_max = int(np.max(off[R::R] - off[0:-1:R]))
+    assert n_max > 10240
+    if kind == "micro":
+        dsc = torch.from_numpy(np.rint(sc * 1e6).astype(np.int32)).to(gpu)
+    rank = np.concatenate(ranks)
+    w = rng.uniform(0.05, 1.0, len(sizes) * R)
+    out = engine.fuse(doff, ddoc, dsc, R, ALL, rrf_k=60,
+                      weights=torch.from_numpy(w).to(gpu),
+                      rank=torch.from_numpy(rank).to(gpu), max_entries=n_max)
+    uc = out.union_count.cpu().numpy()
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fz = out.fused.cpu().numpy()
+    for m, name in enumerate(ALL):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
+                                                   rank=rank)
+        np.testing.assert_array_equal(uc, o_uc)
+        for q in range(len(sizes)):
+            b, n = off[q * R], uc[q]
+            np.testing.assert_array_equal(ud[b:b + n], o_ud[b:b + n])
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=f"{name} q{q}")
+            assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
+def test_workspace_path_learned_ties_by_docid(gpu):
+    """Learned fusion on a very large query: ties in docid order (the groupby's
+    output order, src/fusion.py:443-446).  With two lists the Kahan sum equals
+    the plain left-to-right sum, so the scores are W-CombSUM's."""
+    from qppfuse import engine
+    R, K = 2, 12000
+    rng = np.random.default_rng(5)
+    pool = rng.choice(1 << 31, size=2 * K, replace=False).astype(np.uint32)
+    lists = []
+    for r in range(R):
+        lists.append((rng.choice(pool, size=K, replace=False),
+                      np.sort(rng.integers(0, 50, K))[::-1] / 1e6))
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    w = np.array([0.5, 0.25])
+    out = engine.fuse(doff, ddoc, dsc, R, ["learned"], weights=torch.from_numpy(w).to(gpu),
+                      max_entries=2 * K)
+    o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, "wcombsum", weights=w)
+    n = int(out.union_count[0])
+    assert n == o_uc[0]
+    ud = out.union_docid.cpu().numpy().view(np.uint32)[:n]
+    np.testing.assert_array_equal(ud, o_ud[:n])
+    unsorted = np.empty(n)
+    unsorted[o_perm[:n].astype(np.int64)] = o_fused[:n]
+    want = np.lexsort((ud, -unsorted))
+    perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
+    np.testing.assert_array_equal(perm, want)
+    assert out.fused.cpu().numpy()[0][:n].tobytes() == unsorted[want].tobytes()
