@@ -989,7 +989,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 //      or docid for learned fusion) — unique pairs, so the order equals the
 //      stable sort of the LDS path: passes with stride >= kXlTile run in the
 //      workspace, the rest on kXlTile-item tiles in LDS.
-// A persistent grid of G workgroups lists the large queries of each strided
+// A persistent grid of G <= 512 workgroups (two per CU) lists the large queries of each strided
 // chunk (one parallel load of their sizes) and runs them in turn, so batches
 // without large queries cost one short launch — and fuse_launch only makes it
 // when max_entries says a large query may exist.
@@ -997,7 +997,8 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 constexpr int kXlBlock = 1024;
 constexpr int kXlTile = 4096;  // bitonic items per LDS tile (64 KB of keys + ties)
 constexpr int kXlNMax = 65535; // perm entries and u are uint16
-constexpr int kXlGrid = 64;    // workgroups (each with ~4.5 MB of workspace at kXlNMax)
+constexpr int kXlGrid = 512;   // workgroups: two per CU (74 KB of LDS each) while the
+                               // workspace stays within 1 GB, else one per CU
 
 struct XlWs {
   uint32_t *tkey, *tmask, *tfirst, *tu;  // [TS] hash table
@@ -1021,11 +1022,14 @@ __device__ __forceinline__ XlWs xl_ws(unsigned char* b, int ts, int nmax, int np
   return w;
 }
 
-// Phase boundary of the workspace kernel: agent-scope fence (the tables are
-// written with L2 atomics and read back through L1) + barrier.
-__device__ __forceinline__ void xl_sync() {
-  __threadfence();
-  __syncthreads();
+// Phase boundary of the workspace kernel.  One workgroup owns its workspace and
+// its waves share one CU's write-through L1, so a workgroup barrier orders the
+// plain stores; an agent-scope fence here (an L2 write-back on gfx950) made the
+// kernel ~10x slower.  The L2 atomics of the hash table are read back with
+// L1-bypassing atomic loads instead (xl_ld).
+__device__ __forceinline__ void xl_sync() { __syncthreads(); }
+__device__ __forceinline__ uint32_t xl_ld(const uint32_t* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Exclusive scan of v over the 1,024 threads; *total gets the sum.
@@ -1124,14 +1128,14 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
     bool rep = false;
     if (e < N) {
       h = w.eslot[e];
-      rep = w.tfirst[h] == (uint32_t)e;
+      rep = xl_ld(&w.tfirst[h]) == (uint32_t)e;
     }
     uint32_t tot;
     const uint32_t u = U + xl_scan(rep ? 1u : 0u, s_wsum, &tot);
     if (rep) {
       w.tu[h] = u;
-      w.umask[u] = w.tmask[h];
-      p.union_docid[base + u] = w.tkey[h];
+      w.umask[u] = xl_ld(&w.tmask[h]);
+      p.union_docid[base + u] = xl_ld(&w.tkey[h]);
     }
     U += tot;
   }
@@ -1239,9 +1243,9 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
 }
 
 template <int KIND>
-__global__ __launch_bounds__(kXlBlock) void join_sort_xl_kernel(FuseParams p, int nmin,
+__global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p, int nmin,
                                                                 unsigned char* ws, int64_t ws_each,
-                                                                int tb, int pb) {
+                                                                int nmax, int tb, int pb) {
   __shared__ int64_t s_off[kRMax + 1];
   __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax], s_rden[kRMax];
   __shared__ uint32_t s_wsum[kXlBlock / 64];
@@ -1249,7 +1253,7 @@ __global__ __launch_bounds__(kXlBlock) void join_sort_xl_kernel(FuseParams p, in
   __shared__ int64_t s_list[kXlBlock];
   __shared__ uint64_t t_key[kXlTile], t_tie[kXlTile];
   const int tid = threadIdx.x;
-  const XlWs w = xl_ws(ws + (int64_t)blockIdx.x * ws_each, 1 << tb, kXlNMax, 1 << pb);
+  const XlWs w = xl_ws(ws + (int64_t)blockIdx.x * ws_each, 1 << tb, nmax, 1 << pb);
   const int64_t span = (int64_t)gridDim.x * kXlBlock;
   for (int64_t c0 = 0; c0 < p.n_queries; c0 += span) {
     if (tid == 0) s_n = 0;
@@ -1257,7 +1261,7 @@ __global__ __launch_bounds__(kXlBlock) void join_sort_xl_kernel(FuseParams p, in
     const int64_t q = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
     if (q < p.n_queries) {
       const int64_t n = p.list_off[q * p.R + p.R] - p.list_off[q * p.R];
-      if (n > nmin && n <= kXlNMax) s_list[atomicAdd(&s_n, 1)] = q;
+      if (n > nmin && n <= nmax) s_list[atomicAdd(&s_n, 1)] = q;
     }
     __syncthreads();
     const int n = s_n;
@@ -1320,17 +1324,20 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     int tb = 1, pb = 0;
     while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
     while ((1 << pb) < max_entries) ++pb;
-    const int64_t each = xl_ws_bytes(1 << tb, kXlNMax, 1 << pb);
-    const int64_t g = p.n_queries < kXlGrid ? p.n_queries : kXlGrid;
+    const int nmax = max_entries < kXlNMax ? max_entries : kXlNMax;
+    const int64_t each = xl_ws_bytes(1 << tb, nmax, 1 << pb);
+    int64_t g = ((int64_t)1 << 30) / each;
+    g = g < kXlGrid / 2 ? kXlGrid / 2 : (g > kXlGrid ? kXlGrid : g);
+    if (p.n_queries < g) g = p.n_queries;
     void* ws = nullptr;
     hipError_t e = hipMallocAsync(&ws, (size_t)(each * g), st);
     if (e != hipSuccess) return e;
     if (kind == 1)
       hipLaunchKernelGGL((join_sort_xl_kernel<1>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
-                         JoinXL::kNMax, (unsigned char*)ws, each, tb, pb);
+                         JoinXL::kNMax, (unsigned char*)ws, each, nmax, tb, pb);
     else
       hipLaunchKernelGGL((join_sort_xl_kernel<0>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
-                         JoinXL::kNMax, (unsigned char*)ws, each, tb, pb);
+                         JoinXL::kNMax, (unsigned char*)ws, each, nmax, tb, pb);
     e = hipGetLastError();
     const hipError_t f = hipFreeAsync(ws, st);
     return e != hipSuccess ? e : f;

@@ -1,0 +1,66 @@
+"""Timing of the workspace fusion path (queries above the LDS kernels' 10,240 entries)
+next to the LDS path on the same total entries (development tool, not the bench).
+
+python tools/xlbench.py [Q] [R] [K]   (default 3452 x 16 x 1000 = 16,000 entries/query)
+"""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
+import os
+
+import numpy as np
+import torch
+
+from oracle import _loader as coracle
+from qppfuse import _lib, engine
+
+if os.environ.get("QF_LIB"):  # A/B a development build of the same sources
+    _lib.LIB_PATH = Path(os.environ["QF_LIB"])
+
+
+def timeit(fn, n=5):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n
+
+
+Q = int(sys.argv[1]) if len(sys.argv) > 1 else 3452
+R = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+K = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+dev = torch.device("cuda", 0)
+off, docid, raw = engine.synth_runs(0, Q, R, K)
+_, micro = engine.minmax_per_query(raw, off, want_norm=False)
+w = torch.rand(Q * R, dtype=torch.float64, device=dev)
+res = {"queries": Q, "retrievers": R, "k": K, "entries_per_query": R * K}
+for ms in (["combsum", "rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]):
+    o = engine.alloc_fuse_out(Q, Q * R * K, engine.methods_mask(ms), dev)
+    t = timeit(lambda: engine.fuse(off, docid, micro, R, ms, weights=w, max_entries=R * K, out=o))
+    res["+".join(ms) + "_ms"] = round(t, 3)
+    res["+".join(ms) + "_fused_q_per_s"] = round(Q / t * 1e3, 1)
+# parity of a few queries against the C oracle
+n = min(Q, 4)
+off_h = off.cpu().numpy()[: n * R + 1]
+doc_h = docid.cpu().numpy().view(np.uint32)[: off_h[-1]]
+sc_h = micro.cpu().numpy()[: off_h[-1]].astype(np.float64) / 1e6
+w_h = w.cpu().numpy()[: n * R]
+uc = o.union_count.cpu().numpy()
+ok = True
+for m, name in enumerate(ms):
+    _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60, weights=w_h)
+    for q in range(n):
+        b, u = off_h[q * R], o_uc[q]
+        ok &= bool(uc[q] == u)
+        ok &= o.fused[m, b:b + u].cpu().numpy().tobytes() == o_fused[b:b + u].tobytes()
+res["parity_queries"] = n
+res["bit_exact"] = ok
+res["mean_union"] = float(uc.mean())
+print(json.dumps(res))
