@@ -149,6 +149,12 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
  * query: LDS hash join over docids, contribution groups in first-seen order,
  * the ordered sums of every requested method) and a sort kernel (one workgroup
  * per (query, method): stable LDS radix sort by fused score, in place).
+ * Queries of 10,241 .. qf_max_entries_per_query() (65,535) entries take a third
+ * kernel (the same join in a global workspace + a bitonic sort), launched only
+ * when max_entries > 10,240, with a workspace allocated and freed stream-ordered
+ * (hipMallocAsync / hipFreeAsync on `stream`) — the one internal allocation.
+ * max_entries must bound every query's entry count (larger queries report
+ * QF_QSTATUS_TOOBIG).
  *
  * Inputs (device): list_off[Q*R+1] (int64), docid[E] (uint32, interned
  * docnos, 0xFFFFFFFF reserved), score[E] (score_kind), rank[E] (nullable
