@@ -978,17 +978,20 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 // join_sort_xl_kernel — queries beyond the LDS join (JoinXL::kNMax < N <= 65,535,
 // e.g. 16 runs x top-4000): the same algorithm with its tables in a global
 // workspace, one 1,024-thread workgroup per query.
-//   1. insert every entry into a hash table (docid, retriever mask, first
-//      entry: atomicCAS / atomicOr / atomicMin), remembering each entry's slot;
+//   1. insert every entry into a hash table (docid, retriever mask:
+//      atomicCAS / atomicOr), remembering each entry's slot;
 //   2. number documents u in first-seen order (a document's representative is
-//      its smallest entry index; block scans over the entries in order);
+//      its entry in the lowest retriever holding it, as in the LDS join; block
+//      scans over the entries in order);
 //   3. group offsets (scan of the masks' popcounts), each entry's place in its
 //      group in retriever order, and DocSums over every group — the same sums
 //      as the LDS join, bit for bit;
-//   4. per method slot, a bitonic sort of (key = ~orderable(score), tie = u —
-//      or docid for learned fusion) — unique pairs, so the order equals the
-//      stable sort of the LDS path: passes with stride >= kXlTile run in the
-//      workspace, the rest on kXlTile-item tiles in LDS.
+//   4. unions of up to 10,240 documents are left unsorted, with their U, to the
+//      LDS sort kernels launched after this one; larger ones get, per method
+//      slot, a bitonic sort of (key = ~orderable(score), tie = u — or docid for
+//      learned fusion) — unique pairs, so the order equals the stable sort of
+//      the LDS path: passes with stride >= kXlTile run in the workspace, the rest
+//      on kXlTile-item tiles in LDS.
 // A persistent grid of G <= 512 workgroups (two per CU) lists the large queries of each strided
 // chunk (one parallel load of their sizes) and runs them in turn, so batches
 // without large queries cost one short launch — and fuse_launch only makes it
@@ -1001,21 +1004,21 @@ constexpr int kXlGrid = 512;   // workgroups: two per CU (74 KB of LDS each) whi
                                // workspace stays within 1 GB, else one per CU
 
 struct XlWs {
-  uint32_t *tkey, *tmask, *tfirst, *tu;  // [TS] hash table
+  uint32_t *tkey, *tmask, *tu;           // [TS] hash table
   uint32_t *eslot, *umask, *ugo, *gent;  // [NMAX] entry slot, document masks / group
                                          // starts, grouped entries (e | r << 16)
   uint64_t *skey, *stie;                 // [P] sort keys and ties
   double* sval;                          // [P] unsorted scores (their sign kept)
 };
 static __host__ __device__ inline int64_t xl_ws_bytes(int ts, int nmax, int np) {
-  const int64_t a = 16 * (int64_t)ts + 16 * (int64_t)nmax + 24 * (int64_t)np;
+  const int64_t a = 12 * (int64_t)ts + 16 * (int64_t)nmax + 24 * (int64_t)np;
   return (a + 255) & ~(int64_t)255;
 }
 __device__ __forceinline__ XlWs xl_ws(unsigned char* b, int ts, int nmax, int np) {
   XlWs w;
   uint32_t* t = (uint32_t*)b;
-  w.tkey = t; w.tmask = t + ts; w.tfirst = t + 2 * ts; w.tu = t + 3 * ts;
-  uint32_t* e = t + 4 * ts;
+  w.tkey = t; w.tmask = t + ts; w.tu = t + 2 * ts;
+  uint32_t* e = t + 3 * ts;
   w.eslot = e; w.umask = e + nmax; w.ugo = e + 2 * nmax; w.gent = e + 3 * nmax;
   uint64_t* k = (uint64_t*)(((uintptr_t)(e + 4 * nmax) + 7) & ~(uintptr_t)7);
   w.skey = k; w.stie = k + np; w.sval = (double*)(k + 2 * np);
@@ -1059,12 +1062,13 @@ __device__ __forceinline__ void xl_cmpswap(uint64_t& ka, uint64_t& ta, uint64_t&
 }
 
 template <int KIND>
-__device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, int pb,
-                       int64_t* s_off, double* s_w, double* s_min, double* s_den,
+__device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, int pb,
+                       int sort_min, int64_t* s_off, double* s_w, double* s_min, double* s_den,
                        double* s_rden, uint32_t* s_wsum, int* s_status, uint64_t* t_key,
                        uint64_t* t_tie) {
   const int tid = threadIdx.x;
   const int R = p.R, TS = 1 << tb;
+  QF_STAMP_INIT();
   if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
   if (tid == 0) *s_status = 0;
   __syncthreads();
@@ -1085,9 +1089,9 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
   for (int i = tid; i < TS; i += kXlBlock) {
     w.tkey[i] = kEmpty;
     w.tmask[i] = 0u;
-    w.tfirst[i] = kEmpty;
   }
   xl_sync();
+  QF_STAMP(0);
   // ---- 1. insert --------------------------------------------------------------
   int status = 0, r = 0;
   for (int e = tid; e < N; e += kXlBlock) {
@@ -1103,7 +1107,6 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
     }
     const uint32_t old = atomicOr(&w.tmask[h], 1u << r);
     if ((old >> r) & 1u) status = QF_QSTATUS_DUPDOC;
-    atomicMin(&w.tfirst[h], (uint32_t)e);
     w.eslot[e] = h;
     if (g + 1 < s_off[r + 1]) {
       if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
@@ -1115,6 +1118,7 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
   }
   if (status) atomicMin(s_status, status);
   xl_sync();
+  QF_STAMP(1);
   if (*s_status) {  // uniform
     if (tid == 0) p.union_count[q] = *s_status;
     __syncthreads();
@@ -1122,24 +1126,28 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
   }
   // ---- 2. first-seen numbering ---------------------------------------------------
   uint32_t U = 0;
+  r = 0;
   for (int c0 = 0; c0 < N; c0 += kXlBlock) {
     const int e = c0 + tid;
-    uint32_t h = 0;
+    uint32_t h = 0, msk = 0;
     bool rep = false;
     if (e < N) {
+      while (base + e >= s_off[r + 1]) ++r;
       h = w.eslot[e];
-      rep = xl_ld(&w.tfirst[h]) == (uint32_t)e;
+      msk = xl_ld(&w.tmask[h]);
+      rep = __ffs(msk) - 1 == r;
     }
     uint32_t tot;
     const uint32_t u = U + xl_scan(rep ? 1u : 0u, s_wsum, &tot);
     if (rep) {
       w.tu[h] = u;
-      w.umask[u] = xl_ld(&w.tmask[h]);
+      w.umask[u] = msk;
       p.union_docid[base + u] = xl_ld(&w.tkey[h]);
     }
     U += tot;
   }
   xl_sync();
+  QF_STAMP(2);
   // ---- 3. groups and sums -------------------------------------------------------
   uint32_t go = 0;
   for (int c0 = 0; c0 < (int)U; c0 += kXlBlock) {
@@ -1151,6 +1159,7 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
     go += tot;
   }
   xl_sync();
+  QF_STAMP(3);
   r = 0;
   for (int e = tid; e < N; e += kXlBlock) {
     while (base + e >= s_off[r + 1]) ++r;
@@ -1159,6 +1168,7 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
     w.gent[k] = (uint32_t)e | ((uint32_t)r << 16);
   }
   xl_sync();
+  QF_STAMP(4);
   const int methods = p.methods;
   const ListConsts lc{s_off, s_w, s_min, s_den, s_rden};
   for (int u = tid; u < (int)U; u += kXlBlock) {
@@ -1173,7 +1183,13 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
     acc.store(p, methods, (double)(ge - gs), base + u);
   }
   xl_sync();
-  // ---- 4. sort every method slot ------------------------------------------------
+  QF_STAMP(5);
+  // ---- 4. sort every method slot (unions the LDS sorts cannot hold) ---------------
+  if ((int)U <= sort_min) {  // uniform: the LDS sort kernels that follow take it
+    if (tid == 0) p.union_count[q] = (int)U;
+    __syncthreads();
+    return;
+  }
   const int NP = 1 << pb, T = NP < kXlTile ? NP : kXlTile;
   const int M = __popc(methods);
   for (int ms = 0; ms < M; ++ms) {
@@ -1192,6 +1208,7 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
       w.stie[i] = t;
     }
     xl_sync();
+    QF_STAMP(6);
     // stages k (and strides j < T) inside LDS tiles of T items
     auto tile_pass = [&](int kk, int j0) {
       for (int t0 = 0; t0 < NP; t0 += T) {
@@ -1219,6 +1236,7 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
       xl_sync();
     };
     tile_pass(0, 0);  // every stage k <= T
+    QF_STAMP(7);
     for (int kk = 2 * T; kk <= NP; kk <<= 1) {
       for (int j = kk >> 1; j >= T; j >>= 1) {
         for (int t = tid; t < NP / 2; t += kXlBlock) {
@@ -1231,12 +1249,14 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
       }
       tile_pass(kk, T >> 1);
     }
+    QF_STAMP(8);
     for (int i = tid; i < (int)U; i += kXlBlock) {
       const uint32_t u = (uint32_t)(w.stie[i] & 0xFFFFu);
       pm[i] = (uint16_t)u;
       io[i] = w.sval[u];
     }
     xl_sync();
+    QF_STAMP(9);
   }
   if (tid == 0) p.union_count[q] = (int)U;
   __syncthreads();
@@ -1245,7 +1265,8 @@ __device__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, in
 template <int KIND>
 __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p, int nmin,
                                                                 unsigned char* ws, int64_t ws_each,
-                                                                int nmax, int tb, int pb) {
+                                                                int nmax, int tb, int pb,
+                                                                int sort_min) {
   __shared__ int64_t s_off[kRMax + 1];
   __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax], s_rden[kRMax];
   __shared__ uint32_t s_wsum[kXlBlock / 64];
@@ -1266,8 +1287,8 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
     __syncthreads();
     const int n = s_n;
     for (int t = 0; t < n; ++t)
-      xl_one<KIND>(p, s_list[t], w, tb, pb, s_off, s_w, s_min, s_den, s_rden, s_wsum,
-                   &s_status, t_key, t_tie);
+      xl_one<KIND>(p, s_list[t], w, tb, pb, sort_min, s_off, s_w, s_min, s_den, s_rden,
+                   s_wsum, &s_status, t_key, t_tie);
     __syncthreads();
   }
 }
@@ -1308,41 +1329,54 @@ static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st, int
                      umin);
 }
 
+// Queries above the LDS join (QF_QSTATUS_TOOBIG after it): the workspace join,
+// which sorts only the unions the LDS sorts cannot hold (U > sort_min) and
+// leaves the rest, unsorted with their U, to the sort kernels launched after it.
+static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int sort_min,
+                            hipStream_t st, void** ws_out) {
+  int tb = 1, pb = 0;
+  while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
+  while ((1 << pb) < max_entries) ++pb;
+  const int nmax = max_entries < kXlNMax ? max_entries : kXlNMax;
+  const int64_t each = xl_ws_bytes(1 << tb, nmax, 1 << pb);
+  int64_t g = ((int64_t)1 << 30) / each;
+  g = g < kXlGrid / 2 ? kXlGrid / 2 : (g > kXlGrid ? kXlGrid : g);
+  if (p.n_queries < g) g = p.n_queries;
+  hipError_t e = hipMallocAsync(ws_out, (size_t)(each * g), st);
+  if (e != hipSuccess) return e;
+  unsigned char* ws = (unsigned char*)*ws_out;
+  if (kind == 1)
+    hipLaunchKernelGGL((join_sort_xl_kernel<1>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
+                       JoinXL::kNMax, ws, each, nmax, tb, pb, sort_min);
+  else
+    hipLaunchKernelGGL((join_sort_xl_kernel<0>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
+                       JoinXL::kNMax, ws, each, nmax, tb, pb, sort_min);
+  return hipGetLastError();
+}
+
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
   if (max_entries <= JoinS::kNMax) {
     launch_join<JoinS>(p, kind, st);
     launch_sort<SortS>(p, 0, st);
-  } else {
-    if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
-    else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
-    else launch_join<JoinXL>(p, kind, st);
+    return hipGetLastError();
+  }
+  if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
+  else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
+  else launch_join<JoinXL>(p, kind, st);
+  void* ws = nullptr;
+  hipError_t e = hipSuccess;
+  if (max_entries > JoinXL::kNMax) e = launch_xl(p, kind, max_entries, SortXL::kUMax, st, &ws);
+  if (e == hipSuccess) {
     launch_sort<SortM>(p, 0, st);
     launch_sort_large<SortL>(p, SortM::kUMax + 1, st, 1);  // the queries SortM left
     if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
-  }
-  if (max_entries > JoinXL::kNMax) {  // queries the LDS join marked QF_QSTATUS_TOOBIG
-    int tb = 1, pb = 0;
-    while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
-    while ((1 << pb) < max_entries) ++pb;
-    const int nmax = max_entries < kXlNMax ? max_entries : kXlNMax;
-    const int64_t each = xl_ws_bytes(1 << tb, nmax, 1 << pb);
-    int64_t g = ((int64_t)1 << 30) / each;
-    g = g < kXlGrid / 2 ? kXlGrid / 2 : (g > kXlGrid ? kXlGrid : g);
-    if (p.n_queries < g) g = p.n_queries;
-    void* ws = nullptr;
-    hipError_t e = hipMallocAsync(&ws, (size_t)(each * g), st);
-    if (e != hipSuccess) return e;
-    if (kind == 1)
-      hipLaunchKernelGGL((join_sort_xl_kernel<1>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
-                         JoinXL::kNMax, (unsigned char*)ws, each, nmax, tb, pb);
-    else
-      hipLaunchKernelGGL((join_sort_xl_kernel<0>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
-                         JoinXL::kNMax, (unsigned char*)ws, each, nmax, tb, pb);
     e = hipGetLastError();
-    const hipError_t f = hipFreeAsync(ws, st);
-    return e != hipSuccess ? e : f;
   }
-  return hipGetLastError();
+  if (ws) {
+    const hipError_t f = hipFreeAsync(ws, st);
+    if (e == hipSuccess) e = f;
+  }
+  return e;
 }
 
 // ---- fused top-k compaction (the multi-GPU gather's payload) -------------------

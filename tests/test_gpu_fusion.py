@@ -338,12 +338,15 @@ def test_workspace_path_for_very_large_queries(gpu, kind):
             assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
-def test_workspace_path_learned_ties_by_docid(gpu):
+@pytest.mark.parametrize("K", [6000, 12000])
+def test_workspace_path_learned_ties_by_docid(gpu, K):
     """Learned fusion on a very large query: ties in docid order (the groupby's
     output order, src/fusion.py:443-446).  With two lists the Kahan sum equals
-    the plain left-to-right sum, so the scores are W-CombSUM's."""
+    the plain left-to-right sum, so the scores are W-CombSUM's.  K = 6000: a union
+    of ~9,000 (the workspace join, then the LDS sort); K = 12000: ~18,000 (the
+    workspace bitonic sort)."""
     from qppfuse import engine
-    R, K = 2, 12000
+    R = 2
     rng = np.random.default_rng(5)
     pool = rng.choice(1 << 31, size=2 * K, replace=False).astype(np.uint32)
     lists = []
