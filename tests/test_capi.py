@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol():
 def test_version_and_limits():
     from qppfuse import _lib
     assert "gfx950" in _lib.version()
-    assert _lib.max_entries_per_query() >= 5000  # 5 retrievers x top-1000 in one workgroup
+    # LDS kernels to 10,240 entries, the workspace kernel beyond; perm / u are uint16
+    assert _lib.max_entries_per_query() == 65535
 
 
 def test_argument_validation_without_device():
