@@ -1061,6 +1061,43 @@ __device__ __forceinline__ void xl_cmpswap(uint64_t& ka, uint64_t& ta, uint64_t&
   }
 }
 
+// Bitonic stages on LDS tiles of T items: kk == 0 runs every stage k <= T in
+// full; else stage kk from stride j0 down (the strides below T of a stage whose
+// larger strides ran in the workspace).  Direction from the item's global index.
+__device__ __forceinline__ void xl_tile_pass(uint64_t* __restrict__ gkey,
+                                             uint64_t* __restrict__ gtie, uint64_t* t_key,
+                                             uint64_t* t_tie, int NP, int T, int kk, int j0) {
+  const int tid = threadIdx.x;
+  for (int t0 = 0; t0 < NP; t0 += T) {
+    for (int i = tid; i < T; i += kXlBlock) {
+      t_key[i] = gkey[t0 + i];
+      t_tie[i] = gtie[t0 + i];
+    }
+    __syncthreads();
+    const int k_lo = kk ? kk : 2, k_hi = kk ? kk : T;
+    for (int k2 = k_lo; k2 <= k_hi; k2 <<= 1) {
+      for (int j = kk ? j0 : k2 >> 1; j > 0; j >>= 1) {
+        for (int t = tid; t < T / 2; t += kXlBlock) {
+          const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+          uint64_t ka = t_key[i], ta = t_tie[i], kb = t_key[i + j], tb = t_tie[i + j];
+          const bool asc = ((t0 + i) & k2) == 0;
+          const bool gt = ka > kb || (ka == kb && ta > tb);
+          if (gt == asc) {
+            t_key[i] = kb; t_tie[i] = tb;
+            t_key[i + j] = ka; t_tie[i + j] = ta;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = tid; i < T; i += kXlBlock) {
+      gkey[t0 + i] = t_key[i];
+      gtie[t0 + i] = t_tie[i];
+    }
+    __syncthreads();
+  }
+}
+
 template <int KIND>
 __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, int pb,
                        int sort_min, int64_t* s_off, double* s_w, double* s_min, double* s_den,
@@ -1209,33 +1246,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     }
     xl_sync();
     QF_STAMP(6);
-    // stages k (and strides j < T) inside LDS tiles of T items
-    auto tile_pass = [&](int kk, int j0) {
-      for (int t0 = 0; t0 < NP; t0 += T) {
-        for (int i = tid; i < T; i += kXlBlock) {
-          t_key[i] = w.skey[t0 + i];
-          t_tie[i] = w.stie[t0 + i];
-        }
-        __syncthreads();
-        for (int k2 = (kk ? kk : 2); k2 <= (kk ? kk : T); k2 <<= 1) {
-          for (int j = kk ? j0 : k2 >> 1; j > 0; j >>= 1) {
-            for (int t = tid; t < T / 2; t += kXlBlock) {
-              const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-              xl_cmpswap(t_key[i], t_tie[i], t_key[i + j], t_tie[i + j],
-                         ((t0 + i) & k2) == 0);
-            }
-            __syncthreads();
-          }
-        }
-        for (int i = tid; i < T; i += kXlBlock) {
-          w.skey[t0 + i] = t_key[i];
-          w.stie[t0 + i] = t_tie[i];
-        }
-        __syncthreads();
-      }
-      xl_sync();
-    };
-    tile_pass(0, 0);  // every stage k <= T
+    xl_tile_pass(w.skey, w.stie, t_key, t_tie, NP, T, 0, 0);  // every stage k <= T
     QF_STAMP(7);
     for (int kk = 2 * T; kk <= NP; kk <<= 1) {
       for (int j = kk >> 1; j >= T; j >>= 1) {
@@ -1247,7 +1258,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
         }
         xl_sync();
       }
-      tile_pass(kk, T >> 1);
+      xl_tile_pass(w.skey, w.stie, t_key, t_tie, NP, T, kk, T >> 1);
     }
     QF_STAMP(8);
     for (int i = tid; i < (int)U; i += kXlBlock) {
