@@ -386,8 +386,10 @@ __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (sx.wid * ro + j) * 64 + sx.lane;
     if (j < ro && i < sx.U) {
-      operm[i] = (uint16_t)(item[j] & kUMask);
-      io[i] = v[j];
+      // final outputs, not re-read by the device: non-temporal, so they do not
+      // evict the unsorted scores other workgroups are about to gather
+      __builtin_nontemporal_store((uint16_t)(item[j] & kUMask), &operm[i]);
+      __builtin_nontemporal_store(v[j], &io[i]);
     }
   }
 }
