@@ -154,7 +154,8 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
  * when max_entries > 10,240, with a workspace allocated and freed stream-ordered
  * (hipMallocAsync / hipFreeAsync on `stream`) — the one internal allocation.
  * max_entries must bound every query's entry count (larger queries report
- * QF_QSTATUS_TOOBIG).
+ * QF_QSTATUS_TOOBIG).  n_retrievers <= 32; with more than 16 every query takes
+ * the workspace kernel (its retriever masks are 32-bit, the LDS join's 16-bit).
  *
  * Inputs (device): list_off[Q*R+1] (int64), docid[E] (uint32, interned
  * docnos, 0xFFFFFFFF reserved), score[E] (score_kind), rank[E] (nullable

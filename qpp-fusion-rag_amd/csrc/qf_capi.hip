@@ -30,7 +30,7 @@ int check(hipError_t e, const char* what) {
   return QF_OK;
 }
 
-constexpr int kMaxR = 16;
+constexpr int kMaxR = 32;  // qf_fuse: > 16 runs take the workspace kernel
 }  // namespace
 
 extern "C" {
@@ -231,7 +231,7 @@ int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters
                        int32_t n_runs, const int32_t* run_to_booster, double* w_out,
                        void* stream) {
   if (n_queries < 0 || n_boosters <= 0 || n_boosters > qf::kMaxBoosters || n_runs <= 0 ||
-      n_runs > kMaxR || !run_to_booster)
+      n_runs > qf::kMaxBoosters || !run_to_booster)
     return fail(QF_EINVAL, "qf_learned_weights: bad sizes");
   qf::LearnedWeightParams p{};
   for (int r = 0; r < n_runs; ++r) {

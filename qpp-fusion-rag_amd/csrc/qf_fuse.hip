@@ -30,7 +30,8 @@
 
 namespace qf {
 
-constexpr int kRMax = 16;
+constexpr int kRMax = 16;    // runs per query in the LDS join (u16 retriever masks)
+constexpr int kRMaxXl = 32;  // in the workspace kernel (u32 masks)
 constexpr int kNMethods = 9;  // method bits QF_COMBSUM .. QF_WRRF_MUL
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
@@ -1280,8 +1281,8 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
                                                                 unsigned char* ws, int64_t ws_each,
                                                                 int nmax, int tb, int pb,
                                                                 int sort_min) {
-  __shared__ int64_t s_off[kRMax + 1];
-  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax], s_rden[kRMax];
+  __shared__ int64_t s_off[kRMaxXl + 1];
+  __shared__ double s_w[kRMaxXl], s_min[kRMaxXl], s_den[kRMaxXl], s_rden[kRMaxXl];
   __shared__ uint32_t s_wsum[kXlBlock / 64];
   __shared__ int s_status, s_n;
   __shared__ int64_t s_list[kXlBlock];
@@ -1345,8 +1346,8 @@ static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st, int
 // Queries above the LDS join (QF_QSTATUS_TOOBIG after it): the workspace join,
 // which sorts only the unions the LDS sorts cannot hold (U > sort_min) and
 // leaves the rest, unsorted with their U, to the sort kernels launched after it.
-static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int sort_min,
-                            hipStream_t st, void** ws_out) {
+static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int nmin,
+                            int sort_min, hipStream_t st, void** ws_out) {
   int tb = 1, pb = 0;
   while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
   while ((1 << pb) < max_entries) ++pb;
@@ -1360,29 +1361,36 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
   unsigned char* ws = (unsigned char*)*ws_out;
   if (kind == 1)
     hipLaunchKernelGGL((join_sort_xl_kernel<1>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
-                       JoinXL::kNMax, ws, each, nmax, tb, pb, sort_min);
+                       nmin, ws, each, nmax, tb, pb, sort_min);
   else
     hipLaunchKernelGGL((join_sort_xl_kernel<0>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
-                       JoinXL::kNMax, ws, each, nmax, tb, pb, sort_min);
+                       nmin, ws, each, nmax, tb, pb, sort_min);
   return hipGetLastError();
 }
 
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
-  if (max_entries <= JoinS::kNMax) {
-    launch_join<JoinS>(p, kind, st);
-    launch_sort<SortS>(p, 0, st);
-    return hipGetLastError();
-  }
-  if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
-  else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
-  else launch_join<JoinXL>(p, kind, st);
   void* ws = nullptr;
   hipError_t e = hipSuccess;
-  if (max_entries > JoinXL::kNMax) e = launch_xl(p, kind, max_entries, SortXL::kUMax, st, &ws);
+  if (p.R > kRMax) {
+    // more runs than the LDS join's masks hold: every query takes the workspace join
+    e = launch_xl(p, kind, max_entries < 1 ? 1 : max_entries, -1, SortXL::kUMax, st, &ws);
+  } else if (max_entries <= JoinS::kNMax) {
+    launch_join<JoinS>(p, kind, st);
+  } else {
+    if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
+    else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
+    else launch_join<JoinXL>(p, kind, st);
+    if (max_entries > JoinXL::kNMax)
+      e = launch_xl(p, kind, max_entries, JoinXL::kNMax, SortXL::kUMax, st, &ws);
+  }
   if (e == hipSuccess) {
-    launch_sort<SortM>(p, 0, st);
-    launch_sort_large<SortL>(p, SortM::kUMax + 1, st, 1);  // the queries SortM left
-    if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
+    if (max_entries <= SortS::kUMax) {
+      launch_sort<SortS>(p, 0, st);
+    } else {
+      launch_sort<SortM>(p, 0, st);
+      launch_sort_large<SortL>(p, SortM::kUMax + 1, st, 1);  // the queries SortM left
+      if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
+    }
     e = hipGetLastError();
   }
   if (ws) {

@@ -368,3 +368,47 @@ def test_workspace_path_learned_ties_by_docid(gpu, K):
     perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
     np.testing.assert_array_equal(perm, want)
     assert out.fused.cpu().numpy()[0][:n].tobytes() == unsorted[want].tobytes()
+
+
+@pytest.mark.parametrize("R,K", [(17, 300), (32, 40), (20, 700)])
+def test_more_than_16_runs_take_the_workspace_join(gpu, R, K):
+    """More runs than the LDS join's 16-bit retriever masks: every query goes through
+    the workspace join (32-bit masks), then the LDS sorts.  Every method bit-exact."""
+    from qppfuse import engine
+    rng = np.random.default_rng(R * 1000 + K)
+    sizes = [K, 0, K // 3, 1, K]
+    lists, ranks = [], []
+    for k0 in sizes:
+        pool = rng.choice(1 << 30, size=max(1, 3 * k0), replace=False).astype(np.uint32)
+        for r in range(R):
+            k = k0 if r % 5 else k0 // 2  # ragged
+            docs = rng.choice(pool, size=k, replace=False)
+            lists.append((docs, np.sort(rng.integers(0, 2000, k))[::-1] / 1e6))
+            ranks.append(np.arange(1, k + 1, dtype=np.int32))
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    n_max = int(np.max(off[R::R] - off[0:-1:R]))
+    rank = np.concatenate(ranks)
+    w = rng.uniform(0.05, 1.0, len(sizes) * R)
+    out = engine.fuse(doff, ddoc, dsc, R, ALL, rrf_k=60, weights=torch.from_numpy(w).to(gpu),
+                      rank=torch.from_numpy(rank).to(gpu), max_entries=n_max)
+    uc = out.union_count.cpu().numpy()
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fz = out.fused.cpu().numpy()
+    for m, name in enumerate(ALL):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
+                                                   rank=rank)
+        np.testing.assert_array_equal(uc, o_uc)
+        for q in range(len(sizes)):
+            b, n = off[q * R], uc[q]
+            np.testing.assert_array_equal(ud[b:b + n], o_ud[b:b + n])
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=f"{name} q{q}")
+            assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
+def test_more_than_32_runs_are_rejected(gpu):
+    from qppfuse import engine
+    R = 33
+    off, doc, sc, doff, ddoc, dsc = _csr([([r + 1], [1.0]) for r in range(R)], gpu)
+    with pytest.raises(ValueError, match="n_retrievers"):  # QF_EINVAL
+        engine.fuse(doff, ddoc, dsc, R, ["combsum"], max_entries=R)
