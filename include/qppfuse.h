@@ -151,7 +151,7 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
  * per (query, method): stable LDS radix sort by fused score, in place).
  * Queries of 10,241 .. qf_max_entries_per_query() (65,535) entries take a third
  * kernel (the same join in a global workspace + a bitonic sort), launched only
- * when max_entries > 10,240, with a workspace allocated and freed stream-ordered
+ * when max_entries > 10,240 (or n_retrievers > 16), with a workspace allocated and freed stream-ordered
  * (hipMallocAsync / hipFreeAsync on `stream`) — the one internal allocation.
  * max_entries must bound every query's entry count (larger queries report
  * QF_QSTATUS_TOOBIG).  n_retrievers <= 32; with more than 16 every query takes
