@@ -412,3 +412,41 @@ def test_more_than_32_runs_are_rejected(gpu):
     off, doc, sc, doff, ddoc, dsc = _csr([([r + 1], [1.0]) for r in range(R)], gpu)
     with pytest.raises(ValueError, match="n_retrievers"):  # QF_EINVAL
         engine.fuse(doff, ddoc, dsc, R, ["combsum"], max_entries=R)
+
+
+def test_api_with_18_rankers_matches_port(gpu):
+    """The reference API with more rankers than the LDS join holds (18): every method
+    through qppfuse.fusion, equal to the row-by-row port (weighted: the reference's
+    loops; unweighted: ranx semantics)."""
+    import pandas as pd
+    fusion = _api()
+    rng = np.random.default_rng(18)
+    rankers = [f"R{i:02d}" for i in range(18)]
+    frames, qpp = {}, {}
+    for r in rankers:
+        rows = []
+        for q in range(6):
+            k = int(rng.integers(0, 40))
+            docs = rng.choice(120, size=k, replace=False)
+            sc = np.sort(rng.integers(0, 10**6, k))[::-1] / 1e6
+            rows += [(f"test{q}", f"doc{d}", i + 1, s) for i, (d, s) in enumerate(zip(docs, sc))]
+        df = pd.DataFrame(rows, columns=["qid", "docno", "rank", "score"])
+        df.insert(1, "iter", "Q0")
+        df["runid"] = r
+        frames[r] = df
+    for q in range(6):
+        qpp[f"test{q}"] = {r: list(rng.uniform(0, 1, 13)) for r in rankers}
+    for name, fn in [("wcombsum", fusion.weighted_combsum), ("wcombmnz", fusion.weighted_combmnz)]:
+        got = fn(frames, qpp, 5)
+        want = ref_port.weighted_fusion(frames, qpp, 5, name)
+        for q in want:
+            assert got[q] == want[q], (name, q)
+    got = fusion.weighted_rrf(frames, qpp, -1, k=60)
+    want = ref_port.weighted_fusion(frames, qpp, -1, "wrrf", 60)
+    for q in want:
+        assert got[q] == want[q], ("wrrf", q)
+    for method in ["combsum", "combmnz", "rrf"]:
+        got = getattr(fusion, method)(frames)
+        want = ref_port.ranx_fusion(frames, method, 60)
+        for q in want:
+            assert got[q] == want[q], (method, q)
