@@ -341,7 +341,7 @@ struct qfio_runset {
   std::vector<int32_t> micro;
   std::vector<int64_t> rank;
   bool micro_ok = true;
-  bool rank_is_position = true, canonical = true;
+  bool rank_is_position = true, canonical = true, has_dups = false;
   // per-file rows in file order (for DataFrames): codes and values
   std::vector<int64_t> file_off;  // [n_files + 1]
   std::vector<uint32_t> row_qid, row_docid, row_iter, row_tag;
@@ -465,17 +465,34 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
     }
   // list properties the device path keys on (qppfuse/runset.py _analyse): the
   // rank column is position + 1; every list is score-descending with rising ranks
-  int not_pos = 0, not_canon = 0;
-#pragma omp parallel for schedule(static) reduction(+ : not_pos, not_canon)
-  for (int64_t l = 0; l < Q * R; ++l) {
-    const int64_t a = rs->list_off[l], b = rs->list_off[l + 1];
-    for (int64_t i = a; i < b; ++i) {
-      not_pos += rs->rank[i] != i - a + 1;
-      if (i > a) not_canon += !(rs->score[i] <= rs->score[i - 1] && rs->rank[i] > rs->rank[i - 1]);
+  // and whether a docno repeats inside one list (open addressing per list)
+  int not_pos = 0, not_canon = 0, dups = 0;
+#pragma omp parallel reduction(+ : not_pos, not_canon, dups)
+  {
+    std::vector<uint32_t> table;
+#pragma omp for schedule(static)
+    for (int64_t l = 0; l < Q * R; ++l) {
+      const int64_t a = rs->list_off[l], b = rs->list_off[l + 1];
+      for (int64_t i = a; i < b; ++i) {
+        not_pos += rs->rank[i] != i - a + 1;
+        if (i > a) not_canon += !(rs->score[i] <= rs->score[i - 1] && rs->rank[i] > rs->rank[i - 1]);
+      }
+      if (b - a < 2) continue;
+      size_t ts = 4;
+      while (ts < 2 * (size_t)(b - a)) ts <<= 1;
+      table.assign(ts, 0xFFFFFFFFu);
+      for (int64_t i = a; i < b; ++i) {
+        const uint32_t d = rs->docid[i];
+        size_t h = (size_t)((d * 0x9E3779B1u) & (uint32_t)(ts - 1));
+        while (table[h] != 0xFFFFFFFFu && table[h] != d) h = (h + 1) & (ts - 1);
+        if (table[h] == d) { ++dups; break; }
+        table[h] = d;
+      }
     }
   }
   rs->rank_is_position = not_pos == 0;
   rs->canonical = not_canon == 0;
+  rs->has_dups = dups != 0;
   tm.mark("csr");
   *out = rs;
   return QFIO_OK;
@@ -492,7 +509,8 @@ void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes /* [8] */) {
   sizes[2] = (int64_t)rs->docid.size();
   sizes[3] = qb;
   sizes[4] = db;
-  sizes[5] = (rs->micro_ok ? 1 : 0) | (rs->rank_is_position ? 2 : 0) | (rs->canonical ? 4 : 0);
+  sizes[5] = (rs->micro_ok ? 1 : 0) | (rs->rank_is_position ? 2 : 0) | (rs->canonical ? 4 : 0) |
+             (rs->has_dups ? 8 : 0);
   sizes[6] = (int64_t)rs->iters.size() | ((int64_t)rs->tags.size() << 32);
   sizes[7] = ib | (tb << 32);
 }
@@ -558,7 +576,10 @@ void qfio_runset_free(qfio_runset* rs) { delete rs; }
 // Python's f"{x:.6f}".
 static inline size_t fmt6(double x, char* out) {
   if (!(std::fabs(x) < 8589934592.0)) {  // 2^33, and inf / nan
-    if (std::isnan(x)) return (size_t)snprintf(out, 48, "%snan", std::signbit(x) ? "-" : "");
+    if (std::isnan(x)) {  // Python formats every NaN as "nan", whatever its sign bit
+      memcpy(out, "nan", 3);
+      return 3;
+    }
     return (size_t)snprintf(out, 400, "%.6f", x);
   }
   // m = round-half-even(x * 1e6) on the exact binary value (as qf_common.h round6)
@@ -615,14 +636,10 @@ int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const 
       const std::string_view qid(qid_chars + qid_off[q], (size_t)(qid_off[q + 1] - qid_off[q]));
       for (int32_t k = 0; k < n; ++k) {
         const uint32_t d = union_docid[base + perm[base + k]];
-        size_t o = 0;
-        memcpy(line + o, qid.data(), qid.size());
-        o += qid.size();
-        memcpy(line + o, " Q0 ", 4);
-        o += 4;
-        s.append(line, o);
+        s.append(qid.data(), qid.size());
+        s.append(" Q0 ", 4);
         s.append(docno_chars + docno_off[d], (size_t)(docno_off[d + 1] - docno_off[d]));
-        o = 0;
+        size_t o = 0;
         line[o++] = ' ';
         o += (size_t)snprintf(line + o, 32, "%d", k + 1);
         line[o++] = ' ';

@@ -130,6 +130,7 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
                 docid=docid, score=score, rank=rank, micro=micro)
     rs.rank_is_position = bool(flags & 2)
     rs.canonical = bool(flags & 4)
+    rs.has_dups = bool(flags & 8)
     rs._strtab = {"qid": (qo, qc.tobytes()), "docno": (do, dc.tobytes())}
 
     def column(strings, codes):
@@ -163,9 +164,9 @@ def string_table(rs, which: str) -> Tuple[np.ndarray, bytes]:
 
 def write_run(path: str, order: np.ndarray, qbase: np.ndarray, counts: np.ndarray,
               union_docid: np.ndarray, perm: np.ndarray, fused: np.ndarray, rs, tag: str,
-              n_threads: int = 0) -> None:
+              n_threads: int = 0, qid_table=None) -> None:
     """One fused run -> TREC text (queries in `order`, documents as ranked)."""
-    qo, qc = string_table(rs, "qid")
+    qo, qc = string_table(rs, "qid") if qid_table is None else qid_table
     do, dc = string_table(rs, "docno")
     order = np.ascontiguousarray(order, np.int64)
     qbase = np.ascontiguousarray(qbase, np.int64)

@@ -30,7 +30,7 @@ from . import engine
 from .config import ConfigError, config
 from .config import get_qpp_index as _cfg_qpp_index
 from .data_utils import load_qpp_scores as _load_qpp
-from .runset import RunSet, pack_frames, reorder
+from .runset import RunSet, dedupe_keep_last, expand_duplicates, pack_frames, reorder
 
 __all__ = ["load_runs", "load_qpp_scores", "get_qpp_weight", "get_qpp_index", "combsum",
            "combmnz", "rrf", "weighted_combsum", "weighted_combmnz", "weighted_rrf",
@@ -149,25 +149,77 @@ class FusedRun(Mapping):
 
 # ---------------------------------------------------------------- packing ----
 
-_PACK_CACHE: Dict[tuple, RunSet] = {}
+_PACK_CACHE: Dict[tuple, tuple] = {}  # frames' identity -> (content fingerprint, RunSet)
+
+
+def _column_digest(col) -> int:
+    """xxh3 of one column's contents: the values of a numeric column, the object
+    pointers of an object column (str objects are immutable, so an unchanged
+    pointer is an unchanged value; any assignment into the column changes it)."""
+    import ctypes
+    import xxhash
+    a = np.ascontiguousarray(col.to_numpy())
+    if a.dtype == object:
+        if len(a) == 0:
+            return 0
+        ptrs = (ctypes.c_uint64 * len(a)).from_address(a.ctypes.data)
+        h = xxhash.xxh3_64_intdigest(memoryview(ptrs).cast("B"))
+        del ptrs
+        return h
+    return xxhash.xxh3_64_intdigest(memoryview(a).cast("B"))
+
+
+def _fingerprint(runs: Dict[str, pd.DataFrame]) -> tuple:
+    """Content of every column the fusions read (qid, docno, rank, score)."""
+    return tuple((name, len(df), tuple(_column_digest(df[c]) for c in ("qid", "docno", "rank",
+                                                                       "score")))
+                 for name, df in runs.items())
+
+
+def _key(runs: Dict[str, pd.DataFrame]) -> tuple:
+    return tuple((name, id(df)) for name, df in runs.items())
 
 
 def _remember(runs: Dict[str, pd.DataFrame], rs: RunSet) -> None:
-    key = tuple((name, id(df), len(df)) for name, df in runs.items())
+    key = _key(runs)
     _PACK_CACHE.clear()
-    _PACK_CACHE[key] = rs
+    _PACK_CACHE[key] = (_fingerprint(runs), rs)
     for df in runs.values():
         weakref.finalize(df, _PACK_CACHE.pop, key, None)
 
 
 def _pack(runs: Dict[str, pd.DataFrame]) -> RunSet:
-    """Pack once per runs dict (cached on the frames' identity while they live)."""
-    key = tuple((name, id(df), len(df)) for name, df in runs.items())
-    rs = _PACK_CACHE.get(key)
-    if rs is None:
-        rs = pack_frames(runs)
-        _remember(runs, rs)
+    """Pack once per runs dict: cached while the frames live AND their contents are
+    unchanged (a frame edited in place is packed again — the reference is stateless)."""
+    hit = _PACK_CACHE.get(_key(runs))
+    if hit is not None and hit[0] == _fingerprint(runs):
+        return hit[1]
+    rs = pack_frames(runs)
+    _remember(runs, rs)
     return rs
+
+
+def _derived(rs: RunSet, what: str) -> RunSet:
+    """The run set in the order / shape one method family reads (cached on rs)."""
+    cache = rs.__dict__.setdefault("_derived_sets", {})
+    if what not in cache:
+        if what == "ranx":        # {docno: score} per list, score-sorted (src/fusion.py:459-465)
+            d = dedupe_keep_last(rs)
+            cache[what] = d if d.canonical else reorder(d, "score")
+        elif what == "rows":      # every row, file order (src/fusion.py:272-277)
+            cache[what] = expand_duplicates(rs)
+        elif what == "rank":      # every row, rank order (src/fusion.py:372)
+            cache[what] = expand_duplicates(rs if rs.canonical else reorder(rs, "rank"))
+        else:
+            raise ValueError(what)
+    return cache[what]
+
+
+def _expand_weights(weights: Optional[np.ndarray], rs: RunSet, rv: RunSet):
+    if weights is None or rv.base_ranker is None or rv is rs:
+        return weights
+    return np.ascontiguousarray(weights.reshape(rs.n_queries, rs.n_rankers)[:, rv.base_ranker]
+                                .ravel())
 
 
 def _weights(rs: RunSet, qpp_data, qpp_index: int) -> np.ndarray:
@@ -220,20 +272,23 @@ def fuse_many(runs: Dict[str, pd.DataFrame], methods: Sequence[str], qpp_data=No
     rs = _pack(runs)
     weighted = [m for m in methods if m in WEIGHTED]
     weights = _weights(rs, qpp_data, qpp_index) if weighted else None
-    if rs.canonical:
+    if rs.canonical and not rs.has_dups:
         return _launch(rs, methods, k, weights)
-    # Lists whose file order is not score order: each family gets the order the
-    # reference iterates in (ranx: score-sorted; W-CombSUM/MNZ: file rows;
-    # W-RRF: rank-sorted, src/fusion.py:372).
+    # Lists whose file order is not score order, or with a docno repeated inside
+    # one list: each family gets the lists the reference iterates (ranx:
+    # {docno: score}, last row wins, score-sorted; W-CombSUM/MNZ: every row in
+    # file order; W-RRF: every row in rank order, src/fusion.py:372).
     res = {}
     un = [m for m in methods if m in UNWEIGHTED]
     if un:
-        res.update(_launch(reorder(rs, "score"), un, k, None))
+        res.update(_launch(_derived(rs, "ranx"), un, k, None))
     ws = [m for m in methods if m in ("wcombsum", "wcombmnz")]
     if ws:
-        res.update(_launch(rs, ws, k, weights))
+        rv = _derived(rs, "rows")
+        res.update(_launch(rv, ws, k, _expand_weights(weights, rs, rv)))
     if "wrrf" in methods:
-        res.update(_launch(reorder(rs, "rank"), ["wrrf"], k, weights))
+        rv = _derived(rs, "rank")
+        res.update(_launch(rv, ["wrrf"], k, _expand_weights(weights, rs, rv)))
     return {m: res[m] for m in methods}
 
 
@@ -305,9 +360,13 @@ def learned_fusion(runs: Dict[str, pd.DataFrame], qpp_data, model_path: str,
                 X[i, j * n_qpp:(j + 1) * n_qpp] = qd[retriever][:n_qpp]
     dev = engine.require_device()
     pred = engine.gbdt_predict(torch.from_numpy(X).to(dev), packed)
-    run_to_booster = [retrievers.index(r) if r in retrievers else -1 for r in rs.rankers]
+    # a docno repeated inside one list adds every row (the groupby sum,
+    # src/fusion.py:440-441): repeated rows go to virtual runs of their ranker
+    rv = _derived(rs, "rows")
+    names = [rs.rankers[b] for b in rv.base_ranker] if rv.base_ranker is not None else rs.rankers
+    run_to_booster = [retrievers.index(r) if r in retrievers else -1 for r in names]
     w = engine.learned_weights(pred, run_to_booster)
-    res = _launch(rs, ["learned"], config.fusion.rrf_k, w)
+    res = _launch(rv, ["learned"], config.fusion.rrf_k, w)
     fused = res["learned"]
     print(f"[fusion] Learned fusion done: {len(fused)} queries")
     return fused
@@ -325,11 +384,7 @@ def write_runfile(fused: Mapping, output_path: str, tag: str = "fusion") -> None
     straight from the kernel's ranked arrays; any other mapping as the
     reference does it."""
     if isinstance(fused, FusedRun) and fused._rs is not None:
-        from . import fastio
-        idx = fused._index
-        order = np.asarray([idx[q] for q in sorted(fused.keys(), key=qid_sort_key)], np.int64)
-        fastio.write_run(output_path, order, fused._qbase, fused._counts, fused._udoc,
-                         fused._perm, fused._fused, fused._rs, tag)
+        write_fused_native(fused, output_path, tag)
         print(f"Wrote fused run to {output_path}")
         return
     with open(output_path, "w") as fout:
@@ -338,6 +393,26 @@ def write_runfile(fused: Mapping, output_path: str, tag: str = "fusion") -> None
             fout.write("".join(f"{qid} Q0 {d} {i} {s:.6f} {tag}\n"
                                for i, (d, s) in enumerate(ranked, start=1)))
     print(f"Wrote fused run to {output_path}")
+
+
+def write_fused_native(fused: "FusedRun", output_path: str, tag: str, select=None,
+                       rename=None) -> None:
+    """write_runfile of a FusedRun, optionally of the queries `select(qid)` keeps,
+    written under `rename(qid)` (multicorpus: one corpus, bare qids)."""
+    from . import fastio
+    qids = [q for q in fused.keys() if select is None or select(q)]
+    names = {q: (rename(q) if rename else q) for q in qids}
+    idx = fused._index
+    order = np.asarray([idx[q] for q in sorted(qids, key=lambda q: qid_sort_key(names[q]))],
+                       np.int64)
+    qid_table = None
+    if rename is not None:
+        enc = [(rename(q) if (select is None or select(q)) else q).encode() for q in fused._qids]
+        off = np.zeros(len(enc) + 1, np.int64)
+        np.cumsum([len(e) for e in enc], out=off[1:])
+        qid_table = (off, b"".join(enc))
+    fastio.write_run(output_path, order, fused._qbase, fused._counts, fused._udoc,
+                     fused._perm, fused._fused, fused._rs, tag, qid_table=qid_table)
 
 
 def run_fusion(method: str, runs_dir: str, qpp_dir: Optional[str] = None, qpp_model: str = None,

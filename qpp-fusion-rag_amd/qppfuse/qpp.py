@@ -23,9 +23,12 @@ from typing import Any, Dict, List, Optional
 import numpy as np
 
 from . import _lib, engine, textfeat
+from .config import QPP_METHODS as JAVA_METHODS
 from .config import config
 
-QPP_METHODS = list(config.qpp.methods)
+# The names QPPBridge.java emits, in its output order (QPPBridge.java:148-188);
+# also the column order of the raw predictor kernel qf_qpp_raw.
+QPP_METHODS = list(JAVA_METHODS)
 
 
 @dataclass
@@ -125,6 +128,12 @@ def compute_qpp_for_res_file(res_path: str, output_path: Optional[str] = None,
     QPPBridge()
     raw = _device_qpp(lists, [texts.get(q, q) for q in qids])
     results = {q: raw[i].tolist() for i, q in enumerate(qids)}
+    # columns in config.qpp.methods order, absent names 0.0 (src/qpp.py:319-322)
+    names = list(config.qpp.methods)
+    if names != QPP_METHODS:
+        pos = {n: i for i, n in enumerate(QPP_METHODS)}
+        results = {q: [v[pos[m]] if m in pos else 0.0 for m in names]
+                   for q, v in results.items()}
     if normalize != "none" and results:
         results = _normalize_qpp(results, normalize)
     if output_path:
@@ -140,15 +149,23 @@ def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, Li
     minmax (min / max) or zscore (numpy's mean / population std, bit-exact)."""
     qids = list(results.keys())
     arr = np.asarray([results[q] for q in qids], dtype=np.float64).reshape(len(qids), -1)
-    if arr.shape[1] != _lib.QPP_COLS:
-        raise ValueError(f"expected {_lib.QPP_COLS} QPP columns, got {arr.shape[1]}")
+    n_cols = arr.shape[1]
+    if n_cols > config.qpp.n_methods:  # method_values[i] of the reference (src/qpp.py:347-350)
+        raise IndexError("list index out of range")
+    # the kernels normalise 13 independent columns per row: pad to a multiple
+    width = -(-max(n_cols, 1) // _lib.QPP_COLS) * _lib.QPP_COLS
+    arr = np.ascontiguousarray(np.pad(arr, ((0, 0), (0, width - n_cols)))
+                               .reshape(-1, _lib.QPP_COLS))
+    rows_per = width // _lib.QPP_COLS
     method = "minmax" if method == "minmax" else "zscore"  # src/qpp.py:357-359: else -> zscore
     import torch
     dev = engine.require_device()
     raw = torch.from_numpy(arr).to(dev)
-    off = torch.arange(len(qids) + 1, dtype=torch.int64, device=dev)  # every list present
-    stats = (engine.qpp_colminmax if method == "minmax" else engine.qpp_colmeanstd)(raw, off, 1)
-    norm = engine.qpp_normalize(raw, stats, off, 1, method, qpp_index=0, want_norm=True,
+    # every list present; the padded row pieces of one query are the "retrievers"
+    off = torch.arange(len(qids) * rows_per + 1, dtype=torch.int64, device=dev)
+    stats = (engine.qpp_colminmax if method == "minmax" else engine.qpp_colmeanstd)(
+        raw, off, rows_per)
+    norm = engine.qpp_normalize(raw, stats, off, rows_per, method, qpp_index=0, want_norm=True,
                                 want_micro=False, want_weights=False)["norm"]
-    vals = norm.cpu().numpy()
+    vals = norm.cpu().numpy().reshape(len(qids), width)[:, :n_cols]
     return {q: [float(v) for v in vals[i]] for i, q in enumerate(qids)}

@@ -29,6 +29,8 @@ class RunSet:
     micro: Optional[np.ndarray] = None   # int32 [E] when exact
     rank_is_position: bool = True        # rank == position + 1 in every list
     canonical: bool = True               # file order == score-desc order == rank order
+    has_dups: bool = False               # a docno repeats inside one list
+    base_ranker: Optional[np.ndarray] = None  # expand_duplicates: ranker of each virtual run
     _device: Dict[str, object] = field(default_factory=dict, repr=False)
 
     @property
@@ -127,16 +129,12 @@ def _analyse(rs: RunSet, key_s: np.ndarray) -> None:
     """Order / uniqueness properties the kernels rely on (include/qppfuse.h)."""
     E = rs.n_entries
     same = key_s[1:] == key_s[:-1] if E > 1 else np.zeros(0, bool)
-    # duplicates of a docno inside one list
+    # duplicates of a docno inside one list (handled by dedupe_keep_last /
+    # expand_duplicates, the reference's two behaviours)
     if E > 1:
         o = np.lexsort((rs.docid, key_s))
         dup = (key_s[o][1:] == key_s[o][:-1]) & (rs.docid[o][1:] == rs.docid[o][:-1])
-        if dup.any():
-            i = int(o[1:][dup][0])
-            q, r = divmod(int(key_s[i]), rs.n_rankers)
-            raise ValueError(
-                f"docno '{rs.docnos[rs.docid[i]]}' appears twice in run '{rs.rankers[r]}' for "
-                f"query '{rs.qids[q]}': duplicate docnos within one list are not supported")
+        rs.has_dups = bool(dup.any())
     score_ok = bool(np.all(rs.score[1:][same] <= rs.score[:-1][same])) if E > 1 else True
     rank_inc = bool(np.all(rs.rank[1:][same] > rs.rank[:-1][same])) if E > 1 else True
     pos = np.arange(E, dtype=np.int64) - np.repeat(rs.list_off[:-1], np.diff(rs.list_off))
@@ -156,9 +154,110 @@ def reorder(rs: RunSet, by: str) -> RunSet:
     else:
         raise ValueError(by)
     out = RunSet(qids=rs.qids, rankers=rs.rankers, docnos=rs.docnos, list_off=rs.list_off,
-                 docid=rs.docid[o], score=rs.score[o], rank=rs.rank[o])
+                 docid=rs.docid[o], score=rs.score[o], rank=rs.rank[o],
+                 base_ranker=rs.base_ranker)
+    _share_strings(rs, out)
     _analyse(out, lid[o])
     if by == "rank":
         # the kernel's order check is on scores; rank order is what W-RRF needs
         out.canonical = True
+    return out
+
+
+def _share_strings(src: RunSet, dst: RunSet) -> None:
+    tab = getattr(src, "_strtab", None)
+    if tab is not None:
+        dst._strtab = tab
+
+
+def _list_ids(rs: RunSet) -> np.ndarray:
+    return np.repeat(np.arange(len(rs.list_off) - 1), np.diff(rs.list_off))
+
+
+def _occurrence(lid: np.ndarray, docid: np.ndarray) -> np.ndarray:
+    """For every entry: how many earlier entries of its list hold the same docno."""
+    E = len(lid)
+    o = np.lexsort((np.arange(E), docid, lid))
+    same = np.zeros(E, bool)
+    if E > 1:
+        same[1:] = (lid[o][1:] == lid[o][:-1]) & (docid[o][1:] == docid[o][:-1])
+    # run-length position inside each group of equal (list, docno)
+    idx = np.arange(E)
+    start = np.where(same, 0, idx)
+    np.maximum.accumulate(start, out=start)
+    occ = np.empty(E, np.int64)
+    occ[o] = idx - start
+    return occ
+
+
+def dedupe_keep_last(rs: RunSet) -> RunSet:
+    """One entry per docno per list, at its FIRST position with its LAST score.
+
+    What the ranx methods see: _df_runs_to_ranx builds {qid: {docno: score}} row
+    by row (src/fusion.py:459-464), and a repeated dict key keeps its insertion
+    position while taking the new value.  The rank column keeps the first row's."""
+    if not rs.has_dups:
+        return rs
+    lid = _list_ids(rs)
+    E = rs.n_entries
+    occ = _occurrence(lid, rs.docid)
+    # entries grouped by (list, docno), positions ascending inside a group; the
+    # group's last entry's score is broadcast to the group
+    o = np.lexsort((np.arange(E), rs.docid, lid))
+    gid = np.zeros(E, np.int64)
+    if E > 1:
+        gid[1:] = np.cumsum(~((lid[o][1:] == lid[o][:-1]) & (rs.docid[o][1:] == rs.docid[o][:-1])))
+    last_idx = np.zeros(gid[-1] + 1 if E else 0, np.int64)
+    last_idx[gid] = o  # o is position-ascending inside a group: the last write wins
+    score = rs.score.copy()
+    score[o] = rs.score[last_idx[gid]]
+    keep = occ == 0
+    counts = np.bincount(lid[keep], minlength=len(rs.list_off) - 1)
+    list_off = np.zeros(len(rs.list_off), np.int64)
+    np.cumsum(counts, out=list_off[1:])
+    out = RunSet(qids=rs.qids, rankers=rs.rankers, docnos=rs.docnos, list_off=list_off,
+                 docid=rs.docid[keep], score=score[keep], rank=rs.rank[keep])
+    _share_strings(rs, out)
+    _analyse(out, lid[keep])
+    return out
+
+
+def expand_duplicates(rs: RunSet) -> RunSet:
+    """Every repeated row of a list moved to a virtual run right after its ranker.
+
+    What the weighted loops and learned fusion's groupby do with a docno that
+    repeats inside one list: every row adds its own contribution, rows in file
+    order (src/fusion.py:273-277, 321-324, 372-374, 440-441).  The k-th
+    occurrence (k >= 1) of a docno in ranker r goes to virtual run (r, k), placed
+    after (r, k-1): a document's contributions are then summed in retriever
+    order exactly as the reference adds its rows, and its first occurrence — in
+    run (r, 0) — still fixes the first-seen order.  Virtual runs take their
+    ranker's weight (base_ranker) and carry the file rank column."""
+    if not rs.has_dups:
+        return rs
+    R = rs.n_rankers
+    Q = rs.n_queries
+    lid = _list_ids(rs)
+    occ = _occurrence(lid, rs.docid)
+    q, r = np.divmod(lid, R)
+    kmax = np.zeros(R, np.int64)
+    np.maximum.at(kmax, r, occ)
+    first = np.zeros(R + 1, np.int64)  # virtual run index of (r, 0)
+    np.cumsum(kmax + 1, out=first[1:])
+    R2 = int(first[-1])
+    vr = first[r] + occ
+    key = q * R2 + vr
+    o = np.lexsort((np.arange(len(key)), key))
+    counts = np.bincount(key, minlength=Q * R2)
+    list_off = np.zeros(Q * R2 + 1, np.int64)
+    np.cumsum(counts, out=list_off[1:])
+    base = np.repeat(np.arange(R), kmax + 1)
+    names = [rs.rankers[b] if k == 0 else f"{rs.rankers[b]}#dup{k}"
+             for b, k in zip(base, np.concatenate([np.arange(k + 1) for k in kmax]))]
+    out = RunSet(qids=rs.qids, rankers=names, docnos=rs.docnos, list_off=list_off,
+                 docid=rs.docid[o], score=rs.score[o], rank=rs.rank[o],
+                 base_ranker=base if rs.base_ranker is None else rs.base_ranker[base])
+    _share_strings(rs, out)
+    _analyse(out, key[o])
+    out.rank_is_position = False  # positions inside a virtual run are not file ranks
     return out

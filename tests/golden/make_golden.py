@@ -278,6 +278,161 @@ def main():
                    "col11": [cols[q][2] for q in cols], "col12": [cols[q][3] for q in cols]}
         (OUT / f"qpp_textcols_{ds}.json").write_text(json.dumps(fixture))
     print("golden fixtures written to", OUT)
+    round2(mods)
+
+
+def beir_qids():
+    """Unique qids of the three BEIR test qrels, in file order (src/data_utils.py:175-197)."""
+    out = {}
+    for ds in ("hotpotqa", "nq", "scifact"):
+        seen = {}
+        with open(REF / "data" / ds / f"BEIR-{ds}" / "qrels" / "test.tsv") as fh:
+            next(fh)
+            for line in fh:
+                f = line.strip().split("\t")
+                if len(f) >= 3:
+                    seen.setdefault(f[0], None)
+        out[ds] = list(seen)
+    return out
+
+
+def round2(mods):
+    """Fixtures added in round 2 (separate file, so the round-1 vectors stay byte-stable):
+      dup_cases   docnos repeated inside one list: the weighted loops (every row
+                  counts, src/fusion.py:273-277,321-324,372-374), write_runfile bytes,
+                  and _df_runs_to_ranx's {qid: {docno: score}} (last row wins at the
+                  first row's position, src/fusion.py:459-464) through a recording
+                  stand-in for ranx.Run (ranx is not installed; Run only stores the dict)
+      config      the reference's outputs with its config singleton set to
+                  rrf_k=20, default_index=7, default_method="WIG" (what a user's
+                  edited defaults.yaml gives): weighted_* and run_fusion with no
+                  explicit qpp_index / k / qpp_model
+      qids        write_runfile's qid order for the namespaced ("<corpus>:<qid>")
+                  real BEIR test qids of HotpotQA + NQ + SciFact, and the TypeError
+                  of the bare mixed qids (src/fusion.py:487)
+    """
+    import gzip
+    fu, cfgmod = mods["fusion"], mods["config"]
+    rng = random.Random(20251213)
+    pool = [f"doc{i}" for i in range(40)]
+    rankers = ["BGE", "BM25", "Splade"]
+
+    class RecRun(dict):
+        def __init__(self, d, name=None):
+            super().__init__(d)
+            self.name = name
+    fu.Run = RecRun
+
+    def dup_runs(n_q, k_range, p_dup, unsorted=False, rank_shift=False):
+        qids, runs = make_case(rng, n_q=n_q, rankers=rankers, k_range=k_range, pool=pool,
+                               normed=True, unsorted=unsorted, rank_shift=rank_shift)
+        for r in rankers:
+            rows = runs[r]
+            extra = []
+            used = {(row[0], row[2]) for row in rows}
+            for row in rows:
+                if rng.random() < p_dup:
+                    for _ in range(rng.choice((1, 1, 2))):
+                        # a rank no other row of the list holds: W-RRF's
+                        # sort_values("rank") is numpy's unstable quicksort, whose
+                        # order among equal ranks is not reproducible (DESIGN.md)
+                        rk = rng.randint(1, 40)
+                        while (row[0], rk) in used:
+                            rk = rng.randint(1, 40)
+                        used.add((row[0], rk))
+                        extra.append([row[0], row[1], rk, float(f"{rng.random():.6f}")])
+            for e in extra:  # inserted at random places of the same query's rows
+                idx = [i for i, x in enumerate(rows) if x[0] == e[0]]
+                rows.insert(rng.choice(idx) + rng.randint(0, 1), e)
+        return qids, runs
+
+    dup_cases = []
+    for name, spec in [("dup_basic", dict(n_q=5, k_range=(5, 12), p_dup=0.25)),
+                       ("dup_unsorted", dict(n_q=4, k_range=(5, 10), p_dup=0.3, unsorted=True,
+                                             rank_shift=True)),
+                       ("dup_heavy", dict(n_q=3, k_range=(8, 15), p_dup=0.6))]:
+        qids, runs = dup_runs(**spec)
+        qpp = make_qpp(rng, qids, rankers)
+        frames = to_frames(runs)
+        case = {"name": name, "rankers": rankers, "runs": runs, "qpp": qpp, "qpp_index": 5,
+                "rrf_k": 60, "outputs": {}, "runfiles": {}}
+        with redirect_stdout(io.StringIO()):
+            outs = {"wcombsum": fu.weighted_combsum(frames, qpp, 5),
+                    "wcombmnz": fu.weighted_combmnz(frames, qpp, 5),
+                    "wrrf": fu.weighted_rrf(frames, qpp, 5, k=60)}
+            for m, fused in outs.items():
+                case["outputs"][m] = enc_fused(fused)
+                with tempfile.NamedTemporaryFile("r", suffix=".res", delete=False) as tf:
+                    path = tf.name
+                fu.write_runfile(fused, path, f"{m}-tag")
+                case["runfiles"][m] = Path(path).read_text()
+                os.unlink(path)
+        rx = fu._df_runs_to_ranx(frames)
+        case["ranx_input"] = {r: {q: [[d, hx(v)] for d, v in dq.items()] for q, dq in run.items()}
+                              for r, run in rx.items()}
+        dup_cases.append(case)
+
+    # config: the singleton's values as an edited defaults.yaml would set them
+    c = cfgmod.config._data
+    saved = (c.fusion.rrf_k, c.qpp.default_index, c.qpp.default_method)
+    c.fusion.rrf_k, c.qpp.default_index, c.qpp.default_method = 20, 7, "WIG"
+    qids, runs = make_case(rng, n_q=5, rankers=rankers, k_range=(6, 12), pool=pool, normed=True)
+    qpp = make_qpp(rng, qids, rankers)
+    frames = to_frames(runs)
+    conf = {"yaml": {"fusion": {"rrf_k": 20}, "qpp": {"default_index": 7, "default_method": "WIG"}},
+            "runs": runs, "rankers": rankers, "qpp": qpp, "outputs": {}}
+    tmp = Path(tempfile.mkdtemp(prefix="qppfuse_cfg_"))
+    (tmp / "runs").mkdir()
+    (tmp / "qpp").mkdir()
+    for r, rows in runs.items():
+        with open(tmp / "runs" / f"{r}.norm.res", "w") as fh:
+            for qid, d, rk, sc in rows:
+                fh.write(f"{qid} Q0 {d} {rk} {sc:.6f} {r}\n")
+        with open(tmp / "qpp" / f"{r}.res.mmnorm.qpp", "w") as fh:
+            for qid, vals in qpp.items():
+                fh.write(qid + "\t" + "\t".join(f"{v:.6f}" for v in vals[r]) + "\n")
+    with redirect_stdout(io.StringIO()):
+        conf["outputs"]["wcombsum"] = enc_fused(fu.weighted_combsum(frames, qpp))
+        conf["outputs"]["wrrf"] = enc_fused(fu.weighted_rrf(frames, qpp))
+        fu.run_fusion("wrrf", str(tmp / "runs"), str(tmp / "qpp"), None, None,
+                      str(tmp / "wrrf.res"), None)
+    conf["run_fusion_wrrf"] = (tmp / "wrrf.res").read_text()
+    conf["qpp_files"] = {f.name: f.read_text() for f in sorted((tmp / "qpp").iterdir())}
+    shutil.rmtree(tmp)
+    c.fusion.rrf_k, c.qpp.default_index, c.qpp.default_method = saved
+
+    # namespaced multi-corpus qids
+    bq = beir_qids()
+    (OUT / "beir_qids.json.gz").write_bytes(gzip.compress(json.dumps(bq).encode(), mtime=0))
+    ns = [f"{ds}:{q}" for ds in ("nq", "scifact", "hotpotqa") for q in bq[ds]]
+    with tempfile.NamedTemporaryFile("r", suffix=".res", delete=False) as tf:
+        path = tf.name
+    with redirect_stdout(io.StringIO()):
+        fu.write_runfile({q: [("d", 1.0)] for q in ns}, path, "t")
+    order = [line.split(" ", 1)[0] for line in Path(path).read_text().splitlines()]
+    os.unlink(path)
+    qids_fx = {"namespaced_input": "nq, scifact, hotpotqa blocks in qrels order",
+               "namespaced_order": [ns.index(q) for q in order]}
+    try:
+        with redirect_stdout(io.StringIO()):
+            fu.write_runfile({q: [("d", 1.0)] for ds in ("nq", "scifact", "hotpotqa")
+                              for q in bq[ds]}, os.devnull, "t")
+        qids_fx["bare_error"] = None
+    except Exception as exc:  # noqa: BLE001
+        qids_fx["bare_error"] = [type(exc).__name__, str(exc)]
+    per = {}
+    for ds in ("nq", "scifact", "hotpotqa"):
+        with tempfile.NamedTemporaryFile("r", suffix=".res", delete=False) as tf:
+            path = tf.name
+        with redirect_stdout(io.StringIO()):
+            fu.write_runfile({q: [("d", 1.0)] for q in bq[ds]}, path, "t")
+        got = [line.split(" ", 1)[0] for line in Path(path).read_text().splitlines()]
+        os.unlink(path)
+        per[ds] = [bq[ds].index(q) for q in got]
+    qids_fx["per_corpus_order"] = per
+    (OUT / "reference_round2.json").write_text(json.dumps(
+        {"dup_cases": dup_cases, "config": conf, "qids": qids_fx}, indent=1, sort_keys=True))
+    print("round-2 fixtures written to", OUT)
 
 
 if __name__ == "__main__":
