@@ -15,7 +15,12 @@ Queries shard across ranks (weak scaling); the only collective is the 1 KB
 all-reduce of step 3.  Rank 0 prints ONE JSON line.
 
 python bench.py [--gpus N] [--steps K] [--warmup W]
-(for N > 1 launched by torch.distributed.run, one process per GPU)
+For N > 1 one process per GPU: either the driver launches this script under
+torch.distributed.run (WORLD_SIZE set), or — run plainly as
+`python bench.py --gpus N` — this process, before it makes any GPU call,
+starts `torch.distributed.run --nproc-per-node N` on itself as a child and exits
+with its code.  For N > 1 the timed step includes the north star's collective:
+every rank's fused top-k (default 100) gathered to rank 0 over RCCL.
 """
 from __future__ import annotations
 
@@ -66,9 +71,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
-    ap.add_argument("--gather-topk", type=int, default=0,
-                    help="per step, gather every rank's fused top-k to rank 0 (0 = fused "
-                         "lists stay on their rank, as each rank writes its own qid range)")
+    ap.add_argument("--gather-topk", type=int, default=None,
+                    help="per step, gather every rank's fused top-k to rank 0 over RCCL "
+                         "(default: 100 when N > 1, else 0; 0 = fused lists stay on their "
+                         "rank, as each rank writes its own qid range)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="put every rank on GPU 0 (use with --dist-backend gloo)")
     ap.add_argument("--steps", type=int, default=20)
@@ -79,8 +85,11 @@ def parse():
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--qpp-top-k", type=int, default=100)
     ap.add_argument("--qpp-index", type=int, default=None)
-    ap.add_argument("--cpu-sample", type=int, default=40,
-                    help="queries timed through the Python port of the reference (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="queries per CPU-baseline process timed through the Python port of "
+                         "the reference (0 = skip; default: the workload's, ~10 s each)")
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="processes the CPU baseline runs on (default min(16, cpu_count))")
     ap.add_argument("--native-sample", type=int, default=400,
                     help="queries timed through the C oracle (0 = skip)")
     ap.add_argument("--check", type=int, default=8, help="queries checked bit-exact vs oracle")
@@ -98,8 +107,30 @@ def parse():
     return a
 
 
+def launch_ranks(args, script=None, argv=None) -> int:
+    """`--gpus N` without a launcher: run torch.distributed.run on this script as a
+    child process (this process has made no GPU call) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", str(script or Path(__file__).resolve())] + \
+        list(sys.argv[1:] if argv is None else argv)
+    env = dict(os.environ, QPPFUSE_BENCH_LAUNCHED="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    progress(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus} (or without a "
+                         f"launcher: python bench.py --gpus {args.gpus})")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.rehearse_one_gpu:  # N-rank rehearsal on a 1-GPU box (gloo): all ranks on GPU 0
@@ -112,6 +143,20 @@ def setup_dist(args):
         else:
             dist.init_process_group(args.dist_backend)
     return world, rank, torch.device("cuda", local)
+
+
+def c4_queries():
+    """C4's 11,157 namespaced qids in batch order and their query texts."""
+    import gzip
+    from qppfuse import multicorpus
+    g = ROOT / "tests" / "golden"
+    bq = json.loads(gzip.decompress((g / "beir_qids.json.gz").read_bytes()))
+    text = {}
+    for ds in ("nq", "scifact"):
+        fx = json.loads((g / f"qpp_textcols_{ds}.json").read_text())
+        text.update({multicorpus.namespace_qid(ds, q): t for q, t in zip(fx["qids"], fx["text"])})
+    qids = multicorpus.batch_qids(bq)
+    return qids, [text.get(q, multicorpus.split_qid(q)[1]) for q in qids]
 
 
 def text_inputs(q_begin, Q):
@@ -139,9 +184,26 @@ class Pipeline:
         else:
             Q, self.q_begin = wl["queries"], rank * wl["queries"]
         self.Q, self.R, self.K = Q, R, K
+        if args.queries is not None or not wl["total"]:
+            self.shard_sizes = [Q] * world
+        else:
+            from qppfuse.dist import shard_range
+            self.shard_sizes = [e - b for b, e in (shard_range(wl["queries"], world, r)
+                                                   for r in range(world))]
         self.methods = args.methods
         self.off, self.docid, self.raw = engine.synth_runs(self.q_begin, Q, R, K, seed=SEED)
-        nt, tf = text_inputs(self.q_begin, Q)
+        self.qids = None
+        if args.workload == "c4" and args.queries is None:
+            # the real test qids of HotpotQA + SciFact + NQ, namespaced (qppfuse.multicorpus),
+            # in batch order; query texts as compute_qpp_for_res_file gets them
+            # (queries.jsonl; HotpotQA's is an LFS pointer, so its qid, src/qpp.py:312)
+            self.qids, texts = c4_queries()
+            self.qids, texts = (self.qids[self.q_begin:self.q_begin + Q],
+                                texts[self.q_begin:self.q_begin + Q])
+            from qppfuse import textfeat
+            nt, tf = textfeat.feature_arrays(texts)
+        else:
+            nt, tf = text_inputs(self.q_begin, Q)
         self.nt = torch.from_numpy(nt).to(dev)
         self.tf = torch.from_numpy(tf).to(dev)
         E = Q * R * K
@@ -197,13 +259,13 @@ class Pipeline:
             t0.record()
         e.fuse(self.off, self.docid, self.micro, self.R, self.methods, 60, weights=w,
                max_entries=self.R * self.K, out=self.out)
-        if a.gather_topk > 0:  # the final fused top-k of every shard onto rank 0 (RCCL)
-            from qppfuse.dist import gather_fused_topk
-            d, sc = e.fused_topk(self.out, self.off, self.R, a.gather_topk)
-            self.gathered = gather_fused_topk(d, sc, dst=0)
         if timed:
             t1.record()
             self.ev.append((t0, t1))
+        if a.gather_topk > 0:  # the final fused top-k of every shard onto rank 0 (RCCL)
+            from qppfuse.dist import gather_fused_topk
+            d, sc = e.fused_topk(self.out, self.off, self.R, a.gather_topk)
+            self.gathered = gather_fused_topk(d, sc, dst=0, sizes=self.shard_sizes)
         self.w = w
 
     def fuse_kernel_ms(self):
@@ -312,20 +374,17 @@ def check_parity(p: Pipeline, nq: int):
     return ok
 
 
-def cpu_baseline_port(p: Pipeline, nq: int):
-    """The reference's per-row CPU algorithm (oracle/ref_port.py) on nq queries, 1 thread."""
-    import pandas as pd
+CPU_SAMPLE_PER_WORKER = {"c1": 1000, "c2": 25, "c3": 60, "c4": 60, "c5": 0}
 
-    from oracle import ref_port
-    h = host_sample(p, nq)
-    R, K = p.R, p.K
-    names = NAMES[:R]
-    qids = [f"test{p.q_begin + q}" for q in range(nq)]
+
+def _port_frames(h, R, names, q0, qids):
+    """Host sample -> the reference's {ranker: DataFrame} (rows in file order)."""
+    import pandas as pd
     frames, raw_lists = {}, {}
     for r, name in enumerate(names):
         rows_q, rows_d, rows_r, rows_s = [], [], [], []
-        for q in range(nq):
-            a, b = h["off"][q * R + r], h["off"][q * R + r + 1]
+        for q in range(len(qids)):
+            a, b = h["off"][(q0 + q) * R + r], h["off"][(q0 + q) * R + r + 1]
             rows_q += [qids[q]] * (b - a)
             rows_d += [f"doc{d}" for d in h["docid"][a:b]]
             rows_r += list(range(1, b - a + 1))
@@ -333,18 +392,66 @@ def cpu_baseline_port(p: Pipeline, nq: int):
             raw_lists[(qids[q], name)] = h["raw"][a:b].tolist()
         frames[name] = pd.DataFrame({"qid": rows_q, "iter": "Q0", "docno": rows_d,
                                      "rank": rows_r, "score": rows_s, "runid": name})
+    return frames, raw_lists
+
+
+def _cpu_worker(job):
+    """One CPU-baseline worker: its slice of the sample through oracle/ref_port.py —
+    the reference's per-row algorithm (QPPBridge restated, pandas groupby/iterrows,
+    ranx-equivalent dict loops) — timed per stage, single-threaded."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import ref_port
+    h, R, names, q0, nq, q_begin, methods, qpp_on, qpp_index = job
+    qids = [f"test{q_begin + q0 + q}" for q in range(nq)]
+    frames, raw_lists = _port_frames(h, R, names, q0, qids)
+    t = {}
     t0 = time.perf_counter()
-    # QPP: per (query, retriever) list, Java restated in Python (QPPBridge.java:134-453)
-    qpp = {q: {} for q in qids}
-    for (qid, name), scores in raw_lists.items():
-        qi = qids.index(qid)
-        d = ref_port.java_qpp(int(h["nt"][qi]), float(h["tf"][qi][0]), float(h["tf"][qi][1]),
-                              sorted(scores, reverse=True)[:100])
-        qpp[qid][name] = [d[n] for n in ref_port.QPP_NAMES]
-    for m in p.methods:
-        ref_port.fuse(frames, m, qpp, p.args.qpp_index, 60)
-    dt = time.perf_counter() - t0
-    return nq / dt, dt
+    qpp = {q: {n: [0.5] * 13 for n in names} for q in qids}
+    if qpp_on:  # per (query, retriever) list, Java restated in Python (QPPBridge.java:134-453)
+        for i, qid in enumerate(qids):
+            for name in names:
+                d = ref_port.java_qpp(int(h["nt"][q0 + i]), float(h["tf"][q0 + i][0]),
+                                      float(h["tf"][q0 + i][1]),
+                                      sorted(raw_lists[(qid, name)], reverse=True)[:100])
+                qpp[qid][name] = [d[n] for n in ref_port.QPP_NAMES]
+    t["qpp"] = time.perf_counter() - t0
+    for m in methods:
+        t1 = time.perf_counter()
+        ref_port.fuse(frames, m, qpp, qpp_index, 60)
+        t[m] = time.perf_counter() - t1
+    rows = int(sum(len(df) for df in frames.values()))
+    return nq, time.perf_counter() - t0, t, rows
+
+
+def cpu_baseline_port(p: Pipeline, per_worker: int, workers: int):
+    """The reference's CPU path on a bounded sample: `workers` processes, each timing
+    `per_worker` queries single-threaded; value = sample / slowest worker's time."""
+    import multiprocessing as mp
+    nq = min(per_worker * workers, p.Q)
+    workers = max(1, min(workers, nq))
+    h = host_sample(p, nq)
+    bounds = [nq * i // workers for i in range(workers + 1)]
+    jobs = []
+    for i in range(workers):
+        a, b = bounds[i], bounds[i + 1]
+        sub = dict(off=h["off"], docid=h["docid"], raw=h["raw"], micro=h["micro"],
+                   nt=h["nt"], tf=h["tf"])
+        jobs.append((sub, p.R, NAMES[:p.R], a, b - a, p.q_begin, p.methods, p.args.wl["qpp"],
+                     p.args.qpp_index))
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(workers) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    slowest = max(r[1] for r in res)
+    busy = sum(r[1] for r in res)
+    stage = {k: sum(r[2][k] for r in res) for k in res[0][2]}
+    rows = sum(r[3] for r in res)
+    out = {"value": round(nq / slowest, 4), "per_core_value": round(nq / busy, 4),
+           "sample_queries": nq, "workers": workers, "wall_s": round(wall, 2),
+           "stage_s_all_workers": {k: round(v, 2) for k, v in stage.items()}}
+    if "wcombsum" in stage:  # calibration: the survey timed the reference itself at
+        out["wcombsum_us_per_row"] = round(stage["wcombsum"] / rows * 1e6, 2)  # 30.8 us/row
+    return out
 
 
 def cpu_baseline_native(p: Pipeline, nq: int):
@@ -396,29 +503,15 @@ def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     return None, None
 
 
-def progress(msg: str):
-    """One line on stderr per phase (long runs are not silent; stdout stays one JSON line)."""
-    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
-
-
-def main():
-    args = parse()
-    world, rank, dev = setup_dist(args)
-    from qppfuse import _lib
-    _lib.lib()
-    progress(f"rank {rank}/{world}: generating {args.workload} inputs")
-    p = Pipeline(args, world, rank, dev)
-    progress(f"rank {rank}: {p.Q} queries x {p.R} x top-{p.K} resident; warmup {args.warmup}")
-    for _ in range(args.warmup):
-        p.step()
+def timed_loop(p: Pipeline, steps: int, world: int, dev) -> float:
+    """Barrier + synchronize, `steps` steps, synchronize + barrier; max over ranks."""
     torch.cuda.synchronize()
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
-    progress(f"rank {rank}: timing {args.steps} steps")
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         p.step(timed=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -428,12 +521,49 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    return elapsed
+
+
+def progress(msg: str):
+    """One line on stderr per phase (long runs are not silent; stdout stays one JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    # stdout carries exactly one JSON line: everything else (library banners such as
+    # gloo's, progress) goes to stderr; the result is written on the saved stdout
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    world, rank, dev = setup_dist(args)
+    if args.gather_topk is None:
+        args.gather_topk = 100 if world > 1 else 0
+    from qppfuse import _lib
+    _lib.lib()
+    progress(f"rank {rank}/{world}: generating {args.workload} inputs")
+    p = Pipeline(args, world, rank, dev)
+    progress(f"rank {rank}: {p.Q} queries x {p.R} x top-{p.K} resident; warmup {args.warmup}")
+    for _ in range(args.warmup):
+        p.step()
+    progress(f"rank {rank}: timing {args.steps} steps")
+    elapsed = timed_loop(p, args.steps, world, dev)
+    total_q = p.Q * args.steps
     if world > 1:
+        import torch.distributed as dist
         qt = torch.tensor([p.Q], dtype=torch.int64, device=dev)
         dist.all_reduce(qt)
         total_q = int(qt.item()) * args.steps
-    else:
-        total_q = p.Q * args.steps
+    without_gather = None
+    if world > 1 and args.gather_topk > 0:  # the same step without the collective
+        k, args.gather_topk = args.gather_topk, 0
+        ms_fuse = list(p.ev)
+        e2 = timed_loop(p, args.steps, world, dev)
+        p.ev, args.gather_topk = ms_fuse, k
+        without_gather = {"value": round(total_q / e2, 2),
+                          "ms_per_step": round(e2 / args.steps * 1e3, 4)}
     value = total_q / elapsed
     fuse_ms = p.fuse_kernel_ms()
     fbytes, mean_u = p.fuse_bytes()
@@ -447,15 +577,21 @@ def main():
     if rank == 0:
         cpu = None
         ported = all(m in METHODS for m in p.methods)
-        if world == 1 and args.cpu_sample > 0 and ported:
-            nq = min(args.cpu_sample, p.Q)
-            progress(f"CPU baseline on {nq} queries")
-            v, dt = cpu_baseline_port(p, nq)
-            cpu = {"value": round(v, 4), "unit": "fused queries/s", "cores": 1, "kind": "port",
-                   "sample": f"{nq} queries x {args.retrievers} x top-{args.k}: 13 QPP "
-                             f"predictors + {len(p.methods)} fusion(s) through "
-                             f"oracle/ref_port.py (pandas groupby/iterrows, the reference's "
-                             f"per-row algorithm), 1 thread, {dt:.1f} s"}
+        per_worker = (CPU_SAMPLE_PER_WORKER[args.workload] if args.cpu_sample is None
+                      else args.cpu_sample)
+        if world == 1 and per_worker > 0 and ported:
+            workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+            progress(f"CPU baseline: {workers} processes x {per_worker} queries")
+            c = cpu_baseline_port(p, per_worker, workers)
+            cpu = {"value": c["value"], "unit": "fused queries/s", "cores": c["workers"],
+                   "kind": "port",
+                   "sample": f"{c['sample_queries']} queries x {args.retrievers} x top-{args.k}"
+                             f"{' + 13 QPP predictors' if args.wl['qpp'] else ''} + "
+                             f"{len(p.methods)} fusion(s) through oracle/ref_port.py (the "
+                             f"reference's per-row algorithm: pandas groupby/iterrows, "
+                             f"ranx-equivalent dict loops), {c['workers']} single-threaded "
+                             f"processes, {c['wall_s']} s wall",
+                   **{k: v for k, v in c.items() if k not in ("value", "workers")}}
             if args.native_sample > 0:
                 cpu["native_c_oracle_value"] = round(
                     cpu_baseline_native(p, min(args.native_sample, p.Q)), 2)
@@ -474,7 +610,10 @@ def main():
                        "queries_per_gpu": p.Q, "retrievers": args.retrievers,
                        "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": p.methods,
                        "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1),
-                       "gather_topk_to_rank0": args.gather_topk},
+                       "gather_topk_to_rank0": args.gather_topk,
+                       "qids": (None if p.qids is None else
+                                f"real BEIR test qids, namespaced: {p.qids[0]} .. {p.qids[-1]}"),
+                       "without_gather": without_gather},
             "roofline": {"bound": "hbm", "kernel": "qf_fuse", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -498,7 +637,7 @@ def main():
                 "queries": nq, "max_abs_per_query": dq, "max_abs_mean": dm,
                 "ref": "CPU reference path: C oracle fusion + trec_eval restatement "
                        "(oracle/), scores as the .res text"}
-        print(json.dumps(result), flush=True)
+        os.write(out_fd, (json.dumps(result) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
     return result

@@ -225,7 +225,7 @@ int qf_gbdt_predict(int64_t n_rows, const double* X, int32_t n_features, int32_t
  * Learned weights (src/models/base.py:120-125 _normalize_weights, then
  * src/fusion.py:431-440): per query clip the n_boosters predictions at 0,
  * divide by their numpy row sum (1 when 0); run r gets the weight of booster
- * run_to_booster[r] (HOST array, n_runs <= 16), or 1/n_boosters when it is -1
+ * run_to_booster[r] (HOST array, n_runs <= 32), or 1/n_boosters when it is -1
  * (a run the model does not know).  w_out[q*n_runs + r] feeds qf_fuse(QF_LEARNED).
  */
 int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters,

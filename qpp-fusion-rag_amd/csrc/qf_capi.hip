@@ -1,7 +1,9 @@
 // qf_capi.hip — the C-ABI of libqppfuse.so (declared in include/qppfuse.h).
 // Argument validation, kernel selection, thread-local error strings.  No entry
-// point allocates, frees or synchronises: everything is stream-ordered on the
-// caller's stream, so a caller may capture the whole pipeline in a hipGraph.
+// point synchronises: everything is stream-ordered on the caller's stream.  The
+// only allocation is qf_fuse's workspace for queries beyond the LDS join (more
+// than 10,240 entries or 16 runs): hipMallocAsync / hipFreeAsync on the call's
+// stream (include/qppfuse.h).
 #include <cstdio>
 #include <string>
 
@@ -231,7 +233,7 @@ int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters
                        int32_t n_runs, const int32_t* run_to_booster, double* w_out,
                        void* stream) {
   if (n_queries < 0 || n_boosters <= 0 || n_boosters > qf::kMaxBoosters || n_runs <= 0 ||
-      n_runs > qf::kMaxBoosters || !run_to_booster)
+      n_runs > qf::kMaxLearnedRuns || !run_to_booster)
     return fail(QF_EINVAL, "qf_learned_weights: bad sizes");
   qf::LearnedWeightParams p{};
   for (int r = 0; r < n_runs; ++r) {

@@ -1297,6 +1297,7 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
     if (q < p.n_queries) {
       const int64_t n = p.list_off[q * p.R + p.R] - p.list_off[q * p.R];
       if (n > nmin && n <= nmax) s_list[atomicAdd(&s_n, 1)] = q;
+      else if (n > nmax) p.union_count[q] = QF_QSTATUS_TOOBIG;  // beyond max_entries
     }
     __syncthreads();
     const int n = s_n;

@@ -62,6 +62,7 @@ struct EvalParams {
 
 // LightGBM inference (qf_gbdt_predict) and learned weights (qf_learned_weights).
 constexpr int kMaxBoosters = 16;
+constexpr int kMaxLearnedRuns = 32;  // runs a learned weight table maps (qf_fuse's run cap)
 struct GbdtParams {
   int64_t n_rows;
   const double* X;
@@ -83,7 +84,7 @@ struct LearnedWeightParams {
   const double* pred;
   int32_t n_boosters;
   int32_t n_runs;
-  int32_t run_to_booster[kMaxBoosters];
+  int32_t run_to_booster[kMaxLearnedRuns];
   double* w_out;
 };
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st);

@@ -11,11 +11,13 @@ from pathlib import Path
 from ._build import LIB_PATH
 
 QF_OK, QF_EINVAL, QF_ETOOBIG, QF_EHIP = 0, 1, 2, 3
+QF_QSTATUS_TOOBIG, QF_QSTATUS_UNSORTED, QF_QSTATUS_RANKORDER, QF_QSTATUS_BADDOC, \
+    QF_QSTATUS_DUPDOC = -1, -2, -3, -4, -5
 QF_QSTATUS = {-1: "query exceeds the fusion kernel's entry limit",
               -2: "run list not sorted by score descending",
               -3: "rank column not non-decreasing within a run list",
               -4: "reserved docid 0xFFFFFFFF",
-              -5: "a docno repeats within one run list (unsupported)"}
+              -5: "a docno repeats within one run list (the host splits such lists)"}
 
 COMBSUM, COMBMNZ, RRF, WCOMBSUM, WCOMBMNZ, WRRF, LEARNED, PROBFUSE, WRRF_MUL = \
     (1 << i for i in range(9))

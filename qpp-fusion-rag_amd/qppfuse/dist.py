@@ -73,21 +73,29 @@ def allgather_qpp_raw(raw, present, group=None):
             torch.cat([t[:k] for t, k in zip(pres, sizes)]).to(torch.bool))
 
 
-def gather_fused_topk(docid, score, dst: int = 0, group=None):
+def gather_fused_topk(docid, score, dst: int = 0, group=None, sizes=None):
     """The final fused top-k of every rank's query shard, concatenated in rank
     order on rank `dst` (None elsewhere): docid [Q_r, M, k] and score tensors
     from engine.fused_topk.  Shards may differ in size by the shard_range
     remainder: rows are padded to the largest shard for the collective
-    (dist.gather over RCCL/xGMI; gloo in the CPU tests) and trimmed after."""
+    (dist.gather over RCCL/xGMI; gloo in the CPU tests) and trimmed after.
+    `sizes` (every rank's row count, when the caller knows them — fixed shards)
+    skips the all-gather of the counts and its host synchronisation."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return docid, score
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    n = torch.tensor([docid.shape[0]], dtype=torch.int64, device=docid.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if dist.get_backend(group) == "gloo" and docid.is_cuda:  # gloo rehearsal: host buffers
+        docid, score = docid.cpu(), score.cpu()
+    if sizes is None:
+        n = torch.tensor([docid.shape[0]], dtype=torch.int64, device=docid.device)
+        got = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(got, n, group=group)
+        sizes = [int(s.item()) for s in got]
+    sizes = list(sizes)
+    if len(sizes) != world or sizes[rank] != docid.shape[0]:
+        raise ValueError(f"sizes {sizes} do not match this rank's {docid.shape[0]} rows")
     m = max(sizes)
     pad = lambda t, v: torch.cat([t, t.new_full((m - t.shape[0],) + tuple(t.shape[1:]), v)]) \
         if t.shape[0] < m else t

@@ -406,6 +406,29 @@ def test_more_than_16_runs_take_the_workspace_join(gpu, R, K):
             assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
+def test_workspace_join_reports_queries_beyond_max_entries(gpu):
+    """17 runs (the workspace join for every query) with one query larger than the
+    max_entries the caller passes: that query reports QF_QSTATUS_TOOBIG instead of
+    leaving its union_count unwritten; the others are fused as usual."""
+    from qppfuse import engine, _lib
+    R = 17
+    rng = np.random.default_rng(17)
+    lists = []
+    for q, k in enumerate((4, 9, 3)):
+        for r in range(R):
+            docs = rng.choice(1000, size=k, replace=False).astype(np.uint32)
+            lists.append((docs, np.sort(rng.integers(0, 10**6, k))[::-1] / 1e6))
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    out = engine.fuse(doff, ddoc, dsc, R, ["combsum", "rrf"], max_entries=4 * R)
+    uc = out.union_count.cpu().numpy()
+    assert uc[1] == _lib.QF_QSTATUS_TOOBIG
+    o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, "combsum", 60)
+    for q in (0, 2):
+        b, n = off[q * R], uc[q]
+        assert n == o_uc[q] > 0
+        assert out.fused.cpu().numpy()[0][b:b + n].tobytes() == o_fused[b:b + n].tobytes()
+
+
 def test_more_than_32_runs_are_rejected(gpu):
     from qppfuse import engine
     R = 33

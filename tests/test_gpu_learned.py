@@ -29,7 +29,8 @@ def _model(name):
 def _X(rng, n, f):
     X = rng.uniform(0, 1, (n, f))
     X[rng.random((n, f)) < 0.15] = 0.0          # zero features (missing qpp -> 0)
-    X[rng.random((n, f)) < 0.05] = np.round(X[rng.random((n, f)) < 0.05].mean(), 6)
+    m = rng.random((n, f)) < 0.05                # repeated values (one mask for both sides)
+    X[m] = np.round(X[m].mean(), 6)
     return X
 
 
@@ -114,3 +115,31 @@ def test_learned_fusion_matches_reference_pandas(gpu, name, ties, tmp_path, caps
     p = tmp_path / "learned.res"
     fusion.write_runfile(got, str(p), "learned")
     assert p.read_text() == ref_port.runfile_text(want, "learned")
+
+
+@pytest.mark.parametrize("dups", [False, True])
+def test_learned_fusion_18_runs_and_duplicates(gpu, dups):
+    """18 runs (5 the model knows + 13 it does not: weight 1/n_retrievers,
+    src/fusion.py:435) through the workspace join, and docnos repeated inside one
+    list (the groupby adds every row, src/fusion.py:440-441): == the reference's
+    pandas calls (oracle/ref_port.py) bit for bit."""
+    from qppfuse import fusion
+    rng = np.random.default_rng(18 + dups)
+    model = _model("fusion_multioutput")
+    qids = [f"test{i}" for i in range(25)]
+    rankers = list(model.retrievers) + [f"X{i:02d}" for i in range(13)]
+    runs = _runs(rng, qids, rankers, 30)
+    if dups:
+        for r in rankers[::3]:
+            df = runs[r]
+            extra = df.sample(frac=0.2, random_state=int(rng.integers(1 << 30))).copy()
+            extra["score"] = np.round(rng.uniform(0, 1, len(extra)), 6)
+            runs[r] = pd.concat([df, extra], ignore_index=True)
+    qpp = {q: {r: [float(np.round(v, 6)) for v in rng.uniform(0, 1, 13)]
+               for r in model.retrievers} for q in qids}
+    got = fusion.learned_fusion(runs, qpp, str(GOLD / "nq_fusion_multioutput.json.gz"))
+    wd = lgbm_oracle.weights_dict(runs, qpp, model)
+    want = ref_port.learned_fusion_from_weights(runs, wd, len(model.retrievers))
+    assert list(got.keys()) == sorted(want.keys())
+    for q in want:
+        assert got[q] == want[q], q
