@@ -56,6 +56,64 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
   return (uint32_t)x;
 }
 
+// MIN / MAX of a u64 over the wave, result in lane 63 (DPP only: quad_perm,
+// row_half_mirror and row_mirror reduce each 16-lane row, row_bcast:15/31 carry
+// rows into lane 63; no ds_bpermute addresses).  Masked lanes read the identity.
+#define QF_DPP_U64_STEP(x, id, ctrl, rmask, MAX)                                          \
+  do {                                                                                     \
+    const uint32_t _lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(id), (int)(uint32_t)(x), \
+                                                               ctrl, rmask, 0xf, false);      \
+    const uint32_t _hi = (uint32_t)__builtin_amdgcn_update_dpp(                            \
+        (int)(id), (int)(uint32_t)((x) >> 32), ctrl, rmask, 0xf, false);                   \
+    const uint64_t _o = ((uint64_t)_hi << 32) | _lo;                                       \
+    x = (MAX) ? (_o > x ? _o : x) : (_o < x ? _o : x);                                     \
+  } while (0)
+template <bool MAX>
+__device__ __forceinline__ uint64_t wave_minmax_u64_dpp(uint64_t x) {
+  const uint32_t id = MAX ? 0u : 0xFFFFFFFFu;
+  QF_DPP_U64_STEP(x, id, 0xB1, 0xf, MAX);   // quad_perm [1,0,3,2]
+  QF_DPP_U64_STEP(x, id, 0x4E, 0xf, MAX);   // quad_perm [2,3,0,1]
+  QF_DPP_U64_STEP(x, id, 0x141, 0xf, MAX);  // row_half_mirror
+  QF_DPP_U64_STEP(x, id, 0x140, 0xf, MAX);  // row_mirror
+  QF_DPP_U64_STEP(x, id, 0x142, 0xa, MAX);  // row_bcast:15
+  QF_DPP_U64_STEP(x, id, 0x143, 0xc, MAX);  // row_bcast:31
+  return x;
+}
+// MIN / MAX of a double over the wave, result in lane 63 (the same DPP pattern;
+// fmin / fmax skip a NaN, so callers flag NaNs themselves).
+#define QF_DPP_F64_STEP(x, ctrl, rmask, MAX)                                                 \
+  do {                                                                                     \
+    const double _id = (MAX) ? -INFINITY : INFINITY;                                       \
+    const uint64_t _xb = (uint64_t)__double_as_longlong(x);                                \
+    const uint64_t _ib = (uint64_t)__double_as_longlong(_id);                              \
+    const uint32_t _lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)_ib,         \
+                                                               (int)(uint32_t)_xb, ctrl,   \
+                                                               rmask, 0xf, false);         \
+    const uint32_t _hi = (uint32_t)__builtin_amdgcn_update_dpp(                            \
+        (int)(uint32_t)(_ib >> 32), (int)(uint32_t)(_xb >> 32), ctrl, rmask, 0xf, false);  \
+    const double _o = __longlong_as_double((long long)(((uint64_t)_hi << 32) | _lo));      \
+    x = (MAX) ? fmax(x, _o) : fmin(x, _o);                                                 \
+  } while (0)
+template <bool MAX>
+__device__ __forceinline__ double wave_minmax_f64_dpp(double x) {
+  QF_DPP_F64_STEP(x, 0xB1, 0xf, MAX);
+  QF_DPP_F64_STEP(x, 0x4E, 0xf, MAX);
+  QF_DPP_F64_STEP(x, 0x141, 0xf, MAX);
+  QF_DPP_F64_STEP(x, 0x140, 0xf, MAX);
+  QF_DPP_F64_STEP(x, 0x142, 0xa, MAX);
+  QF_DPP_F64_STEP(x, 0x143, 0xc, MAX);
+  return x;
+}
+__device__ __forceinline__ double wave_min_f64_dpp(double x) { return wave_minmax_f64_dpp<false>(x); }
+__device__ __forceinline__ double wave_max_f64_dpp(double x) { return wave_minmax_f64_dpp<true>(x); }
+
+__device__ __forceinline__ uint64_t wave_min_u64_dpp(uint64_t x) {
+  return wave_minmax_u64_dpp<false>(x);
+}
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t x) {
+  return wave_minmax_u64_dpp<true>(x);
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));

@@ -23,6 +23,7 @@
 //   descending, ties in first-seen order (Python's stable sorted(),
 //   src/fusion.py:475,488), and writes perm / fused back in place, coalesced.
 #include <cstdlib>
+#include <type_traits>
 
 #include "../../include/qppfuse.h"
 #include "qf_common.h"
@@ -501,43 +502,57 @@ struct JoinLds {
   static_assert(kBytes <= 160 * 1024, "LDS budget");
 };
 
-// f64 scores need 72 KB of LDS (2 per CU), so only micro-unit scores aim higher
-template <class C, int KIND>
-__global__ __launch_bounds__(C::kBlock, KIND == 1 ? C::kMinWaves : (C::kMinWaves < 4 ? C::kMinWaves : 4))
-void join_kernel(FuseParams p) {
+// Shared memory of the join: the table / groups area (Extra: bytes the fused
+// join + sort kernel reuses it for) and the per-query constants.
+template <class C, int KIND, int EXTRA = 0>
+struct JoinShared {
+  using L = JoinLds<C, KIND>;
+  static constexpr int kBytes = L::kBytes > EXTRA ? L::kBytes : EXTRA;
+  __attribute__((aligned(16))) unsigned char smem[kBytes];
+  int64_t off[kRMax + 1];
+  double w[kRMax], mn[kRMax], den[kRMax], rden[kRMax];
+  int cnt[C::kItems * C::kWaves], gof[C::kItems * C::kWaves];
+  int U, status;
+  int slow;  // bit 0: a non-empty list is not [0, 1]-normalised; bit 1: a weight needs IEEE division
+};
+
+// The join proper, phases 1-3 (see the file header): loads, LDS hash join with the
+// order / duplicate checks, first-seen numbering (union_docid written) and the
+// contribution groups left in LDS (gsc / gpr / ugo of JoinLds).  Returns N, or -1
+// when the query exceeds the configuration (union_count already written);
+// sh.U / sh.status are set (block-uniform after the final barrier).
+template <class C, int KIND, int EXTRA>
+__device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KIND, EXTRA>& sh,
+                                           int64_t q) {
   constexpr int BLOCK = C::kBlock, ITEMS = C::kItems, WAVES = C::kWaves;
   constexpr int NMAX = C::kNMax, TS = C::kTS;
   using L = JoinLds<C, KIND>;
   using raw_t = typename L::raw_t;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[L::kBytes];
-  __shared__ int64_t s_off[kRMax + 1];
-  __shared__ double s_w[kRMax], s_min[kRMax], s_den[kRMax], s_rden[kRMax];
-  __shared__ int s_cnt[ITEMS * WAVES], s_gof[ITEMS * WAVES];
-  __shared__ int s_U, s_status;
+  unsigned char* smem = sh.smem;
   uint32_t* tkey = (uint32_t*)smem;
   uint32_t* tmask2 = (uint32_t*)(smem + 4 * TS);  // two u16 masks per word
   auto mask_of = [&](uint32_t slot) -> uint32_t {
     return (tmask2[slot >> 1] >> ((slot & 1u) * 16u)) & 0xFFFFu;
   };
-
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t q = block_id();
-  if (q >= p.n_queries) return;
   QF_STAMP_INIT();
   const int R = p.R;
-  if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
-  if (tid == 0) s_status = 0;
+  if (tid <= R) sh.off[tid] = p.list_off[q * R + tid];
+  if (tid == 0) {
+    sh.status = 0;
+    sh.slow = 0;
+  }
   __syncthreads();
-  const int64_t base = s_off[0];
-  const int64_t N64 = s_off[R] - base;
+  const int64_t base = sh.off[0];
+  const int64_t N64 = sh.off[R] - base;
   if (N64 > NMAX) {  // uniform
     if (tid == 0) p.union_count[q] = QF_QSTATUS_TOOBIG;
-    return;
+    return -1;
   }
   const int N = (int)N64;
   if (tid < R) {
-    const int64_t a = s_off[tid], b = s_off[tid + 1];
-    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
+    const int64_t a = sh.off[tid], b = sh.off[tid + 1];
+    sh.w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
     // ranx min-max (norm="min-max", the fuse() default); lists are sorted
     // descending (checked below), so max / min are the end points.
     double mx = 0.0, mn = 0.0;
@@ -545,9 +560,15 @@ void join_kernel(FuseParams p) {
       mx = ScoreIn<KIND>::load(p.score, a);
       mn = ScoreIn<KIND>::load(p.score, b - 1);
     }
-    s_min[tid] = mn;
-    s_den[tid] = mx - mn;
-    s_rden[tid] = 1.0 / (mx - mn);  // one IEEE division per list (div_by_recip)
+    sh.mn[tid] = mn;
+    sh.den[tid] = mx - mn;
+    sh.rden[tid] = 1.0 / (mx - mn);  // one IEEE division per list (div_by_recip)
+    // block-uniform fast paths of the sums: every list already [0, 1] (a .norm.res
+    // list: x = s), every weight in div_int's division-free range
+    const double aw = fabs(sh.w[tid]);
+    const int slow = ((b > a && !(mx == 1.0 && mn == 0.0)) ? 1 : 0) |
+                     ((aw > 0x1p-900 && aw < 0x1p900) ? 0 : 2);
+    if (slow) atomicOr(&sh.slow, slow);
   }
   for (int i = tid * 4; i < TS; i += BLOCK * 4)
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
@@ -575,7 +596,7 @@ void join_kernel(FuseParams p) {
     if (e < N) {
       const uint32_t d = dk[j];
       if (d == kEmpty) status = QF_QSTATUS_BADDOC;
-      while (base + e >= s_off[r + 1]) ++r;
+      while (base + e >= sh.off[r + 1]) ++r;
       rj[j] = (uint32_t)r;
       uint32_t h = (d * 0x9E3779B1u) >> (32 - C::kTB);
       while (true) {
@@ -589,7 +610,7 @@ void join_kernel(FuseParams p) {
       dk[j] = h;  // keep the slot
       // preconditions of the ranx methods / W-RRF (checked once, here)
       const int64_t g = base + e;
-      if (g + 1 < s_off[r + 1]) {
+      if (g + 1 < sh.off[r + 1]) {
         if (p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) {
           const raw_t nx = lane == 63 ? ScoreIn<KIND>::raw(p.score, g + 1) : nxt;
           // raw compare: m / 1e6 is strictly increasing in the micro-units m
@@ -600,7 +621,7 @@ void join_kernel(FuseParams p) {
       }
     }
   }
-  if (status) atomicMin(&s_status, status);
+  if (status) atomicMin(&sh.status, status);
   __syncthreads();
   QF_STAMP(4);
   // ---- number distinct documents in first-seen order; size their groups ------
@@ -619,8 +640,8 @@ void join_kernel(FuseParams p) {
     const uint64_t b = ballot(rep);
     const uint32_t tot = readlane_u32(wave_incl_scan_dpp(pc), 63);
     if (lane == 0) {
-      s_cnt[j * WAVES + wid] = __popcll(b);
-      s_gof[j * WAVES + wid] = (int)tot;
+      sh.cnt[j * WAVES + wid] = __popcll(b);
+      sh.gof[j * WAVES + wid] = (int)tot;
     }
   }
   __syncthreads();
@@ -628,21 +649,20 @@ void join_kernel(FuseParams p) {
     uint32_t c1 = 0, c2 = 0;
     for (int c0 = 0; c0 < ITEMS * WAVES; c0 += 64) {
       const int i = c0 + lane;
-      const uint32_t v1 = i < ITEMS * WAVES ? (uint32_t)s_cnt[i] : 0u;
-      const uint32_t v2 = i < ITEMS * WAVES ? (uint32_t)s_gof[i] : 0u;
+      const uint32_t v1 = i < ITEMS * WAVES ? (uint32_t)sh.cnt[i] : 0u;
+      const uint32_t v2 = i < ITEMS * WAVES ? (uint32_t)sh.gof[i] : 0u;
       const uint32_t i1 = wave_incl_scan_dpp(v1), i2 = wave_incl_scan_dpp(v2);
       if (i < ITEMS * WAVES) {
-        s_cnt[i] = (int)(c1 + i1 - v1);
-        s_gof[i] = (int)(c2 + i2 - v2);
+        sh.cnt[i] = (int)(c1 + i1 - v1);
+        sh.gof[i] = (int)(c2 + i2 - v2);
       }
       c1 += readlane_u32(i1, 63);
       c2 += readlane_u32(i2, 63);
     }
-    if (lane == 0) s_U = (int)c1;
+    if (lane == 0) sh.U = (int)c1;
   }
   __syncthreads();
   QF_STAMP(5);
-  const int U = s_U;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const bool rep = (repm >> j) & 1u;
@@ -654,8 +674,8 @@ void join_kernel(FuseParams p) {
     }
     const uint32_t gpre = wave_incl_scan_dpp(pc) - pc;
     if (rep) {
-      const uint32_t u = (uint32_t)s_cnt[j * WAVES + wid] + mbcnt(b);
-      const uint32_t go = (uint32_t)s_gof[j * WAVES + wid] + gpre;
+      const uint32_t u = (uint32_t)sh.cnt[j * WAVES + wid] + mbcnt(b);
+      const uint32_t go = (uint32_t)sh.gof[j * WAVES + wid] + gpre;
       p.union_docid[base + u] = tkey[dk[j]];
       tkey[dk[j]] = go | (u << 16);  // slot -> group offset | u (the docid is dead)
     }
@@ -685,18 +705,76 @@ void join_kernel(FuseParams p) {
     if (e < N) {
       const uint32_t k = dk[j] & 0xFFFFu, r = rj[j];
       gsc[k] = sc[j];
-      gpr[k] = (uint32_t)(base + e - s_off[r]) | (r << 16);
+      gpr[k] = (uint32_t)(base + e - sh.off[r]) | (r << 16);
       if ((repm >> j) & 1u) ugo[dk[j] >> 16] = (uint16_t)k;
     }
   }
   __syncthreads();
   QF_STAMP(7);
+  return N;
+}
+
+constexpr int kFastSumMethods = QF_COMBSUM | QF_COMBMNZ | QF_RRF | QF_WCOMBSUM | QF_WCOMBMNZ |
+                                QF_WRRF;
+
+// Every document's fused score for every requested method, from the groups the
+// join left in LDS, stored unsorted at fused[slot][base + u] (the sort kernels
+// read them back): one thread per document, strided.
+template <class C, int KIND, int EXTRA>
+__device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
+                                                    JoinShared<C, KIND, EXTRA>& sh, int N) {
+  constexpr int BLOCK = C::kBlock;
+  using L = JoinLds<C, KIND>;
+  using raw_t = typename L::raw_t;
+  const int tid = threadIdx.x;
+  const int64_t base = sh.off[0];
+  const int U = sh.U;
+  const raw_t* gsc = (const raw_t*)(sh.smem + L::kGscOff);
+  const uint32_t* gpr = (const uint32_t*)(sh.smem + L::kGprOff);
+  const uint16_t* ugo = (const uint16_t*)(sh.smem + L::kGoOff);
   // ---- fused score of every document, every requested method ------------------
   const int methods = p.methods, rrf_k = p.rrf_k;
   int slot[kNMethods];
   for (int t = 0, c = 0; t < kNMethods; ++t) {
     slot[t] = c;
     c += (methods >> t) & 1;
+  }
+  // The common case without any per-entry range check: micro-unit scores, every
+  // list already [0, 1] (x = s), every weight in the division-free range, ranks =
+  // positions, k + N + 1 <= 2^24 — CombSUM / CombMNZ / RRF / W-* only.  1 / (k +
+  // rank) is computed once per entry for RRF and W-RRF (div_small's reciprocal).
+  const bool fast = KIND == 1 && sh.slow == 0 && !p.rank && (methods & ~kFastSumMethods) == 0 &&
+                    rrf_k >= 0 && rrf_k + N + 1 <= (1 << 24);
+  if (fast) {
+    for (int u = tid; u < U; u += BLOCK) {
+      const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0;
+      for (int k = gs; k < ge; ++k) {
+        const double s = ScoreIn<KIND>::val(gsc[k]);
+        const uint32_t q2 = gpr[k];
+        const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
+        const int n = rrf_k + pos + 1;
+        const double y = (methods & (QF_RRF | QF_WRRF)) ? recip_small(n) : 0.0;
+        const double w = sh.w[r];
+        if (methods & (QF_COMBSUM | QF_COMBMNZ)) a0 += s;  // (s - 0.0) / 1.0 == s
+        if (methods & QF_RRF) a1 += y;
+        if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += w * s;
+        if (methods & QF_WRRF) {  // div_small(w, n) with the same reciprocal
+          const double qt = w * y;
+          a5 += fma(fma(-qt, (double)n, w), y, qt);
+        }
+      }
+      const double cnt = (double)(ge - gs);
+      double* out = p.fused + base + u;
+      const int64_t st = p.out_stride;
+      if (methods & QF_COMBSUM) out[slot[0] * st] = a0;
+      if (methods & QF_COMBMNZ) out[slot[1] * st] = a0 * cnt;
+      if (methods & QF_RRF) out[slot[2] * st] = a1;
+      if (methods & QF_WCOMBSUM) out[slot[3] * st] = a2;
+      if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
+      if (methods & QF_WRRF) out[slot[5] * st] = a5;
+    }
+    return;
   }
   for (int u = tid; u < U; u += BLOCK) {
     const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
@@ -706,7 +784,7 @@ void join_kernel(FuseParams p) {
       const uint32_t q2 = gpr[k];
       const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
       if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // ranx min-max normalised score
-        const double den = s_den[r], mn = s_min[r];
+        const double den = sh.den[r], mn = sh.mn[r];
         // A .norm.res list is already [0, 1] (min 0.000000, max 1.000000), where
         // (s - 0.0) / 1.0 == s bit for bit (-0.0 included): skip the division.
         double x = 0.0;
@@ -714,19 +792,19 @@ void join_kernel(FuseParams p) {
           const double d = s - mn;
           x = (den == 1.0 && mn == 0.0) ? s
               : (den >= 0x1p-900 && den <= 0x1p900 && d >= 0x1p-900 && d <= 0x1p900)
-                  ? div_by_recip(d, den, s_rden[r])
+                  ? div_by_recip(d, den, sh.rden[r])
                   : d / den;
         }
         a0 += x;
       }
       if (methods & QF_RRF) a1 += recip_int(rrf_k + pos + 1);  // ranx rrf: rank = position
-      if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += s_w[r] * s;  // src/fusion.py:273
-      if (methods & QF_WRRF) {                                      // src/fusion.py:374
-        const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;
-        a5 += div_int(s_w[r], rrf_k + rk);
+      if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += sh.w[r] * s;  // src/fusion.py:273
+      if (methods & QF_WRRF) {                                       // src/fusion.py:374
+        const int rk = p.rank ? p.rank[sh.off[r] + pos] : pos + 1;
+        a5 += div_int(sh.w[r], rrf_k + rk);
       }
       if (methods & (QF_PROBFUSE | QF_WRRF_MUL)) {
-        const int rk = p.rank ? p.rank[s_off[r] + pos] : pos + 1;  // int(row["rank"])
+        const int rk = p.rank ? p.rank[sh.off[r] + pos] : pos + 1;  // int(row["rank"])
         if (methods & QF_PROBFUSE) {  // ProbFuse.py:30-39,172-179
           // ceil(rank * x / L) in integers (exact: the float quotient of two
           // integers below 2^26 is never rounded onto an integer), clipped to [1, x]
@@ -736,10 +814,10 @@ void join_kernel(FuseParams p) {
           a7 += div_int(p.seg_prob[r * p.n_seg + (int)k - 1], (int)k);
         }
         if (methods & QF_WRRF_MUL)  // QPPrrf_argmax.py:71: weight * (1.0 / (k + rank))
-          a8 += s_w[r] * recip_int(rrf_k + rk);
+          a8 += sh.w[r] * recip_int(rrf_k + rk);
       }
       if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
-        const double y = s * s_w[r] - c6;
+        const double y = s * sh.w[r] - c6;
         const double t = a6 + y;
         c6 = (t - a6) - y;
         if (c6 != c6) c6 = 0.0;  // +-inf contributions (pandas GH#53606)
@@ -759,7 +837,20 @@ void join_kernel(FuseParams p) {
     if (methods & QF_PROBFUSE) out[slot[7] * st] = a7;
     if (methods & QF_WRRF_MUL) out[slot[8] * st] = a8;
   }
-  if (tid == 0) p.union_count[q] = s_status ? s_status : U;
+}
+
+// f64 scores need 72 KB of LDS (2 per CU), so only micro-unit scores aim higher
+template <class C, int KIND>
+__global__ __launch_bounds__(C::kBlock, KIND == 1 ? C::kMinWaves : (C::kMinWaves < 4 ? C::kMinWaves : 4))
+void join_kernel(FuseParams p) {
+  __shared__ JoinShared<C, KIND> sh;
+  const int64_t q = block_id();
+  if (q >= p.n_queries) return;
+  QF_STAMP_INIT();
+  const int N = join_groups<C, KIND>(p, sh, q);
+  if (N < 0) return;
+  store_unsorted_sums<C, KIND>(p, sh, N);
+  if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : sh.U;
   QF_STAMP(14);
 }
 
@@ -976,6 +1067,622 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
   }
 }
 
+
+// ============================================================================
+// join_sort_kernel — the common case in ONE kernel: the join above, the sums in
+// registers, and every requested method's stable descending sort in LDS, so the
+// unsorted fused scores never travel through HBM (one workgroup per query;
+// micro-unit scores, <= 16 runs, N <= 5,120 entries, U <= kJsUMax documents,
+// methods among CombSUM / CombMNZ / RRF / W-CombSUM / W-CombMNZ / W-RRF).
+//
+// Per method, a bucket sort on a monotone key:
+//   w(v) = (bits(float((v - smin) + delta)) - bits(float(delta))) >> sh
+//   (delta = (smax - smin) / 32): every rounding in it is monotone and the bits
+//   of a non-negative float are ordered, so w is non-decreasing in v and equal
+//   scores (-0.0 and +0.0 included) share a bucket.  In float bits it resolves
+//   scores relative to their distance from smin — ~4,096 buckets over ~5
+//   binades above delta — which suits the skewed fused distributions (most
+//   documents sit in one list, near the bottom).
+//   1. count: one returning LDS atomic per item on its bucket (order inside a
+//      bucket is arbitrary);
+//   2. exclusive scan of the kJsBuckets counters (and the largest bucket);
+//   3. scatter value + u to start[w] + slot;
+//   4. the final position of an item is its bucket's start + the number of
+//      items of its bucket that precede it in (score descending, u ascending)
+//      order — the stable sort's order, counted exactly with f64 compares.
+// Its cost per item is the size of its bucket (measured on C2: 2-4 on average).
+// A bucket above kJsBucketMax (long runs of equal or near-equal scores) or a
+// non-finite score range sends the method through the LSD window sort of
+// sort_desc instead (the same order), with the scores staged in LDS.
+// Unions above kJsUMax are stored unsorted for fuse_large_kernel.
+// ============================================================================
+constexpr int kJsBits = 12;
+constexpr int kJsBuckets = 1 << kJsBits;
+constexpr int kJsUMax = 3072;
+constexpr int kJsBucketMax = 128;
+constexpr uint16_t kJsUnsorted = 0xFFFF;  // perm[ms][0] of a (query, method) left unsorted
+constexpr int kJsMethods = QF_COMBSUM | QF_COMBMNZ | QF_RRF | QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF;
+
+template <int BLOCK>
+struct JsCfg {
+  using J = JoinCfg<BLOCK, 5120 / BLOCK, 13>;  // N <= 5,120
+  static constexpr int kWaves = BLOCK / 64;
+  static constexpr int kRows = (kJsUMax + BLOCK - 1) / BLOCK;
+  // sort-phase LDS, over the join's: scores by position f64 [kJsUMax], u by
+  // position u16 [kJsUMax], and two sets of bucket counters / starts u32
+  // [kJsBuckets + 4] used by alternate methods (each method zeroes the next
+  // one's set while it counts: no zeroing pass, no extra barrier).  Set 0 lies
+  // beyond the join's LDS and is zeroed when the kernel starts.
+  static constexpr int kValOff = 0;
+  static constexpr int kUOff = kValOff + 8 * kJsUMax;
+  static constexpr int kCnt1Off = kUOff + 2 * kJsUMax;
+  static constexpr int kCntBytes = 4 * (kJsBuckets + 4);
+  static constexpr int kCnt0Off = (JoinLds<J, 1>::kBytes > kCnt1Off + kCntBytes
+                                   ? JoinLds<J, 1>::kBytes : kCnt1Off + kCntBytes);
+  static constexpr int kBytes = kCnt0Off + kCntBytes;
+};
+
+// Buckets: descending scores fill ascending buckets.  Scores above smin take
+// [0, kJsMinBase) by the float-bit key; the minimum score — often shared by
+// hundreds of documents (every document of a zero-weight run, the 0.000000
+// bottom of each .norm.res list) — takes [kJsMinBase, kJsBuckets) split by u,
+// so equal scores do not pile into one bucket.
+constexpr int kJsMinSub = 256;
+constexpr int kJsMinBase = kJsBuckets - kJsMinSub;
+
+// The bucket of a score (x >= delta > 0 for every v in [smin, smax]); usub =
+// kJsMinSub / U (rounded), so u * usub is non-decreasing in u and below kJsMinSub.
+__device__ __forceinline__ uint32_t js_bucket(double v, uint32_t u, float usub, double smin,
+                                              double delta, uint32_t b0, int sh) {
+  const float x = (float)((v - smin) + delta);
+  const uint32_t above = (uint32_t)(kJsMinBase - 1) - (((uint32_t)__float_as_uint(x) - b0) >> sh);
+  const uint32_t sub = min((uint32_t)((float)u * usub), (uint32_t)(kJsMinSub - 1));
+  return v == smin ? (uint32_t)kJsMinBase + sub : above;
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
+  using Cfg = JsCfg<BLOCK>;
+  using C = typename Cfg::J;
+  constexpr int ROWS = Cfg::kRows, WAVES = Cfg::kWaves;
+  __shared__ JoinShared<C, 1, Cfg::kBytes> sh;
+  static_assert(Cfg::kCnt0Off >= JoinLds<C, 1>::kBytes, "counter set 0 outside the join's LDS");
+  __shared__ unsigned long long s_kmin[kNMethods], s_kmax[kNMethods];
+  __shared__ int s_nan[kNMethods];
+  __shared__ uint32_t s_wtot[WAVES];
+  __shared__ int s_bmax;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t q = block_id();
+  if (q >= p.n_queries) return;
+  if (tid < kNMethods) {  // ordered before their atomics by join_groups' barriers
+    s_kmin[tid] = ~0ull;
+    s_kmax[tid] = 0ull;
+    s_nan[tid] = 0;
+  }
+  for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)  // counter set 0 (see JsCfg)
+    *(uint4*)(sh.smem + Cfg::kCnt0Off + 4 * i) = make_uint4(0u, 0u, 0u, 0u);
+  QF_STAMP_INIT();
+  const int N = join_groups<C, 1>(p, sh, q);
+  if (N < 0) return;
+  QF_STAMP(0);  // the whole join
+  const int U = sh.U;
+  const int64_t base = sh.off[0];
+  if (sh.status != 0 || U > kJsUMax) {  // uniform: an error, or a union for fuse_large_kernel
+    if (sh.status == 0) store_unsorted_sums<C, 1>(p, sh, N);
+    if (tid == 0) p.union_count[q] = sh.status ? sh.status : U;
+    return;
+  }
+  // ---- sums, one document per (thread, row): u = (wid * rows + j) * 64 + lane ----
+  const int rows_all = (U + BLOCK - 1) / BLOCK;
+  const int rows = rows_all;
+  const int methods = p.methods, rrf_k = p.rrf_k;
+  const int32_t* gsc = (const int32_t*)(sh.smem + JoinLds<C, 1>::kGscOff);
+  const uint32_t* gpr = (const uint32_t*)(sh.smem + JoinLds<C, 1>::kGprOff);
+  const uint16_t* ugo = (const uint16_t*)(sh.smem + JoinLds<C, 1>::kGoOff);
+  double a0[ROWS], a1[ROWS], a2[ROWS], a5[ROWS];
+  uint32_t cnts = 0u;  // each document's list count, 5 bits per row
+  // The sums of js_sums, with the per-entry range checks of the division-free
+  // quotients dropped when the whole query is in range (FAST: every list already
+  // [0, 1], every weight in range, ranks = positions, k + N + 1 <= 2^24).
+  auto js_sums = [&](auto fast_tag) {
+    constexpr bool FAST = decltype(fast_tag)::value;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      a0[j] = a1[j] = a2[j] = a5[j] = 0.0;
+      const int u = (wid * rows + j) * 64 + lane;
+      if (j < rows && u < U) {
+        const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
+        cnts |= (uint32_t)(ge - gs) << (5 * j);
+        for (int k = gs; k < ge; ++k) {
+          const double s = micro_to_f64(gsc[k]);
+          const uint32_t q2 = gpr[k];
+          const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
+          if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // as store_unsorted_sums
+            if (FAST) {
+              a0[j] += s;  // (s - 0.0) / 1.0 == s, -0.0 included
+            } else {
+              const double den = sh.den[r], mn = sh.mn[r];
+              double x = 0.0;
+              if (den > 0.0) {
+                const double d = s - mn;
+                x = (den == 1.0 && mn == 0.0) ? s
+                    : (den >= 0x1p-900 && den <= 0x1p900 && d >= 0x1p-900 && d <= 0x1p900)
+                        ? div_by_recip(d, den, sh.rden[r])
+                        : d / den;
+              }
+              a0[j] += x;
+            }
+          }
+          if (methods & QF_RRF)
+            a1[j] += FAST ? recip_small(rrf_k + pos + 1) : recip_int(rrf_k + pos + 1);
+          if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2[j] += sh.w[r] * s;
+          if (methods & QF_WRRF) {
+            if (FAST) {
+              a5[j] += div_small(sh.w[r], rrf_k + pos + 1);
+            } else {
+              const int rk = p.rank ? p.rank[sh.off[r] + pos] : pos + 1;
+              a5[j] += div_int(sh.w[r], rrf_k + rk);
+            }
+          }
+        }
+      }
+    }
+  };
+  const bool fast_sums = sh.slow == 0 && !p.rank && rrf_k >= 0 && rrf_k + N + 1 <= (1 << 24);
+  if (fast_sums) js_sums(std::true_type{});
+  else js_sums(std::false_type{});
+  // the score of method bit t for row j (CombMNZ: sum x count, src/fusion.py:327)
+  auto score_of = [&](int t, int j) -> double {
+    const double c = (double)((cnts >> (5 * j)) & 31u);
+    switch (t) {
+      case 0: return a0[j];
+      case 1: return a0[j] * c;
+      case 2: return a1[j];
+      case 3: return a2[j];
+      case 4: return a2[j] * c;
+      default: return a5[j];
+    }
+  };
+  // ---- every method's score range (f64 min / max; NaN flagged) --------------------
+  const int M = __popc(methods);
+#pragma unroll 1
+  for (int ms = 0; ms < M; ++ms) {
+    const int t = slot_method(methods, ms);
+    double vmn = INFINITY, vmx = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = (wid * rows + j) * 64 + lane;
+      if (j < rows && u < U) {
+        const double v = score_of(t, j);
+        vmn = fmin(vmn, v);  // IEEE minNum / maxNum: a NaN is skipped (flagged below)
+        vmx = fmax(vmx, v);
+        nan |= v != v;
+      }
+    }
+    vmn = wave_min_f64_dpp(vmn);
+    vmx = wave_max_f64_dpp(vmx);
+    const bool anynan = ballot(nan) != 0ull;
+    if (lane == 63) {
+      atomicMin(&s_kmin[ms], (unsigned long long)~f64_asc_key(vmx));  // kmin <-> smax
+      atomicMax(&s_kmax[ms], (unsigned long long)~f64_asc_key(vmn));
+      if (anynan) s_nan[ms] = 1;
+    }
+  }
+  if (tid == 0) p.union_count[q] = U;
+  QF_STAMP(8);
+  __syncthreads();  // the groups are dead: their LDS becomes the sort's
+  QF_STAMP(14);
+  double* sval = (double*)(sh.smem + Cfg::kValOff);   // scores by position
+  uint16_t* su = (uint16_t*)(sh.smem + Cfg::kUOff);   // u by position
+#pragma unroll 1
+  for (int ms = 0; ms < M; ++ms) {
+    const int t = slot_method(methods, ms);
+    // opaque per iteration: keeps the compiler from hoisting every row's products and
+    // addresses out of this loop (register pressure; they are cheap to recompute)
+    int rows = rows_all;
+    asm volatile("" : "+s"(rows));
+    asm volatile("" : "+v"(cnts));
+    uint32_t* bk = (uint32_t*)(sh.smem + ((ms & 1) ? Cfg::kCnt1Off : Cfg::kCnt0Off));
+    uint32_t* bk_next = (uint32_t*)(sh.smem + ((ms & 1) ? Cfg::kCnt0Off : Cfg::kCnt1Off));
+    const uint64_t kmin = s_kmin[ms], kmax = s_kmax[ms];  // ~orderable: kmin <-> smax
+    double* outv = p.fused + (int64_t)ms * p.out_stride + base;
+    uint16_t* outp = p.perm + (int64_t)ms * p.out_stride + base;
+    QF_STAMP(9);
+    if (kmax == kmin && !s_nan[ms]) {  // every score equal: first-seen order
+      for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)
+        *(uint4*)&bk_next[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = (wid * rows + j) * 64 + lane;
+        if (j < rows && u < U) {
+          __builtin_nontemporal_store((uint16_t)u, &outp[u]);
+          __builtin_nontemporal_store(score_of(t, j), &outv[u]);
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
+    const double rng = smax - smin;
+    const double delta = rng * 0x1p-5;
+    const float ftop = (float)(rng + delta);
+    // a finite range without NaN (a NaN's key lies beyond +-inf's) and a positive
+    // delta: the bucket sort; otherwise fuse_fallback_kernel's LSD window sort
+    bool fast = isfinite(rng) && isfinite(ftop) && delta > 0.0 && !s_nan[ms];
+    const uint32_t b0 = __float_as_uint((float)delta);
+    const uint32_t span = __float_as_uint(ftop) - b0;
+    int bsh = span >= (uint32_t)kJsBuckets ? (32 - __clz((int)span)) - kJsBits : 0;
+    if ((span >> bsh) >= (uint32_t)kJsMinBase) ++bsh;  // now span >> bsh < kJsMinBase
+    const float usub = (float)kJsMinSub / (float)U;
+    QF_STAMP(10);
+    uint32_t ws[ROWS];
+    if (fast) {
+      // ---- 1. count (and zero the next method's counters) ----------------------------
+      // every row's atomic issued before any result is used: rows past U add 0
+      // to bucket 0
+      uint32_t old[ROWS];
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = (wid * rows + j) * 64 + lane;
+        const bool ok = j < rows && u < U;
+        ws[j] = ok ? js_bucket(score_of(t, j), (uint32_t)u, usub, smin, delta, b0, bsh) : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = (wid * rows + j) * 64 + lane;
+        old[j] = atomicAdd(&bk[ws[j]], (j < rows && u < U) ? 1u : 0u);
+      }
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) ws[j] |= old[j] << 16;
+      for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)
+        *(uint4*)&bk_next[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (tid == 0) s_bmax = 0;
+      QF_STAMP(11);
+      __syncthreads();
+      QF_STAMP(12);
+      // ---- 2. exclusive scan of the counters, largest bucket ----------------------
+      {
+        constexpr int kPer = kJsBuckets / BLOCK;
+        uint32_t c[kPer], tot = 0u, mx = 0u;
+#pragma unroll
+        for (int i = 0; i < kPer; i += 4) {
+          const uint4 x4 = *(const uint4*)&bk[tid * kPer + i];
+          c[i] = x4.x; c[i + 1] = x4.y; c[i + 2] = x4.z; c[i + 3] = x4.w;
+        }
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+          mx = max(mx, c[i]);
+          const uint32_t x = c[i];
+          c[i] = tot;
+          tot += x;
+        }
+        const uint32_t incl = wave_incl_scan_dpp(tot);
+        if (lane == 63) s_wtot[wid] = incl;
+        mx = (uint32_t)wave_max_u64_dpp(mx);
+        if (lane == 63) atomicMax(&s_bmax, (int)mx);
+        __syncthreads();
+        uint32_t pre = incl - tot;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w)
+          if (w < wid) pre += s_wtot[w];
+#pragma unroll
+        for (int i = 0; i < kPer; i += 4)
+          *(uint4*)&bk[tid * kPer + i] =
+              make_uint4(pre + c[i], pre + c[i + 1], pre + c[i + 2], pre + c[i + 3]);
+        if (tid == 0) bk[kJsBuckets] = (uint32_t)U;
+      }
+      __syncthreads();
+      QF_STAMP(13);
+      fast = s_bmax <= kJsBucketMax;  // uniform
+    } else {
+      for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)
+        *(uint4*)&bk_next[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (fast) {
+      // ---- 3. scatter ----------------------------------------------------------
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = (wid * rows + j) * 64 + lane;
+        if (j < rows && u < U) {
+          const uint32_t pos = bk[ws[j] & 0xFFFFu] + (ws[j] >> 16);
+          sval[pos] = score_of(t, j);
+          su[pos] = (uint16_t)u;
+        }
+      }
+      __syncthreads();
+      QF_STAMP(1);
+      // ---- 4. rank inside the bucket, write the outputs ---------------------------
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int i = (wid * rows + j) * 64 + lane;
+        if (j < rows && i < U) {
+          const double vi = sval[i];
+          const uint32_t ui = su[i];
+          const uint32_t w = js_bucket(vi, ui, usub, smin, delta, b0, bsh);
+          const uint32_t lo = bk[w], hi = bk[w + 1];
+          // items of the bucket before this one: higher scores, or equal scores
+          // with a smaller u (branch-free; two items per step, loads issued together)
+          uint32_t before = 0u;
+          uint32_t k = hi - lo > 1u ? lo : hi;  // a bucket of one: nothing to count
+          for (; k + 1 < hi; k += 2) {
+            const double v0 = sval[k], v1 = sval[k + 1];
+            const uint32_t u0 = su[k], u1 = su[k + 1];
+            before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui))) +
+                      (uint32_t)((v1 > vi) | ((v1 == vi) & (u1 < ui)));
+          }
+          if (k < hi) {
+            const double v0 = sval[k];
+            const uint32_t u0 = su[k];
+            before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui)));
+          }
+          const uint32_t P = lo + before;
+          __builtin_nontemporal_store((uint16_t)ui, &outp[P]);
+          __builtin_nontemporal_store(vi, &outv[P]);
+        }
+      }
+      QF_STAMP(2);
+    } else {
+      // ---- fallback: the scores go out unsorted (by u), perm[0] marked; the LSD
+      // window sort of fuse_fallback_kernel finishes this (query, method) ---------
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = (wid * rows + j) * 64 + lane;
+        if (j < rows && u < U) outv[u] = score_of(t, j);
+      }
+      if (tid == 0) outp[0] = kJsUnsorted;
+    }
+    __syncthreads();
+    QF_STAMP(15);
+  }
+  QF_STAMP(14);
+}
+
+// ============================================================================
+// bucket_sort_kernel — the same bucket sort as join_sort_kernel, as a kernel of
+// its own over the join kernel's unsorted fused[slot][u]: one workgroup per
+// (query, method slot), U <= kJsUMax, everything after the load in LDS
+// (scores by position f64, u by position u16, 2^BITS bucket counters).  Small
+// enough to keep 4 workgroups (32 waves) per CU.  A (query, method) it cannot
+// order (a bucket above kJsBucketMax, a non-finite range, a NaN) gets its perm[0]
+// marked for fuse_fallback_kernel; its scores stay unsorted in place.
+// ============================================================================
+template <int BLOCK, int BITS>
+struct BsCfg {
+  static constexpr int kWaves = BLOCK / 64;
+  static constexpr int kRows = (kJsUMax + BLOCK - 1) / BLOCK;
+  static constexpr int kBuckets = 1 << BITS;
+  static constexpr int kMinSub = kBuckets / 16;
+  static constexpr int kMinBase = kBuckets - kMinSub;
+};
+
+template <int NB, int MINBASE, int MINSUB>
+__device__ __forceinline__ uint32_t bs_bucket(double v, uint32_t u, float usub, double smin,
+                                              double delta, uint32_t b0, int sh) {
+  const float x = (float)((v - smin) + delta);
+  const uint32_t above = (uint32_t)(MINBASE - 1) - (((uint32_t)__float_as_uint(x) - b0) >> sh);
+  const uint32_t sub = min((uint32_t)((float)u * usub), (uint32_t)(MINSUB - 1));
+  return v == smin ? (uint32_t)MINBASE + sub : above;
+}
+
+template <int BLOCK, int BITS>
+__global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
+  using Cfg = BsCfg<BLOCK, BITS>;
+  constexpr int ROWS = Cfg::kRows, WAVES = Cfg::kWaves, NB = Cfg::kBuckets;
+  constexpr int MINBASE = Cfg::kMinBase, MINSUB = Cfg::kMinSub;
+  __shared__ double sval[kJsUMax];
+  __shared__ uint16_t su[kJsUMax];
+  __shared__ __attribute__((aligned(16))) uint32_t bk[NB + 4];
+  __shared__ uint32_t s_wtot[WAVES];
+  __shared__ unsigned long long s_kmin, s_kmax;
+  __shared__ int s_nan, s_bmax;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // block -> (query, method slot): slot-major groups of 8 queries (fuse_kernel's map)
+  const int M = __popc(p.methods);
+  const int64_t bid = block_id();
+  const int64_t grp8 = bid >> 3;
+  const int64_t q = (grp8 / M) * 8 + (bid & 7);
+  const int ms = (int)(grp8 % M);
+  if (q >= p.n_queries) return;
+  const int U = p.union_count[q];
+  const int64_t base = p.list_off[q * p.R];
+  if (U < 1 || U > kJsUMax) return;  // error / fuse_large_kernel's
+  QF_STAMP_INIT();
+  double* io = p.fused + (int64_t)ms * p.out_stride + base;
+  uint16_t* outp = p.perm + (int64_t)ms * p.out_stride + base;
+  const int rows = (U + BLOCK - 1) / BLOCK;
+  double v[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {  // every row's load in flight before the first use
+    const int u = (wid * rows + j) * 64 + lane;
+    v[j] = (j < rows && u < U) ? io[u] : 0.0;
+  }
+  if (tid == 0) {
+    s_kmin = ~0ull;
+    s_kmax = 0ull;
+    s_nan = 0;
+    s_bmax = 0;
+  }
+  for (int i = tid * 4; i < NB + 4; i += BLOCK * 4) *(uint4*)&bk[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  QF_STAMP(0);
+  {  // score range: f64 min / max (a NaN flagged), folded keys as join_sort_kernel
+    double vmn = INFINITY, vmx = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = (wid * rows + j) * 64 + lane;
+      if (j < rows && u < U) {
+        vmn = fmin(vmn, v[j]);
+        vmx = fmax(vmx, v[j]);
+        nan |= v[j] != v[j];
+      }
+    }
+    vmn = wave_min_f64_dpp(vmn);
+    vmx = wave_max_f64_dpp(vmx);
+    const bool anynan = ballot(nan) != 0ull;
+    if (lane == 63) {
+      atomicMin(&s_kmin, (unsigned long long)~f64_asc_key(vmx));
+      atomicMax(&s_kmax, (unsigned long long)~f64_asc_key(vmn));
+      if (anynan) s_nan = 1;
+    }
+  }
+  __syncthreads();
+  QF_STAMP(1);
+  const uint64_t kmin = s_kmin, kmax = s_kmax;
+  const bool nan = s_nan != 0;
+  if (kmax == kmin && !nan) {  // every score equal: first-seen order, scores in place
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = (wid * rows + j) * 64 + lane;
+      if (j < rows && u < U) __builtin_nontemporal_store((uint16_t)u, &outp[u]);
+    }
+    return;
+  }
+  const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
+  const double rng = smax - smin;
+  const double delta = rng * 0x1p-5;
+  const float ftop = (float)(rng + delta);
+  if (!(isfinite(rng) && isfinite(ftop) && delta > 0.0) || nan) {  // uniform
+    if (tid == 0) outp[0] = kJsUnsorted;
+    return;
+  }
+  const uint32_t b0 = __float_as_uint((float)delta);
+  const uint32_t span = __float_as_uint(ftop) - b0;
+  int bsh = span >= (uint32_t)NB ? (32 - __clz((int)span)) - BITS : 0;
+  if ((span >> bsh) >= (uint32_t)MINBASE) ++bsh;
+  const float usub = (float)MINSUB / (float)U;
+  // ---- 1. count ------------------------------------------------------------------
+  uint32_t ws[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    ws[j] = 0u;
+    const int u = (wid * rows + j) * 64 + lane;
+    if (j < rows && u < U) {
+      const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, usub, smin, delta,
+                                                        b0, bsh);
+      ws[j] = w | (atomicAdd(&bk[w], 1u) << 16);
+    }
+  }
+  QF_STAMP(2);
+  __syncthreads();
+  QF_STAMP(3);
+  // ---- 2. exclusive scan of the counters, largest bucket ---------------------------
+  {
+    constexpr int kPer = NB / BLOCK;
+    static_assert(kPer % 4 == 0, "uint4 counter loads");
+    uint32_t c[kPer], tot = 0u, mx = 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; i += 4) {
+      const uint4 x4 = *(const uint4*)&bk[tid * kPer + i];
+      c[i] = x4.x; c[i + 1] = x4.y; c[i + 2] = x4.z; c[i + 3] = x4.w;
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      mx = max(mx, c[i]);
+      const uint32_t x = c[i];
+      c[i] = tot;
+      tot += x;
+    }
+    const uint32_t incl = wave_incl_scan_dpp(tot);
+    if (lane == 63) s_wtot[wid] = incl;
+    mx = (uint32_t)wave_max_u64_dpp(mx);
+    if (lane == 63) atomicMax(&s_bmax, (int)mx);
+    __syncthreads();
+    uint32_t pre = incl - tot;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w)
+      if (w < wid) pre += s_wtot[w];
+#pragma unroll
+    for (int i = 0; i < kPer; i += 4)
+      *(uint4*)&bk[tid * kPer + i] =
+          make_uint4(pre + c[i], pre + c[i + 1], pre + c[i + 2], pre + c[i + 3]);
+    if (tid == 0) bk[NB] = (uint32_t)U;
+  }
+  __syncthreads();
+  QF_STAMP(4);
+  if (s_bmax > kJsBucketMax) {  // uniform
+    if (tid == 0) outp[0] = kJsUnsorted;
+    return;
+  }
+  // ---- 3. scatter --------------------------------------------------------------------
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = (wid * rows + j) * 64 + lane;
+    if (j < rows && u < U) {
+      const uint32_t pos = bk[ws[j] & 0xFFFFu] + (ws[j] >> 16);
+      sval[pos] = v[j];
+      su[pos] = (uint16_t)u;
+    }
+  }
+  __syncthreads();
+  QF_STAMP(5);
+  // ---- 4. rank inside the bucket, outputs in place -------------------------------------
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = (wid * rows + j) * 64 + lane;
+    if (j < rows && i < U) {
+      const double vi = sval[i];
+      const uint32_t ui = su[i];
+      const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(vi, ui, usub, smin, delta, b0, bsh);
+      const uint32_t lo = bk[w], hi = bk[w + 1];
+      uint32_t before = 0u;
+      uint32_t k = hi - lo > 1u ? lo : hi;  // a bucket of one: nothing to count
+      for (; k + 1 < hi; k += 2) {
+        const double v0 = sval[k], v1 = sval[k + 1];
+        const uint32_t u0 = su[k], u1 = su[k + 1];
+        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui))) +
+                  (uint32_t)((v1 > vi) | ((v1 == vi) & (u1 < ui)));
+      }
+      if (k < hi) {
+        const double v0 = sval[k];
+        const uint32_t u0 = su[k];
+        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui)));
+      }
+      const uint32_t P = lo + before;
+      __builtin_nontemporal_store((uint16_t)ui, &outp[P]);
+      __builtin_nontemporal_store(vi, &io[P]);
+    }
+  }
+  QF_STAMP(6);
+}
+
+// The (query, method) pairs join_sort_kernel left unsorted (a bucket above
+// kJsBucketMax, or a non-finite score range): a persistent grid like
+// fuse_large_kernel's lists the marked pairs of its stride and sorts them with
+// the LSD window sort (sort_one), which overwrites the marker.
+template <class C>
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_fallback_kernel(FuseParams p) {
+  __shared__ SortShared<C> sh;
+  __shared__ int s_list[C::kBlock];
+  __shared__ int s_n;
+  const int tid = threadIdx.x;
+  const int M = __popc(p.methods);
+  const int64_t pairs = p.n_queries * M;
+  const int64_t span = (int64_t)gridDim.x * C::kBlock;
+  for (int64_t c0 = 0; c0 < pairs; c0 += span) {
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    const int64_t idx = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
+    if (idx < pairs) {
+      const int64_t q = idx / M;
+      const int ms = (int)(idx % M);
+      const int U = p.union_count[q];
+      if (U > 1 && U <= kJsUMax &&
+          p.perm[(int64_t)ms * p.out_stride + p.list_off[q * p.R]] == kJsUnsorted)
+        s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
+    }
+    __syncthreads();
+    const int n = s_n;
+    for (int t = 0; t < n; ++t) {
+      const int64_t id = c0 + s_list[t];
+      const int64_t q = id / M;
+      const int ms = (int)(id % M);
+      sort_one<C>(p, sh, ms, p.union_count[q], p.list_off[q * p.R], false);
+      __syncthreads();
+    }
+  }
+}
 
 // ============================================================================
 // join_sort_xl_kernel — queries beyond the LDS join (JoinXL::kNMax < N <= 65,535,
@@ -1317,6 +2024,7 @@ using SortS = SortCfg<256, 4, 4>;     // U <= 1024
 using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
 using SortXL = SortCfg<1024, 10, 2>;  // U <= 10240
+using SortFb = SortCfg<512, 6, 4>;    // join_sort_kernel's fallback (U <= 3072; no spills)
 
 int fuse_max_entries() { return kXlNMax; }
 
@@ -1369,9 +2077,55 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
   return hipGetLastError();
 }
 
+// Blocks per query of the fused join + sort (development switch: QF_JS_BLOCK=0
+// turns it off, 512 / 1024 pick the workgroup size).
+static int js_block() {
+  static const int b = [] {
+    const char* e = std::getenv("QF_JS_BLOCK");
+    return e ? std::atoi(e) : 11;
+  }();
+  return b;
+}
+
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
   void* ws = nullptr;
   hipError_t e = hipSuccess;
+  const int jsb = js_block();
+  if ((jsb == 11 || jsb == 12) && p.R <= kRMax && max_entries <= JoinXL::kNMax &&
+      max_entries > JoinS::kNMax && !(p.methods & QF_LEARNED)) {
+    // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
+    if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
+    else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
+    else launch_join<JoinXL>(p, kind, st);
+    const int M = __builtin_popcount((unsigned)p.methods);
+    const dim3 g = grid_for((p.n_queries + 7) / 8 * 8 * M);
+    if (jsb == 11) hipLaunchKernelGGL((bucket_sort_kernel<512, 11>), g, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((bucket_sort_kernel<512, 12>), g, dim3(512), 0, st, p);
+    launch_sort_large<SortL>(p, kJsUMax + 1, st, 1);
+    if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
+    const int64_t pairs = p.n_queries * M;
+    const int64_t gf = pairs < 1024 ? pairs : 1024;
+    hipLaunchKernelGGL((fuse_fallback_kernel<SortFb>), dim3((unsigned)(gf > 0 ? gf : 1)),
+                       dim3(SortFb::kBlock), 0, st, p);
+    return hipGetLastError();
+  }
+  if (kind == 1 && p.R <= kRMax && max_entries <= 5120 && max_entries > JoinS::kNMax &&
+      (p.methods & ~kJsMethods) == 0 && (jsb == 512 || jsb == 1024)) {
+    // one kernel: join + sums + sorts in LDS; unions above kJsUMax (stored unsorted)
+    // are sorted by fuse_large_kernel, which costs a few microseconds when none exist
+    if (jsb == 512)
+      hipLaunchKernelGGL((join_sort_kernel<512>), grid_for(p.n_queries), dim3(512), 0, st, p);
+    else
+      hipLaunchKernelGGL((join_sort_kernel<1024>), grid_for(p.n_queries), dim3(1024), 0, st, p);
+    launch_sort_large<SortL>(p, kJsUMax + 1, st, 1);
+    {
+      const int64_t pairs = p.n_queries * __builtin_popcount((unsigned)p.methods);
+      const int64_t g = pairs < 1024 ? pairs : 1024;  // 4 per CU, resident together
+      hipLaunchKernelGGL((fuse_fallback_kernel<SortFb>), dim3((unsigned)(g > 0 ? g : 1)),
+                         dim3(SortFb::kBlock), 0, st, p);
+    }
+    return hipGetLastError();
+  }
   if (p.R > kRMax) {
     // more runs than the LDS join's masks hold: every query takes the workspace join
     e = launch_xl(p, kind, max_entries < 1 ? 1 : max_entries, -1, SortXL::kUMax, st, &ws);

@@ -8,14 +8,16 @@ import torch
 import bench
 
 args = bench.parse()
-args.queries = 64
+args.queries = 200
+args.gather_topk = 0
 world, rank, dev = 1, 0, torch.device("cuda", 0)
 p = bench.Pipeline(args, world, rank, dev)
 p.step()
 torch.cuda.synchronize()
 uc = p.out.union_count.cpu().numpy()
 off = p.off.cpu().numpy()
-out = {"uc": uc, "off": off}
+out = {"uc": uc, "off": off, "micro": p.micro.cpu().numpy(),
+       "docid": p.docid.cpu().numpy(), "w": p.w.cpu().numpy()}
 for m, name in enumerate(bench.METHODS):
     out[name] = p.out.fused[m].cpu().numpy()
     out[name + "_perm"] = p.out.perm[m].cpu().numpy()
