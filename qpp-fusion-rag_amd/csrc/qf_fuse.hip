@@ -1472,10 +1472,12 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   constexpr int MINBASE = Cfg::kMinBase, MINSUB = Cfg::kMinSub;
   __shared__ double sval[kJsUMax];
   __shared__ uint16_t su[kJsUMax];
-  __shared__ __attribute__((aligned(16))) uint32_t bk[NB + 4];
-  __shared__ uint32_t s_wtot[WAVES];
-  __shared__ unsigned long long s_kmin, s_kmax;
-  __shared__ int s_nan, s_bmax;
+  // bucket counters, then starts: u16 (U <= kJsUMax), two per word
+  __shared__ __attribute__((aligned(16))) uint32_t bkw[NB / 2 + 8];
+  const uint16_t* bk = (const uint16_t*)bkw;
+  __shared__ uint32_t s_wtot[WAVES], s_wmax[WAVES];
+  __shared__ double s_wmin_v[WAVES], s_wmax_v[WAVES];
+  __shared__ int s_wnan[WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // block -> (query, method slot): slot-major groups of 8 queries (fuse_kernel's map)
   const int M = __popc(p.methods);
@@ -1497,16 +1499,10 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     const int u = (wid * rows + j) * 64 + lane;
     v[j] = (j < rows && u < U) ? io[u] : 0.0;
   }
-  if (tid == 0) {
-    s_kmin = ~0ull;
-    s_kmax = 0ull;
-    s_nan = 0;
-    s_bmax = 0;
-  }
-  for (int i = tid * 4; i < NB + 4; i += BLOCK * 4) *(uint4*)&bk[i] = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
+  for (int i = tid * 4; i < NB / 2 + 8; i += BLOCK * 4)
+    *(uint4*)&bkw[i] = make_uint4(0u, 0u, 0u, 0u);
   QF_STAMP(0);
-  {  // score range: f64 min / max (a NaN flagged), folded keys as join_sort_kernel
+  {  // score range: f64 min / max (a NaN flagged); per-wave results, one barrier
     double vmn = INFINITY, vmx = -INFINITY;
     bool nan = false;
 #pragma unroll
@@ -1522,15 +1518,24 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     vmx = wave_max_f64_dpp(vmx);
     const bool anynan = ballot(nan) != 0ull;
     if (lane == 63) {
-      atomicMin(&s_kmin, (unsigned long long)~f64_asc_key(vmx));
-      atomicMax(&s_kmax, (unsigned long long)~f64_asc_key(vmn));
-      if (anynan) s_nan = 1;
+      s_wmin_v[wid] = vmn;
+      s_wmax_v[wid] = vmx;
+      s_wnan[wid] = anynan ? 1 : 0;
     }
   }
-  __syncthreads();
+  __syncthreads();  // also orders the counters' zeroing before the count
   QF_STAMP(1);
-  const uint64_t kmin = s_kmin, kmax = s_kmax;
-  const bool nan = s_nan != 0;
+  double gmn = s_wmin_v[0], gmx = s_wmax_v[0];
+  int gnan = s_wnan[0];
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w) {
+    gmn = fmin(gmn, s_wmin_v[w]);
+    gmx = fmax(gmx, s_wmax_v[w]);
+    gnan |= s_wnan[w];
+  }
+  // folded keys as join_sort_kernel: kmin <-> the largest score, -0.0 == +0.0
+  const uint64_t kmin = ~f64_asc_key(gmx), kmax = ~f64_asc_key(gmn);
+  const bool nan = gnan != 0;
   if (kmax == kmin && !nan) {  // every score equal: first-seen order, scores in place
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
@@ -1561,21 +1566,24 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     if (j < rows && u < U) {
       const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, usub, smin, delta,
                                                         b0, bsh);
-      ws[j] = w | (atomicAdd(&bk[w], 1u) << 16);
+      const uint32_t hs = (w & 1u) * 16u;
+      ws[j] = w | (((atomicAdd(&bkw[w >> 1], 1u << hs) >> hs) & 0xFFFFu) << 16);
     }
   }
   QF_STAMP(2);
   __syncthreads();
   QF_STAMP(3);
   // ---- 2. exclusive scan of the counters, largest bucket ---------------------------
+  bool big;
   {
-    constexpr int kPer = NB / BLOCK;
-    static_assert(kPer % 4 == 0, "uint4 counter loads");
+    constexpr int kPer = NB / BLOCK;  // u16 counters per thread
+    static_assert(kPer % 8 == 0 || kPer == 4, "uint4 / uint2 counter loads");
     uint32_t c[kPer], tot = 0u, mx = 0u;
 #pragma unroll
-    for (int i = 0; i < kPer; i += 4) {
-      const uint4 x4 = *(const uint4*)&bk[tid * kPer + i];
-      c[i] = x4.x; c[i + 1] = x4.y; c[i + 2] = x4.z; c[i + 3] = x4.w;
+    for (int i = 0; i < kPer; i += 2) {
+      const uint32_t x = bkw[(tid * kPer + i) / 2];
+      c[i] = x & 0xFFFFu;
+      c[i + 1] = x >> 16;
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -1587,21 +1595,24 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     const uint32_t incl = wave_incl_scan_dpp(tot);
     if (lane == 63) s_wtot[wid] = incl;
     mx = (uint32_t)wave_max_u64_dpp(mx);
-    if (lane == 63) atomicMax(&s_bmax, (int)mx);
+    if (lane == 63) s_wmax[wid] = mx;
     __syncthreads();
     uint32_t pre = incl - tot;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w)
       if (w < wid) pre += s_wtot[w];
+    uint32_t bmax = 0u;
 #pragma unroll
-    for (int i = 0; i < kPer; i += 4)
-      *(uint4*)&bk[tid * kPer + i] =
-          make_uint4(pre + c[i], pre + c[i + 1], pre + c[i + 2], pre + c[i + 3]);
-    if (tid == 0) bk[NB] = (uint32_t)U;
+    for (int w = 0; w < WAVES; ++w) bmax = max(bmax, s_wmax[w]);
+    big = bmax > (uint32_t)kJsBucketMax;
+#pragma unroll
+    for (int i = 0; i < kPer; i += 2)
+      bkw[(tid * kPer + i) / 2] = (pre + c[i]) | ((pre + c[i + 1]) << 16);
+    if (tid == 0) bkw[NB / 2] = (uint32_t)U;
   }
   __syncthreads();
   QF_STAMP(4);
-  if (s_bmax > kJsBucketMax) {  // uniform
+  if (big) {  // uniform
     if (tid == 0) outp[0] = kJsUnsorted;
     return;
   }
@@ -2082,7 +2093,7 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
 static int js_block() {
   static const int b = [] {
     const char* e = std::getenv("QF_JS_BLOCK");
-    return e ? std::atoi(e) : 11;
+    return e ? std::atoi(e) : 12;
   }();
   return b;
 }
@@ -2091,7 +2102,7 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
   void* ws = nullptr;
   hipError_t e = hipSuccess;
   const int jsb = js_block();
-  if ((jsb == 11 || jsb == 12) && p.R <= kRMax && max_entries <= JoinXL::kNMax &&
+  if ((jsb == 11 || jsb == 12 || jsb == 13) && p.R <= kRMax && max_entries <= JoinXL::kNMax &&
       max_entries > JoinS::kNMax && !(p.methods & QF_LEARNED)) {
     // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
     if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
@@ -2100,7 +2111,8 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     const int M = __builtin_popcount((unsigned)p.methods);
     const dim3 g = grid_for((p.n_queries + 7) / 8 * 8 * M);
     if (jsb == 11) hipLaunchKernelGGL((bucket_sort_kernel<512, 11>), g, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((bucket_sort_kernel<512, 12>), g, dim3(512), 0, st, p);
+    else if (jsb == 12) hipLaunchKernelGGL((bucket_sort_kernel<512, 12>), g, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((bucket_sort_kernel<512, 13>), g, dim3(512), 0, st, p);
     launch_sort_large<SortL>(p, kJsUMax + 1, st, 1);
     if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
     const int64_t pairs = p.n_queries * M;
