@@ -846,9 +846,9 @@ void join_kernel(FuseParams p) {
   __shared__ JoinShared<C, KIND> sh;
   const int64_t q = block_id();
   if (q >= p.n_queries) return;
-  QF_STAMP_INIT();
   const int N = join_groups<C, KIND>(p, sh, q);
   if (N < 0) return;
+  QF_STAMP_INIT();
   store_unsorted_sums<C, KIND>(p, sh, N);
   if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : sh.U;
   QF_STAMP(14);
@@ -1077,23 +1077,25 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 //
 // Per method, a bucket sort on a monotone key:
 //   w(v) = (bits(float((v - smin) + delta)) - bits(float(delta))) >> sh
-//   (delta = (smax - smin) / 32): every rounding in it is monotone and the bits
-//   of a non-negative float are ordered, so w is non-decreasing in v and equal
-//   scores (-0.0 and +0.0 included) share a bucket.  In float bits it resolves
-//   scores relative to their distance from smin — ~4,096 buckets over ~5
-//   binades above delta — which suits the skewed fused distributions (most
-//   documents sit in one list, near the bottom).
+//   (delta = (smax - smin) / 4096): every rounding in it is monotone and the
+//   bits of a non-negative float are ordered, so w is non-decreasing in v and
+//   equal scores (-0.0 and +0.0 included) share a bucket.  In float bits it
+//   resolves scores relative to their distance from smin — ~3,840 buckets over
+//   ~12 binades above delta — which suits the skewed fused distributions (most
+//   documents sit in one list near the bottom; a run with a tiny weight packs
+//   its documents just above smin).  The minimum itself (shared by hundreds of
+//   documents when a run has weight 0) gets 256 buckets split by u.
 //   1. count: one returning LDS atomic per item on its bucket (order inside a
 //      bucket is arbitrary);
-//   2. exclusive scan of the kJsBuckets counters (and the largest bucket);
+//   2. exclusive scan of the bucket counters (and the largest bucket);
 //   3. scatter value + u to start[w] + slot;
 //   4. the final position of an item is its bucket's start + the number of
 //      items of its bucket that precede it in (score descending, u ascending)
 //      order — the stable sort's order, counted exactly with f64 compares.
-// Its cost per item is the size of its bucket (measured on C2: 2-4 on average).
-// A bucket above kJsBucketMax (long runs of equal or near-equal scores) or a
-// non-finite score range sends the method through the LSD window sort of
-// sort_desc instead (the same order), with the scores staged in LDS.
+// Its cost per item is the size of its bucket (C2 with QPP or random weights:
+// 2-2.5 on average, largest buckets ~10-60; tools/bucket_stats.py).  A bucket
+// above kJsBucketMax or a non-finite / NaN score range leaves the (query,
+// method) to fuse_fallback_kernel's LSD window sort (the same order).
 // Unions above kJsUMax are stored unsorted for fuse_large_kernel.
 // ============================================================================
 constexpr int kJsBits = 12;
@@ -1305,7 +1307,7 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
     }
     const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
     const double rng = smax - smin;
-    const double delta = rng * 0x1p-5;
+    const double delta = rng * 0x1p-12;
     const float ftop = (float)(rng + delta);
     // a finite range without NaN (a NaN's key lies beyond +-inf's) and a positive
     // delta: the bucket sort; otherwise fuse_fallback_kernel's LSD window sort
@@ -1501,7 +1503,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   }
   for (int i = tid * 4; i < NB / 2 + 8; i += BLOCK * 4)
     *(uint4*)&bkw[i] = make_uint4(0u, 0u, 0u, 0u);
-  QF_STAMP(0);
+  QF_STAMP(8);
   {  // score range: f64 min / max (a NaN flagged); per-wave results, one barrier
     double vmn = INFINITY, vmx = -INFINITY;
     bool nan = false;
@@ -1524,7 +1526,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     }
   }
   __syncthreads();  // also orders the counters' zeroing before the count
-  QF_STAMP(1);
+  QF_STAMP(9);
   double gmn = s_wmin_v[0], gmx = s_wmax_v[0];
   int gnan = s_wnan[0];
 #pragma unroll
@@ -1546,7 +1548,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   }
   const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
   const double rng = smax - smin;
-  const double delta = rng * 0x1p-5;
+  const double delta = rng * 0x1p-12;
   const float ftop = (float)(rng + delta);
   if (!(isfinite(rng) && isfinite(ftop) && delta > 0.0) || nan) {  // uniform
     if (tid == 0) outp[0] = kJsUnsorted;
@@ -1570,9 +1572,9 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
       ws[j] = w | (((atomicAdd(&bkw[w >> 1], 1u << hs) >> hs) & 0xFFFFu) << 16);
     }
   }
-  QF_STAMP(2);
+  QF_STAMP(10);
   __syncthreads();
-  QF_STAMP(3);
+  QF_STAMP(11);
   // ---- 2. exclusive scan of the counters, largest bucket ---------------------------
   bool big;
   {
@@ -1611,7 +1613,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     if (tid == 0) bkw[NB / 2] = (uint32_t)U;
   }
   __syncthreads();
-  QF_STAMP(4);
+  QF_STAMP(12);
   if (big) {  // uniform
     if (tid == 0) outp[0] = kJsUnsorted;
     return;
@@ -1627,7 +1629,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     }
   }
   __syncthreads();
-  QF_STAMP(5);
+  QF_STAMP(13);
   // ---- 4. rank inside the bucket, outputs in place -------------------------------------
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
@@ -1655,7 +1657,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
       __builtin_nontemporal_store(vi, &io[P]);
     }
   }
-  QF_STAMP(6);
+  QF_STAMP(15);
 }
 
 // The (query, method) pairs join_sort_kernel left unsorted (a bucket above

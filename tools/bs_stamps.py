@@ -1,8 +1,9 @@
 """Phase cycles of bucket_sort_kernel (QF_STAMPS build; development tool).
 
-Slots per (query, method) workgroup (thread 0's s_memtime deltas): 0 load +
-zero + barrier, 1 range + barrier, 2 count, 3 barrier, 4 scan + barriers,
-5 scatter + barrier, 6 rank + output.  The join kernel's slots are not read.
+Slots per (query, method) workgroup (thread 0's s_memtime deltas): 8 load +
+zero, 9 range + barrier, 10 count, 11 barrier, 12 scan + barriers, 13 scatter +
+barrier, 15 rank + output; the join kernel's (per query): 3-7 join_groups'
+phases, 14 sums + unsorted writes.
 """
 import ctypes as C
 import json
@@ -23,8 +24,10 @@ lib = _lib.lib()
 lib.qf_debug_stamps.restype = C.c_int
 lib.qf_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
 NB, NS = 32768, 16
-names = {0: "load+zero+bar", 1: "range+bar", 2: "count", 3: "bar(count)", 4: "scan+bars",
-         5: "scatter+bar", 6: "rank+out"}
+names = {8: "load+zero", 9: "range+bar", 10: "count", 11: "bar(count)", 12: "scan+bars",
+         13: "scatter+bar", 15: "rank+out"}
+jnames = {3: "join:load+init", 4: "join:insert", 5: "join:reps+scans", 6: "join:placement",
+          7: "join:groups", 14: "join:sums+write"}
 Q, R, K = 3452, 5, 1000
 dev = torch.device("cuda", 0)
 off, docid, raw = engine.synth_runs(0, Q, R, K)
@@ -38,8 +41,11 @@ for rep in range(2):
     lib.qf_debug_stamps(buf.ctypes.data_as(C.c_void_p), NB * NS, 1)
 nb = min(NB, ((Q + 7) // 8) * 8 * len(M))
 st = buf.reshape(NB, NS)[:nb].astype(np.float64)
-st = st[st[:, 6] > 0]
+st = st[st[:, 15] > 0]
 out = {v: round(float(st[:, k].mean())) for k, v in names.items()}
+js = buf.reshape(NB, NS)[:Q].astype(np.float64)
+out.update({v: round(float(js[:, k].mean())) for k, v in jnames.items()})
+out["join_total"] = round(float(js[:, list(jnames)].sum(1).mean()))
 out["total"] = round(float(st[:, list(names)].sum(1).mean()))
 out["blocks"] = int(len(st))
 Path("gpurun_out").mkdir(exist_ok=True)
