@@ -1458,13 +1458,14 @@ struct BsCfg {
   static constexpr int kMinBase = kBuckets - kMinSub;
 };
 
+// The bucket of a score: join_sort_kernel's js_bucket, with the minimum's
+// sub-bucket u >> ush (ush chosen so that U - 1 >> ush < MINSUB).
 template <int NB, int MINBASE, int MINSUB>
-__device__ __forceinline__ uint32_t bs_bucket(double v, uint32_t u, float usub, double smin,
+__device__ __forceinline__ uint32_t bs_bucket(double v, uint32_t u, int ush, double smin,
                                               double delta, uint32_t b0, int sh) {
   const float x = (float)((v - smin) + delta);
   const uint32_t above = (uint32_t)(MINBASE - 1) - (((uint32_t)__float_as_uint(x) - b0) >> sh);
-  const uint32_t sub = min((uint32_t)((float)u * usub), (uint32_t)(MINSUB - 1));
-  return v == smin ? (uint32_t)MINBASE + sub : above;
+  return v == smin ? (uint32_t)MINBASE + (u >> ush) : above;
 }
 
 template <int BLOCK, int BITS>
@@ -1558,20 +1559,23 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   const uint32_t span = __float_as_uint(ftop) - b0;
   int bsh = span >= (uint32_t)NB ? (32 - __clz((int)span)) - BITS : 0;
   if ((span >> bsh) >= (uint32_t)MINBASE) ++bsh;
-  const float usub = (float)MINSUB / (float)U;
+  int ush = 0;  // U - 1 >> ush < MINSUB
+  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
   // ---- 1. count ------------------------------------------------------------------
-  uint32_t ws[ROWS];
+  // every row's atomic issued before any result is used; rows past U add 0 to
+  // bucket 0 (no branches around the atomics, one wait)
+  uint32_t ws[ROWS], old[ROWS];
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
-    ws[j] = 0u;
     const int u = (wid * rows + j) * 64 + lane;
-    if (j < rows && u < U) {
-      const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, usub, smin, delta,
-                                                        b0, bsh);
-      const uint32_t hs = (w & 1u) * 16u;
-      ws[j] = w | (((atomicAdd(&bkw[w >> 1], 1u << hs) >> hs) & 0xFFFFu) << 16);
-    }
+    const bool ok = j < rows && u < U;
+    ws[j] = ok ? bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, ush, smin, delta, b0, bsh)
+               : 0u;
+    old[j] = atomicAdd(&bkw[ws[j] >> 1], ok ? 1u << ((ws[j] & 1u) * 16u) : 0u);
   }
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+    ws[j] |= ((old[j] >> ((ws[j] & 1u) * 16u)) & 0xFFFFu) << 16;
   QF_STAMP(10);
   __syncthreads();
   QF_STAMP(11);
@@ -1637,7 +1641,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     if (j < rows && i < U) {
       const double vi = sval[i];
       const uint32_t ui = su[i];
-      const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(vi, ui, usub, smin, delta, b0, bsh);
+      const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(vi, ui, ush, smin, delta, b0, bsh);
       const uint32_t lo = bk[w], hi = bk[w + 1];
       uint32_t before = 0u;
       uint32_t k = hi - lo > 1u ? lo : hi;  // a bucket of one: nothing to count
