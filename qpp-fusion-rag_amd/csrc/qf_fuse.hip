@@ -31,6 +31,9 @@
 
 namespace qf {
 
+#ifndef QF_JOIN_REV
+#define QF_JOIN_REV 0
+#endif
 constexpr int kRMax = 16;    // runs per query in the LDS join (u16 retriever masks)
 constexpr int kRMaxXl = 32;  // in the workspace kernel (u32 masks)
 constexpr int kNMethods = 9;  // method bits QF_COMBSUM .. QF_WRRF_MUL
@@ -844,7 +847,11 @@ template <class C, int KIND>
 __global__ __launch_bounds__(C::kBlock, KIND == 1 ? C::kMinWaves : (C::kMinWaves < 4 ? C::kMinWaves : 4))
 void join_kernel(FuseParams p) {
   __shared__ JoinShared<C, KIND> sh;
+#if QF_JOIN_REV
+  const int64_t q = p.n_queries - 1 - block_id();
+#else
   const int64_t q = block_id();
+#endif
   if (q >= p.n_queries) return;
   const int N = join_groups<C, KIND>(p, sh, q);
   if (N < 0) return;
@@ -1449,6 +1456,9 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
 // order (a bucket above kJsBucketMax, a non-finite range, a NaN) gets its perm[0]
 // marked for fuse_fallback_kernel; its scores stay unsorted in place.
 // ============================================================================
+#ifndef QF_BS_REV
+#define QF_BS_REV 1
+#endif
 template <int BLOCK, int BITS>
 struct BsCfg {
   static constexpr int kWaves = BLOCK / 64;
@@ -1482,11 +1492,18 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   __shared__ double s_wmin_v[WAVES], s_wmax_v[WAVES];
   __shared__ int s_wnan[WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // block -> (query, method slot): slot-major groups of 8 queries (fuse_kernel's map)
+  // block -> (query, method slot): slot-major groups of 8 queries (fuse_kernel's
+  // map: query q on XCD q % 8, where the join wrote it), the groups in reverse:
+  // the join's last-written scores are the likeliest still in the L2 /
+  // Infinity Cache
   const int M = __popc(p.methods);
   const int64_t bid = block_id();
   const int64_t grp8 = bid >> 3;
+#if QF_BS_REV
+  const int64_t q = ((p.n_queries + 7) / 8 - 1 - grp8 / M) * 8 + (bid & 7);
+#else
   const int64_t q = (grp8 / M) * 8 + (bid & 7);
+#endif
   const int ms = (int)(grp8 % M);
   if (q >= p.n_queries) return;
   const int U = p.union_count[q];
@@ -1634,10 +1651,19 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   }
   __syncthreads();
   QF_STAMP(13);
-  // ---- 4. rank inside the bucket, outputs in place -------------------------------------
+  // ---- 4. rank inside the bucket, in position order --------------------------------------
+  // (positions follow the bucket order, so the outputs below land nearly in
+  // place: a wave's stores cover a few lines instead of 64 scattered ones.
+  // Every row's position before any global store: a store in flight would make
+  // the next row's loop wait for it.)
+  uint32_t P[ROWS], uo[ROWS];
+  double vo[ROWS];
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int i = (wid * rows + j) * 64 + lane;
+    P[j] = 0u;
+    uo[j] = 0u;
+    vo[j] = 0.0;
     if (j < rows && i < U) {
       const double vi = sval[i];
       const uint32_t ui = su[i];
@@ -1656,9 +1682,19 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
         const uint32_t u0 = su[k];
         before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui)));
       }
-      const uint32_t P = lo + before;
-      __builtin_nontemporal_store((uint16_t)ui, &outp[P]);
-      __builtin_nontemporal_store(vi, &io[P]);
+      P[j] = lo + before;
+      uo[j] = ui;
+      vo[j] = vi;
+    }
+  }
+  QF_STAMP(2);
+  // ---- 5. outputs ------------------------------------------------------------------------
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = (wid * rows + j) * 64 + lane;
+    if (j < rows && i < U) {
+      __builtin_nontemporal_store((uint16_t)uo[j], &outp[P[j]]);
+      __builtin_nontemporal_store(vo[j], &io[P[j]]);
     }
   }
   QF_STAMP(15);

@@ -2,7 +2,7 @@
 
 Slots per (query, method) workgroup (thread 0's s_memtime deltas): 8 load +
 zero, 9 range + barrier, 10 count, 11 barrier, 12 scan + barriers, 13 scatter +
-barrier, 15 rank + output; the join kernel's (per query): 3-7 join_groups'
+barrier, 2 rank, 15 output; the join kernel's (per query): 3-7 join_groups'
 phases, 14 sums + unsorted writes.
 """
 import ctypes as C
@@ -25,7 +25,7 @@ lib.qf_debug_stamps.restype = C.c_int
 lib.qf_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
 NB, NS = 32768, 16
 names = {8: "load+zero", 9: "range+bar", 10: "count", 11: "bar(count)", 12: "scan+bars",
-         13: "scatter+bar", 15: "rank+out"}
+         13: "scatter+bar", 2: "rank", 15: "out"}
 jnames = {3: "join:load+init", 4: "join:insert", 5: "join:reps+scans", 6: "join:placement",
           7: "join:groups", 14: "join:sums+write"}
 Q, R, K = 3452, 5, 1000
