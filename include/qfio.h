@@ -59,6 +59,12 @@ int qfio_join_lines(const int64_t* off, const char* chars, int64_t n, char* out)
 int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, uint32_t* docid,
                      uint32_t* iter, uint32_t* tag, int64_t* rank, double* score);
 void qfio_runset_free(qfio_runset* rs);
+/* per-row strings of a column given as codes into a table (offsets [m+1] +
+ * bytes): out_off[n+1] (int64, Arrow large_string offsets) always, the bytes
+ * into out_chars when it is not NULL (size: the return value of a first call
+ * with out_chars = NULL).  Returns the byte count, -1 on bad arguments. */
+int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
+                            int64_t n, int64_t* out_off, char* out_chars);
 
 /* Python's f"{x:.6f}" of x into out (>= 400 bytes); returns the length. */
 size_t qfio_format_score(double x, char* out);

@@ -69,6 +69,64 @@ struct Mapped {
 };
 
 
+// A column buffer that is NOT initialised on allocation (the parse writes every
+// element, in parallel, so the pages are first touched by the threads that fill
+// them); large ones are anonymous mappings with transparent huge pages asked for.
+template <class T>
+struct RawArray {
+  T* a = nullptr;
+  size_t n = 0, bytes = 0;
+  bool mapped = false;
+  RawArray() = default;
+  RawArray(const RawArray&) = delete;
+  RawArray& operator=(const RawArray&) = delete;
+  RawArray(RawArray&& o) noexcept { *this = std::move(o); }
+  RawArray& operator=(RawArray&& o) noexcept {
+    if (this != &o) {
+      release();
+      a = o.a; n = o.n; bytes = o.bytes; mapped = o.mapped;
+      o.a = nullptr; o.n = o.bytes = 0; o.mapped = false;
+    }
+    return *this;
+  }
+  ~RawArray() { release(); }
+  void release() {
+    if (a && mapped) munmap((void*)a, bytes);
+    else free(a);
+    a = nullptr;
+    n = bytes = 0;
+  }
+  void resize(size_t m) {  // contents undefined
+    release();
+    n = m;
+    bytes = std::max<size_t>(1, m * sizeof(T));
+    if (bytes >= (size_t)4 << 20) {
+      void* v = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (v != MAP_FAILED) {
+        madvise(v, bytes, MADV_HUGEPAGE);
+        a = (T*)v;
+        mapped = true;
+        return;
+      }
+    }
+    a = (T*)malloc(bytes);
+    if (!a) throw std::bad_alloc();
+  }
+  size_t size() const { return n; }
+  T& operator[](size_t i) { return a[i]; }
+  const T& operator[](size_t i) const { return a[i]; }
+  T* data() { return a; }
+  const T* data() const { return a; }
+};
+
+// A string view that is trivially constructible (rows of the column buffers).
+struct SV {
+  const char* p;
+  size_t n;
+};
+inline std::string_view sv(const SV& v) { return std::string_view(v.p, v.n); }
+inline std::string_view sv(std::string_view v) { return v; }
+
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
 // [-]digits[.digits<=6] that fits int32 micro-units; "-0.000000" (which parses
@@ -128,10 +186,10 @@ size_t count_rows(const char* p, const char* end) {
 
 // Row columns, structure of arrays over all files in file order.
 struct Cols {
-  std::vector<std::string_view> q, d, it, tag;
-  std::vector<int64_t> rank;
-  std::vector<double> score;
-  std::vector<int32_t> micro;
+  RawArray<SV> q, d, it, tag;
+  RawArray<int64_t> rank;
+  RawArray<double> score;
+  RawArray<int32_t> micro;
   void resize(size_t n) {
     q.resize(n); d.resize(n); it.resize(n); tag.resize(n);
     rank.resize(n); score.resize(n); micro.resize(n);
@@ -161,10 +219,10 @@ bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micr
             " in line: " + std::string(line, std::min<size_t>(120, (size_t)(p - line)));
       return false;
     }
-    c.q[o] = f[0];
-    c.it[o] = f[1];
-    c.d[o] = f[2];
-    c.tag[o] = f[5];
+    c.q[o] = SV{f[0].data(), f[0].size()};
+    c.it[o] = SV{f[1].data(), f[1].size()};
+    c.d[o] = SV{f[2].data(), f[2].size()};
+    c.tag[o] = SV{f[5].data(), f[5].size()};
     // rank: [+-]digits (strtoll's accepted form for plain integer text)
     {
       const std::string_view t = f[3];
@@ -201,13 +259,13 @@ inline uint64_t hash_sv(std::string_view v) {  // FNV-1a + avalanche
 
 // Sorted unique strings of `views`, and each view's index among them: hash
 // partitions deduplicated in parallel, then only the distinct strings sorted.
-void intern(const std::vector<std::string_view>& views, std::vector<std::string_view>& uniq,
-            std::vector<uint32_t>& id) {
+template <class Views>
+void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<uint32_t>& id) {
   const size_t n = views.size();
   constexpr int P = 256;
   std::vector<uint64_t> hs(n);
 #pragma omp parallel for schedule(static)
-  for (size_t i = 0; i < n; ++i) hs[i] = hash_sv(views[i]);
+  for (size_t i = 0; i < n; ++i) hs[i] = hash_sv(sv(views[i]));
   // rows of each partition (top 8 bits), in row order
   const int T = std::max(1, omp_get_max_threads());
   std::vector<std::vector<uint32_t>> cnt(T, std::vector<uint32_t>(P, 0));
@@ -252,7 +310,7 @@ void intern(const std::vector<std::string_view>& views, std::vector<std::string_
           break;
         }
         const uint32_t r = uf[u];
-        if (hs[r] == hs[i] && views[r] == views[i]) { local[i] = u; break; }
+        if (hs[r] == hs[i] && sv(views[r]) == sv(views[i])) { local[i] = u; break; }
         h = (h + 1) & (cap - 1);
       }
     }
@@ -274,7 +332,7 @@ void intern(const std::vector<std::string_view>& views, std::vector<std::string_
   std::vector<Key> keys(U);
 #pragma omp parallel for schedule(static)
   for (size_t k = 0; k < U; ++k) {
-    const std::string_view v = views[reps[k]];
+    const std::string_view v = sv(views[reps[k]]);
     unsigned char b[16] = {0};
     memcpy(b, v.data(), std::min<size_t>(16, v.size()));
     uint64_t k1 = 0, k2 = 0;
@@ -287,14 +345,14 @@ void intern(const std::vector<std::string_view>& views, std::vector<std::string_
   __gnu_parallel::sort(keys.begin(), keys.end(), [&](const Key& a, const Key& b) {
     if (a.k1 != b.k1) return a.k1 < b.k1;
     if (a.k2 != b.k2) return a.k2 < b.k2;
-    return views[reps[a.u]] < views[reps[b.u]];
+    return sv(views[reps[a.u]]) < sv(views[reps[b.u]]);
   });
   std::vector<uint32_t> rank(U);
   uniq.resize(U);
 #pragma omp parallel for schedule(static)
   for (size_t k = 0; k < U; ++k) {
     rank[keys[k].u] = (uint32_t)k;
-    uniq[k] = views[reps[keys[k].u]];
+    uniq[k] = sv(views[reps[keys[k].u]]);
   }
   id.resize(n);
 #pragma omp parallel for schedule(static)
@@ -303,12 +361,12 @@ void intern(const std::vector<std::string_view>& views, std::vector<std::string_
 
 // intern() for columns made of long runs of one value (qid, Q0, tag): only the
 // run heads are interned.
-void intern_runs(const std::vector<std::string_view>& views, std::vector<std::string_view>& uniq,
-                 std::vector<uint32_t>& id) {
+template <class Views>
+void intern_runs(const Views& views, std::vector<std::string_view>& uniq, RawArray<uint32_t>& id) {
   const size_t n = views.size();
   std::vector<uint8_t> head(n);
 #pragma omp parallel for schedule(static)
-  for (size_t i = 0; i < n; ++i) head[i] = i == 0 || views[i] != views[i - 1];
+  for (size_t i = 0; i < n; ++i) head[i] = i == 0 || sv(views[i]) != sv(views[i - 1]);
   std::vector<size_t> hix;
   for (size_t i = 0; i < n; ++i)
     if (head[i]) hix.push_back(i);
@@ -317,8 +375,8 @@ void intern_runs(const std::vector<std::string_view>& views, std::vector<std::st
     return;
   }
   std::vector<std::string_view> hv(hix.size());
-  for (size_t k = 0; k < hix.size(); ++k) hv[k] = views[hix[k]];
-  std::vector<uint32_t> hid;
+  for (size_t k = 0; k < hix.size(); ++k) hv[k] = sv(views[hix[k]]);
+  RawArray<uint32_t> hid;
   intern(hv, uniq, hid);
   id.resize(n);
 #pragma omp parallel for schedule(dynamic, 64)
@@ -336,21 +394,32 @@ struct qfio_runset {
   std::vector<std::string_view> qids, docnos, iters, tags;
   // CSR (query-major, run-minor), rows in file order
   std::vector<int64_t> list_off;
-  std::vector<uint32_t> docid;
-  std::vector<double> score;
-  std::vector<int32_t> micro;
-  std::vector<int64_t> rank;
+  RawArray<uint32_t> docid;
+  RawArray<double> score;
+  RawArray<int32_t> micro;
+  RawArray<int64_t> rank;
   bool micro_ok = true;
   bool rank_is_position = true, canonical = true, has_dups = false;
   // per-file rows in file order (for DataFrames): codes and values
   std::vector<int64_t> file_off;  // [n_files + 1]
-  std::vector<uint32_t> row_qid, row_docid, row_iter, row_tag;
-  std::vector<int64_t> row_rank;
-  std::vector<double> row_score;
+  RawArray<uint32_t> row_qid, row_docid, row_iter, row_tag;
+  RawArray<int64_t> row_rank;
+  RawArray<double> row_score;
   ~qfio_runset() {
     for (auto* m : maps) delete m;
   }
 };
+
+// memcpy over the threads (the column copies out of the run set are 0.1-0.3 GB)
+static void pcopy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kChunk = (size_t)8 << 20;
+  const int64_t nc = (int64_t)((bytes + kChunk - 1) / kChunk);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t c = 0; c < nc; ++c) {
+    const size_t a = (size_t)c * kChunk, e = std::min(bytes, a + kChunk);
+    memcpy((char*)dst + a, (const char*)src + a, e - a);
+  }
+}
 
 extern "C" {
 
@@ -432,7 +501,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->micro_ok = micro_bad == 0;
   rs->row_rank = std::move(cols.rank);
   rs->row_score = std::move(cols.score);
-  std::vector<int32_t> row_micro = std::move(cols.micro);
+  RawArray<int32_t> row_micro = std::move(cols.micro);
   // ---- intern qids / docnos / iter / tag ---------------------------------------
   intern_runs(cols.q, rs->qids, rs->row_qid);
   tm.mark("intern qid");
@@ -528,10 +597,10 @@ static void copy_strings(const std::vector<std::string_view>& v, int64_t* off, c
 int qfio_runset_csr(const qfio_runset* rs, int64_t* list_off, uint32_t* docid, double* score,
                     int32_t* micro, int64_t* rank) {
   memcpy(list_off, rs->list_off.data(), rs->list_off.size() * sizeof(int64_t));
-  memcpy(docid, rs->docid.data(), rs->docid.size() * sizeof(uint32_t));
-  memcpy(score, rs->score.data(), rs->score.size() * sizeof(double));
-  memcpy(rank, rs->rank.data(), rs->rank.size() * sizeof(int64_t));
-  if (micro && rs->micro_ok) memcpy(micro, rs->micro.data(), rs->micro.size() * sizeof(int32_t));
+  pcopy(docid, rs->docid.data(), rs->docid.size() * sizeof(uint32_t));
+  pcopy(score, rs->score.data(), rs->score.size() * sizeof(double));
+  pcopy(rank, rs->rank.data(), rs->rank.size() * sizeof(int64_t));
+  if (micro && rs->micro_ok) pcopy(micro, rs->micro.data(), rs->micro.size() * sizeof(int32_t));
   return QFIO_OK;
 }
 
@@ -560,13 +629,44 @@ int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, ui
                      uint32_t* iter, uint32_t* tag, int64_t* rank, double* score) {
   const size_t E = rs->row_qid.size();
   memcpy(file_off, rs->file_off.data(), rs->file_off.size() * sizeof(int64_t));
-  memcpy(qid, rs->row_qid.data(), E * sizeof(uint32_t));
-  memcpy(docid, rs->row_docid.data(), E * sizeof(uint32_t));
-  memcpy(iter, rs->row_iter.data(), E * sizeof(uint32_t));
-  memcpy(tag, rs->row_tag.data(), E * sizeof(uint32_t));
-  memcpy(rank, rs->row_rank.data(), E * sizeof(int64_t));
-  memcpy(score, rs->row_score.data(), E * sizeof(double));
+  pcopy(qid, rs->row_qid.data(), E * sizeof(uint32_t));
+  pcopy(docid, rs->row_docid.data(), E * sizeof(uint32_t));
+  pcopy(iter, rs->row_iter.data(), E * sizeof(uint32_t));
+  pcopy(tag, rs->row_tag.data(), E * sizeof(uint32_t));
+  pcopy(rank, rs->row_rank.data(), E * sizeof(int64_t));
+  pcopy(score, rs->row_score.data(), E * sizeof(double));
   return QFIO_OK;
+}
+
+int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
+                            int64_t n, int64_t* out_off, char* out_chars) {
+  if (n < 0 || !tab_off || (n && (!codes || !out_off))) return -1;
+  // lengths -> offsets (a blocked parallel scan), then the bytes
+  const int T = std::max(1, omp_get_max_threads());
+  std::vector<int64_t> part(T + 1, 0);
+  out_off[0] = 0;
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+    const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+    int64_t s = 0;
+    for (int64_t i = a; i < b; ++i) {
+      s += tab_off[codes[i] + 1] - tab_off[codes[i]];
+      out_off[i + 1] = s;
+    }
+    part[t + 1] = s;
+#pragma omp barrier
+#pragma omp single
+    for (int k = 0; k < nt; ++k) part[k + 1] += part[k];
+    const int64_t add = part[t];
+    for (int64_t i = a; i < b; ++i) out_off[i + 1] += add;
+#pragma omp barrier  // out_off[a] is the previous thread's last offset
+    if (out_chars)
+      for (int64_t i = a; i < b; ++i)
+        memcpy(out_chars + out_off[i], tab_chars + tab_off[codes[i]],
+               (size_t)(out_off[i + 1] - out_off[i]));
+  }
+  return n ? out_off[n] : 0;
 }
 
 void qfio_runset_free(qfio_runset* rs) { delete rs; }

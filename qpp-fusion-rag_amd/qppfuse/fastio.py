@@ -45,6 +45,8 @@ def lib() -> C.CDLL:
         L.qfio_runset_rows.argtypes = [_vp] + [_vp] * 7
         L.qfio_join_lines.restype = C.c_int
         L.qfio_join_lines.argtypes = [_vp, _vp, _i64, _vp]
+        L.qfio_gather_strings.restype = _i64
+        L.qfio_gather_strings.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp]
         L.qfio_runset_free.restype = None
         L.qfio_runset_free.argtypes = [_vp]
         L.qfio_format_score.restype = C.c_size_t
@@ -83,6 +85,34 @@ def _strings(off: np.ndarray, chars: np.ndarray) -> np.ndarray:
     return out
 
 
+def arrow_strings(off: np.ndarray, chars: np.ndarray, codes: np.ndarray):
+    """Per-row strings (codes into the table off/chars) as a pandas ArrowStringArray:
+    the bytes gathered in C++ straight into Arrow large_string buffers, no Python
+    str per row (they are made when an element is read)."""
+    import pyarrow as pa
+    codes = np.ascontiguousarray(codes, np.uint32)
+    n = len(codes)
+    out_off = np.empty(n + 1, np.int64)
+    L = lib()
+    nb = L.qfio_gather_strings(_p(off), _p(chars), _p(codes), n, _p(out_off), None)
+    if nb < 0:
+        raise ValueError("gather_strings: bad arguments")
+    buf = np.empty(max(int(nb), 1), np.uint8)
+    L.qfio_gather_strings(_p(off), _p(chars), _p(codes), n, _p(out_off), _p(buf))
+    arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(out_off), pa.py_buffer(buf[:nb]))
+    return pd.arrays.ArrowStringArray(pa.chunked_array([arr]))
+
+
+def frame_strings() -> str:
+    """String columns of the frames load_runs returns: "arrow" (default; pandas'
+    string[pyarrow], the dtype pandas >= 3 gives read_csv text by default) or
+    "object" (Python str objects, pandas 2's read_csv dtype); QPPFUSE_FRAME_STRINGS."""
+    v = os.environ.get("QPPFUSE_FRAME_STRINGS", "arrow")
+    if v not in ("arrow", "object"):
+        raise ValueError(f"QPPFUSE_FRAME_STRINGS must be 'arrow' or 'object', not {v!r}")
+    return v
+
+
 def format_score(x: float) -> str:
     buf = C.create_string_buffer(400)
     n = lib().qfio_format_score(float(x), buf)
@@ -105,10 +135,10 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
         ib, tb = int(sz[7]) & 0xFFFFFFFF, int(sz[7]) >> 32
         R = len(paths)
         list_off = np.zeros(Q * R + 1, np.int64)
-        docid = np.zeros(E, np.uint32)
-        score = np.zeros(E, np.float64)
-        micro = np.zeros(E, np.int32) if micro_ok else None
-        rank = np.zeros(E, np.int64)
+        docid = np.empty(E, np.uint32)
+        score = np.empty(E, np.float64)
+        micro = np.empty(E, np.int32) if micro_ok else None
+        rank = np.empty(E, np.int64)
         L.qfio_runset_csr(h, _p(list_off), _p(docid), _p(score),
                           None if micro is None else _p(micro), _p(rank))
         qo, qc = np.zeros(Q + 1, np.int64), np.zeros(max(qb, 1), np.uint8)
@@ -117,21 +147,32 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
         to, tc = np.zeros(n_tag + 1, np.int64), np.zeros(max(tb, 1), np.uint8)
         L.qfio_runset_strings(h, _p(qo), _p(qc), _p(do), _p(dc), _p(io), _p(ic), _p(to), _p(tc))
         fo = np.zeros(R + 1, np.int64)
-        rq, rd = np.zeros(E, np.uint32), np.zeros(E, np.uint32)
-        ri, rt = np.zeros(E, np.uint32), np.zeros(E, np.uint32)
-        rr, rsc = np.zeros(E, np.int64), np.zeros(E, np.float64)
+        rq, rd = np.empty(E, np.uint32), np.empty(E, np.uint32)
+        ri, rt = np.empty(E, np.uint32), np.empty(E, np.uint32)
+        rr, rsc = np.empty(E, np.int64), np.empty(E, np.float64)
         L.qfio_runset_rows(h, _p(fo), _p(rq), _p(rd), _p(ri), _p(rt), _p(rr), _p(rsc))
     finally:
         L.qfio_runset_free(h)
+    from .runset import StringTable
     qids = _strings(qo, qc)
-    docnos = _strings(do, dc)
-    iters, tags = _strings(io, ic), _strings(to, tc)
-    rs = RunSet(qids=list(qids), rankers=list(names), docnos=docnos, list_off=list_off,
-                docid=docid, score=score, rank=rank, micro=micro)
+    dcb = dc.tobytes()
+    rs = RunSet(qids=list(qids), rankers=list(names), docnos=StringTable(do, dcb),
+                list_off=list_off, docid=docid, score=score, rank=rank, micro=micro)
     rs.rank_is_position = bool(flags & 2)
     rs.canonical = bool(flags & 4)
     rs.has_dups = bool(flags & 8)
-    rs._strtab = {"qid": (qo, qc.tobytes()), "docno": (do, dc.tobytes())}
+    rs._strtab = {"qid": (qo, qc.tobytes()), "docno": (do, dcb)}
+    frames = {}
+    if frame_strings() == "arrow":
+        for r, name in enumerate(names):
+            a, b = int(fo[r]), int(fo[r + 1])
+            frames[name] = pd.DataFrame({
+                "qid": arrow_strings(qo, qc, rq[a:b]), "iter": arrow_strings(io, ic, ri[a:b]),
+                "docno": arrow_strings(do, dc, rd[a:b]), "rank": rr[a:b], "score": rsc[a:b],
+                "runid": arrow_strings(to, tc, rt[a:b])}, copy=False)
+        return rs, frames
+    docnos = rs.docnos.materialize()
+    iters, tags = _strings(io, ic), _strings(to, tc)
 
     def column(strings, codes):
         # a column of one value (the usual iter "Q0" / a file's tag) is a broadcast
@@ -139,7 +180,6 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
             return np.full(len(codes), strings[codes[0]], dtype=object)
         return strings[codes]
 
-    frames = {}
     for r, name in enumerate(names):
         a, b = int(fo[r]), int(fo[r + 1])
         frames[name] = pd.DataFrame({

@@ -152,12 +152,19 @@ class FusedRun(Mapping):
 _PACK_CACHE: Dict[tuple, tuple] = {}  # frames' identity -> (content fingerprint, RunSet)
 
 
-def _column_digest(col) -> int:
+def _column_digest(col):
     """xxh3 of one column's contents: the values of a numeric column, the object
     pointers of an object column (str objects are immutable, so an unchanged
-    pointer is an unchanged value; any assignment into the column changes it)."""
+    pointer is an unchanged value; any assignment into the column changes it);
+    an Arrow-backed column by its (immutable) array."""
     import ctypes
     import xxhash
+    pa_arr = getattr(col.array, "_pa_array", None)
+    if pa_arr is not None:
+        # Arrow-backed (load_runs' string columns): Arrow arrays are immutable and
+        # pandas replaces the array on any assignment, so the array object itself
+        # identifies the contents (held here, so its id cannot be reused)
+        return ("arrow", id(pa_arr), pa_arr)
     a = np.ascontiguousarray(col.to_numpy())
     if a.dtype == object:
         if len(a) == 0:

@@ -17,11 +17,63 @@ import numpy as np
 import pandas as pd
 
 
+class StringTable:
+    """docid -> docno over the native parser's (offsets, bytes) table, in docno
+    order: Python str objects are made only for what is looked up (a few
+    thousand per query), and the whole object array only when one is asked for
+    (np.asarray, searchsorted) — load_runs no longer builds ~10^7 of them."""
+
+    _SMALL = 65536  # lookups up to this size decode the bytes directly
+
+    def __init__(self, off: np.ndarray, chars: bytes):
+        self.off = off
+        self.chars = chars
+        self._all: Optional[np.ndarray] = None
+
+    def __len__(self) -> int:
+        return len(self.off) - 1
+
+    def materialize(self) -> np.ndarray:
+        if self._all is None:
+            from .fastio import _strings
+            self._all = _strings(self.off, np.frombuffer(self.chars, np.uint8)
+                                 if self.chars else np.zeros(1, np.uint8))
+        return self._all
+
+    def __iter__(self):
+        return iter(self.materialize())
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.materialize()
+        return a if dtype is None else a.astype(dtype)
+
+    def __getitem__(self, idx):
+        if self._all is not None:
+            return self._all[idx]
+        if isinstance(idx, (int, np.integer)):
+            i = int(idx)
+            if not -len(self) <= i < len(self):
+                raise IndexError(f"docid {i} out of range for {len(self)} docnos")
+            i %= len(self)
+            return self.chars[self.off[i]:self.off[i + 1]].decode()
+        if isinstance(idx, slice):
+            return self.materialize()[idx]
+        idx = np.asarray(idx)
+        if idx.dtype == bool or idx.size > self._SMALL:
+            return self.materialize()[idx]
+        o, c = self.off, self.chars
+        out = np.empty(idx.shape, dtype=object)
+        flat = out.reshape(-1)
+        for k, i in enumerate(idx.reshape(-1).tolist()):
+            flat[k] = c[o[i]:o[i + 1]].decode()
+        return out
+
+
 @dataclass
 class RunSet:
     qids: List[str]
     rankers: List[str]
-    docnos: np.ndarray            # object array: docid -> docno
+    docnos: object                # docid -> docno: object array or StringTable
     list_off: np.ndarray          # int64 [Q*R + 1]
     docid: np.ndarray             # uint32 [E]
     score: np.ndarray             # float64 [E]

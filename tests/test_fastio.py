@@ -175,3 +175,68 @@ def test_list_flags_match_pack(tmp_path, case):
     assert (rs.rank_is_position, rs.canonical) == {
         "shifted_ranks": (False, True), "unsorted_scores": (True, False),
         "canonical": (True, True)}[case]
+
+
+@pytest.mark.parametrize("mode", ["arrow", "object"])
+def test_frame_string_modes(tmp_path, monkeypatch, mode):
+    """load_runs' string columns: Arrow-backed (default, no Python str per row) or
+    object; both hold the values read_csv gives, and the run set is the same."""
+    monkeypatch.setenv("QPPFUSE_FRAME_STRINGS", mode)
+    rng = np.random.default_rng(3)
+    names, paths = _write_runs(tmp_path, rng)
+    rs, frames = fastio.parse_runs(paths, names, n_threads=4)
+    pf = _pandas_frames(paths, names)
+    for n in names:
+        for c in ("qid", "iter", "docno", "runid"):
+            col = frames[n][c]
+            assert (str(col.dtype) == "string") if mode == "arrow" else (col.dtype == object)
+            assert col.astype(str).tolist() == pf[n][c].astype(str).tolist()
+    ref = pack_frames(pf)
+    assert list(rs.docnos) == list(ref.docnos)
+
+
+def test_gather_strings_matches_python():
+    words = ["test0", "", "Δ17", "doc123456789", "x"]
+    enc = [w.encode() for w in words]
+    off = np.zeros(len(enc) + 1, np.int64)
+    np.cumsum([len(e) for e in enc], out=off[1:])
+    chars = np.frombuffer(b"".join(enc), np.uint8).copy()
+    rng = np.random.default_rng(0)
+    for n in (0, 1, 7, 1000, 200003):  # ragged thread ranges
+        codes = rng.integers(0, len(words), n).astype(np.uint32)
+        assert list(fastio.arrow_strings(off, chars, codes)) == [words[c] for c in codes]
+
+
+def test_string_table_lookups():
+    from qppfuse.runset import StringTable
+    words = ["a", "bb", "Δc", "d"]
+    enc = [w.encode() for w in words]
+    off = np.zeros(5, np.int64)
+    np.cumsum([len(e) for e in enc], out=off[1:])
+    t = StringTable(off, b"".join(enc))
+    assert len(t) == 4 and t[1] == "bb" and t[-1] == "d"
+    with pytest.raises(IndexError):
+        t[4]
+    assert t[np.array([2, 0, 2])].tolist() == ["Δc", "a", "Δc"]
+    assert list(t) == words and np.asarray(t, dtype=object).tolist() == words
+    assert t[np.array([3, 1])].tolist() == ["d", "bb"]  # after materialisation too
+
+
+def test_pack_cache_follows_edits_of_arrow_frames(tmp_path, monkeypatch):
+    """load_runs' Arrow-backed frames: the cached run set is reused while the
+    frames are unchanged and rebuilt after an edit of a string or numeric column."""
+    from qppfuse import fusion
+    monkeypatch.setenv("QPPFUSE_FRAME_STRINGS", "arrow")
+    rng = np.random.default_rng(5)
+    _write_runs(tmp_path, rng, n_runs=3, n_q=6, k=8)
+    frames = fusion.load_runs(str(tmp_path))
+    a = fusion._pack(frames)
+    assert fusion._pack(frames) is a
+    name = next(iter(frames))
+    frames[name].loc[0, "docno"] = "zzz_new"
+    b = fusion._pack(frames)
+    assert b is not a and "zzz_new" in list(b.docnos)
+    frames[name].loc[1, "score"] = 123.0
+    c = fusion._pack(frames)
+    assert c is not b and 123.0 in c.score
+    assert fusion._pack(frames) is c
