@@ -20,7 +20,9 @@ torch.distributed.run (WORLD_SIZE set), or — run plainly as
 `python bench.py --gpus N` — this process, before it makes any GPU call,
 starts `torch.distributed.run --nproc-per-node N` on itself as a child and exits
 with its code.  For N > 1 the timed step includes the north star's collective:
-every rank's fused top-k (default 100) gathered to rank 0 over RCCL.
+every rank's fused top-k (default 100) gathered to rank 0 over RCCL, pipelined:
+step i's gather runs on the communicator's stream beside step i+1's kernels (the
+last one is waited for inside the timed region).
 """
 from __future__ import annotations
 
@@ -224,6 +226,7 @@ class Pipeline:
             self.run_to_booster = [model.retrievers.index(n) if n in model.retrievers else -1
                                    for n in names]
         self.ev = []
+        self.pending = None  # the previous step's top-k gather (dist.PendingGather)
         torch.cuda.synchronize()
 
     def step(self, timed=False):
@@ -264,9 +267,21 @@ class Pipeline:
             self.ev.append((t0, t1))
         if a.gather_topk > 0:  # the final fused top-k of every shard onto rank 0 (RCCL)
             from qppfuse.dist import gather_fused_topk
+            # pipelined: this step's gather runs on the communicator's stream beside
+            # the next step's kernels; the previous step's is waited for here, after
+            # this step's kernels are queued (its top-k buffers are its own)
+            if self.pending is not None:
+                self.gathered = self.pending.wait()
             d, sc = e.fused_topk(self.out, self.off, self.R, a.gather_topk)
-            self.gathered = gather_fused_topk(d, sc, dst=0, sizes=self.shard_sizes)
+            self.pending = gather_fused_topk(d, sc, dst=0, sizes=self.shard_sizes,
+                                             async_op=True)
         self.w = w
+
+    def drain(self):
+        """The last step's gather, before the timed region's final synchronize."""
+        if self.pending is not None:
+            self.gathered = self.pending.wait()
+            self.pending = None
 
     def fuse_kernel_ms(self):
         return float(np.mean([a.elapsed_time(b) for a, b in self.ev]))
@@ -513,6 +528,7 @@ def timed_loop(p: Pipeline, steps: int, world: int, dev) -> float:
     t0 = time.perf_counter()
     for _ in range(steps):
         p.step(timed=True)
+    p.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -548,6 +564,7 @@ def main():
     progress(f"rank {rank}: {p.Q} queries x {p.R} x top-{p.K} resident; warmup {args.warmup}")
     for _ in range(args.warmup):
         p.step()
+    p.drain()
     progress(f"rank {rank}: timing {args.steps} steps")
     elapsed = timed_loop(p, args.steps, world, dev)
     total_q = p.Q * args.steps

@@ -58,6 +58,13 @@ int qfio_join_lines(const int64_t* off, const char* chars, int64_t n, char* out)
  * file_off[R+1], codes into qids / docnos / iters / tags, rank, score */
 int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, uint32_t* docid,
                      uint32_t* iter, uint32_t* tag, int64_t* rank, double* score);
+/* the same columns without copies: pointers [12] into the run set (valid until
+ * qfio_runset_free) to list_off, docid, score, micro (NULL unless micro_ok),
+ * rank, file_off, and the row codes / rank / score of qfio_runset_rows */
+void qfio_runset_views(const qfio_runset* rs, const void** ptrs);
+/* after qfio_runset_strings: release the string views and unmap the files (the
+ * columns stay); qfio_runset_sizes / _strings must not be called after it */
+void qfio_runset_drop_text(qfio_runset* rs);
 void qfio_runset_free(qfio_runset* rs);
 /* per-row strings of a column given as codes into a table (offsets [m+1] +
  * bytes): out_off[n+1] (int64, Arrow large_string offsets) always, the bytes

@@ -32,6 +32,7 @@
 #include <parallel/algorithm>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 #include "../../include/qfio.h"
@@ -563,6 +564,10 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->canonical = not_canon == 0;
   rs->has_dups = dups != 0;
   tm.mark("csr");
+  // the per-row views (~1 GB for C2) are released on a thread of their own:
+  // unmapping them is not on the caller's path
+  std::thread([c = new Cols(std::move(cols))] { delete c; }).detach();
+  tm.mark("release columns");
   *out = rs;
   return QFIO_OK;
 }
@@ -588,10 +593,12 @@ static void copy_strings(const std::vector<std::string_view>& v, int64_t* off, c
   int64_t o = 0;
   off[0] = 0;
   for (size_t i = 0; i < v.size(); ++i) {
-    memcpy(chars + o, v[i].data(), v[i].size());
     o += (int64_t)v[i].size();
     off[i + 1] = o;
   }
+  // the bytes in parallel: the views point all over the mapped files
+#pragma omp parallel for schedule(static, 4096)
+  for (int64_t i = 0; i < (int64_t)v.size(); ++i) memcpy(chars + off[i], v[i].data(), v[i].size());
 }
 
 int qfio_runset_csr(const qfio_runset* rs, int64_t* list_off, uint32_t* docid, double* score,
@@ -638,8 +645,34 @@ int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, ui
   return QFIO_OK;
 }
 
-int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
-                            int64_t n, int64_t* out_off, char* out_chars) {
+void qfio_runset_drop_text(qfio_runset* rs) {
+  std::vector<std::string_view>().swap(rs->qids);
+  std::vector<std::string_view>().swap(rs->docnos);
+  std::vector<std::string_view>().swap(rs->iters);
+  std::vector<std::string_view>().swap(rs->tags);
+  for (auto* m : rs->maps) delete m;
+  rs->maps.clear();
+}
+
+void qfio_runset_views(const qfio_runset* rs, const void** ptrs) {
+  ptrs[0] = rs->list_off.data();
+  ptrs[1] = rs->docid.data();
+  ptrs[2] = rs->score.data();
+  ptrs[3] = rs->micro_ok ? rs->micro.data() : nullptr;
+  ptrs[4] = rs->rank.data();
+  ptrs[5] = rs->file_off.data();
+  ptrs[6] = rs->row_qid.data();
+  ptrs[7] = rs->row_docid.data();
+  ptrs[8] = rs->row_iter.data();
+  ptrs[9] = rs->row_tag.data();
+  ptrs[10] = rs->row_rank.data();
+  ptrs[11] = rs->row_score.data();
+}
+
+}  // extern "C"
+template <class Off>
+static int64_t gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
+                              int64_t n, Off* out_off, char* out_chars) {
   if (n < 0 || !tab_off || (n && (!codes || !out_off))) return -1;
   // lengths -> offsets (a blocked parallel scan), then the bytes
   const int T = std::max(1, omp_get_max_threads());
@@ -652,21 +685,27 @@ int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const
     int64_t s = 0;
     for (int64_t i = a; i < b; ++i) {
       s += tab_off[codes[i] + 1] - tab_off[codes[i]];
-      out_off[i + 1] = s;
+      out_off[i + 1] = (Off)s;
     }
     part[t + 1] = s;
 #pragma omp barrier
 #pragma omp single
     for (int k = 0; k < nt; ++k) part[k + 1] += part[k];
     const int64_t add = part[t];
-    for (int64_t i = a; i < b; ++i) out_off[i + 1] += add;
+    for (int64_t i = a; i < b; ++i) out_off[i + 1] += (Off)add;
 #pragma omp barrier  // out_off[a] is the previous thread's last offset
     if (out_chars)
       for (int64_t i = a; i < b; ++i)
         memcpy(out_chars + out_off[i], tab_chars + tab_off[codes[i]],
                (size_t)(out_off[i + 1] - out_off[i]));
   }
-  return n ? out_off[n] : 0;
+  return n ? (int64_t)out_off[n] : 0;
+}
+extern "C" {
+
+int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
+                            int64_t n, int64_t* out_off, char* out_chars) {
+  return gather_strings(tab_off, tab_chars, codes, n, out_off, out_chars);
 }
 
 void qfio_runset_free(qfio_runset* rs) { delete rs; }

@@ -73,18 +73,39 @@ def allgather_qpp_raw(raw, present, group=None):
             torch.cat([t[:k] for t, k in zip(pres, sizes)]).to(torch.bool))
 
 
-def gather_fused_topk(docid, score, dst: int = 0, group=None, sizes=None):
+class PendingGather:
+    """An in-flight gather_fused_topk(async_op=True): wait() makes the caller's
+    stream wait for the collective (no host block on RCCL) and returns the
+    concatenated (docid, score) on the destination rank, None elsewhere."""
+
+    def __init__(self, works, dl, sl, sizes):
+        self._works, self._dl, self._sl, self._sizes = works, dl, sl, sizes
+
+    def wait(self):
+        import torch
+        for w in self._works:
+            w.wait()
+        if self._dl is None:
+            return None
+        k = self._sizes
+        return (torch.cat([t[:n] for t, n in zip(self._dl, k)]),
+                torch.cat([t[:n] for t, n in zip(self._sl, k)]))
+
+
+def gather_fused_topk(docid, score, dst: int = 0, group=None, sizes=None, async_op=False):
     """The final fused top-k of every rank's query shard, concatenated in rank
     order on rank `dst` (None elsewhere): docid [Q_r, M, k] and score tensors
     from engine.fused_topk.  Shards may differ in size by the shard_range
     remainder: rows are padded to the largest shard for the collective
     (dist.gather over RCCL/xGMI; gloo in the CPU tests) and trimmed after.
     `sizes` (every rank's row count, when the caller knows them — fixed shards)
-    skips the all-gather of the counts and its host synchronisation."""
+    skips the all-gather of the counts and its host synchronisation.
+    async_op=True returns a PendingGather at once (the collective runs on the
+    communicator's stream beside whatever the caller launches next)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        return docid, score
+        return PendingGather([], [docid], [score], [docid.shape[0]]) if async_op else (docid, score)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     if dist.get_backend(group) == "gloo" and docid.is_cuda:  # gloo rehearsal: host buffers
         docid, score = docid.cpu(), score.cpu()
@@ -102,9 +123,8 @@ def gather_fused_topk(docid, score, dst: int = 0, group=None, sizes=None):
     d, s = pad(docid, -1), pad(score, float("nan"))
     dl = [torch.empty_like(d) for _ in range(world)] if rank == dst else None
     sl = [torch.empty_like(s) for _ in range(world)] if rank == dst else None
-    dist.gather(d, dl, dst=dst, group=group)
-    dist.gather(s, sl, dst=dst, group=group)
-    if rank != dst:
-        return None
-    return (torch.cat([t[:k] for t, k in zip(dl, sizes)]),
-            torch.cat([t[:k] for t, k in zip(sl, sizes)]))
+    works = [dist.gather(d, dl, dst=dst, group=group, async_op=async_op),
+             dist.gather(s, sl, dst=dst, group=group, async_op=async_op)]
+    pending = PendingGather([w for w in works if w is not None] if async_op else [],
+                            dl if rank == dst else None, sl, sizes)
+    return pending if async_op else pending.wait()

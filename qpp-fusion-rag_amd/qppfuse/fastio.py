@@ -47,6 +47,10 @@ def lib() -> C.CDLL:
         L.qfio_join_lines.argtypes = [_vp, _vp, _i64, _vp]
         L.qfio_gather_strings.restype = _i64
         L.qfio_gather_strings.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp]
+        L.qfio_runset_drop_text.restype = None
+        L.qfio_runset_drop_text.argtypes = [_vp]
+        L.qfio_runset_views.restype = None
+        L.qfio_runset_views.argtypes = [_vp, _vp]
         L.qfio_runset_free.restype = None
         L.qfio_runset_free.argtypes = [_vp]
         L.qfio_format_score.restype = C.c_size_t
@@ -68,6 +72,27 @@ def _check(rc: int, what: str):
     raise OSError(f"{what}: {msg}")
 
 
+class _RunSetOwner:
+    """A parsed qfio_runset whose column buffers back numpy arrays: freed when
+    the last array made by array() (each holds a reference) is collected."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def array(self, ptr, n: int, dtype) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if n == 0 or not ptr:
+            return np.zeros(n, dt)
+        buf = (C.c_char * (n * dt.itemsize)).from_address(ptr)
+        buf._owner = self  # the ctypes buffer is the array's base
+        return np.frombuffer(buf, dt, n)
+
+    def __del__(self):
+        if self.h is not None and _LIB is not None:
+            _LIB.qfio_runset_free(self.h)
+            self.h = None
+
+
 def _p(a: np.ndarray):
     return a.ctypes.data_as(_vp)
 
@@ -87,13 +112,20 @@ def _strings(off: np.ndarray, chars: np.ndarray) -> np.ndarray:
 
 def arrow_strings(off: np.ndarray, chars: np.ndarray, codes: np.ndarray):
     """Per-row strings (codes into the table off/chars) as a pandas ArrowStringArray:
-    the bytes gathered in C++ straight into Arrow large_string buffers, no Python
-    str per row (they are made when an element is read)."""
+    the bytes gathered in C++ straight into Arrow string buffers, no Python str
+    per row (they are made when an element is read).  A column of one value
+    (iter "Q0", a run's tag) is a repeat."""
     import pyarrow as pa
     codes = np.ascontiguousarray(codes, np.uint32)
     n = len(codes)
-    out_off = np.empty(n + 1, np.int64)
+    if n and codes[0] == codes[-1] and (codes == codes[0]).all():
+        v = bytes(chars[off[codes[0]]:off[codes[0] + 1]])
+        o = np.arange(n + 1, dtype=np.int64) * len(v)
+        arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(o), pa.py_buffer(v * n))
+        return pd.arrays.ArrowStringArray(pa.chunked_array([arr]))
+    # large_string (int64 offsets): what pandas' ArrowStringArray holds, so no cast
     L = lib()
+    out_off = np.empty(n + 1, np.int64)
     nb = L.qfio_gather_strings(_p(off), _p(chars), _p(codes), n, _p(out_off), None)
     if nb < 0:
         raise ValueError("gather_strings: bad arguments")
@@ -134,25 +166,31 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
         n_iter, n_tag = int(sz[6]) & 0xFFFFFFFF, int(sz[6]) >> 32
         ib, tb = int(sz[7]) & 0xFFFFFFFF, int(sz[7]) >> 32
         R = len(paths)
-        list_off = np.zeros(Q * R + 1, np.int64)
-        docid = np.empty(E, np.uint32)
-        score = np.empty(E, np.float64)
-        micro = np.empty(E, np.int32) if micro_ok else None
-        rank = np.empty(E, np.int64)
-        L.qfio_runset_csr(h, _p(list_off), _p(docid), _p(score),
-                          None if micro is None else _p(micro), _p(rank))
-        qo, qc = np.zeros(Q + 1, np.int64), np.zeros(max(qb, 1), np.uint8)
-        do, dc = np.zeros(D + 1, np.int64), np.zeros(max(db, 1), np.uint8)
-        io, ic = np.zeros(n_iter + 1, np.int64), np.zeros(max(ib, 1), np.uint8)
-        to, tc = np.zeros(n_tag + 1, np.int64), np.zeros(max(tb, 1), np.uint8)
+        # (every offset and byte is written by qfio_runset_strings)
+        qo, qc = np.empty(Q + 1, np.int64), np.zeros(max(qb, 1), np.uint8)
+        do, dc = np.empty(D + 1, np.int64), np.empty(max(db, 1), np.uint8)
+        io, ic = np.empty(n_iter + 1, np.int64), np.zeros(max(ib, 1), np.uint8)
+        to, tc = np.empty(n_tag + 1, np.int64), np.zeros(max(tb, 1), np.uint8)
         L.qfio_runset_strings(h, _p(qo), _p(qc), _p(do), _p(dc), _p(io), _p(ic), _p(to), _p(tc))
-        fo = np.zeros(R + 1, np.int64)
-        rq, rd = np.empty(E, np.uint32), np.empty(E, np.uint32)
-        ri, rt = np.empty(E, np.uint32), np.empty(E, np.uint32)
-        rr, rsc = np.empty(E, np.int64), np.empty(E, np.float64)
-        L.qfio_runset_rows(h, _p(fo), _p(rq), _p(rd), _p(ri), _p(rt), _p(rr), _p(rsc))
+        # the columns stay in the run set's buffers (no copies): numpy views that
+        # keep the run set alive until the last of them is gone
+        L.qfio_runset_drop_text(h)  # the text is copied out; unmap the files
+        owner = _RunSetOwner(h)
+        h = None
+        ptrs = (C.c_void_p * 12)()
+        L.qfio_runset_views(owner.h, ptrs)
+        view = lambda i, n, dt: owner.array(ptrs[i], n, dt)
+        list_off = view(0, Q * R + 1, np.int64)
+        docid, score = view(1, E, np.uint32), view(2, E, np.float64)
+        micro = view(3, E, np.int32) if micro_ok else None
+        rank = view(4, E, np.int64)
+        fo = view(5, R + 1, np.int64)
+        rq, rd = view(6, E, np.uint32), view(7, E, np.uint32)
+        ri, rt = view(8, E, np.uint32), view(9, E, np.uint32)
+        rr, rsc = view(10, E, np.int64), view(11, E, np.float64)
     finally:
-        L.qfio_runset_free(h)
+        if h is not None:
+            L.qfio_runset_free(h)
     from .runset import StringTable
     qids = _strings(qo, qc)
     dcb = dc.tobytes()

@@ -102,25 +102,33 @@ def test_zscore_gathers_the_whole_table():
         assert np.array_equal(fp, np.arange(Q * R) % 7 != 3)
 
 
-def _topk_worker(rank, world, port, sizes, out):
+def _topk_worker(rank, world, port, sizes, out, async_op=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from qppfuse.dist import gather_fused_topk
     n = sizes[rank]
     docid = torch.arange(n * 2 * 3, dtype=torch.int32).reshape(n, 2, 3) + 1000 * rank
     score = docid.to(torch.float64) / 7
-    res = gather_fused_topk(docid, score, dst=0)
+    if async_op:  # bench.py's pipelined form: two gathers in flight, waited in order
+        p1 = gather_fused_topk(docid, score, dst=0, sizes=sizes, async_op=True)
+        p2 = gather_fused_topk(docid + 1, score, dst=0, sizes=sizes, async_op=True)
+        res, res2 = p1.wait(), p2.wait()
+        if res2 is not None:
+            assert torch.equal(res2[0], res[0] + 1)
+    else:
+        res = gather_fused_topk(docid, score, dst=0)
     out[rank] = None if res is None else (res[0].numpy().copy(), res[1].numpy().copy())
     dist.destroy_process_group()
 
 
-def test_gather_fused_topk_concatenates_shards_in_rank_order():
+@pytest.mark.parametrize("async_op", [False, True])
+def test_gather_fused_topk_concatenates_shards_in_rank_order(async_op):
     """Unequal shards (the shard_range remainder) are padded for the collective and
     trimmed: rank 0 holds every rank's rows in rank order, the others None."""
     sizes = [3, 2]
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_topk_worker, args=(2, _free_port(), sizes, out), nprocs=2, join=True)
+    mp.spawn(_topk_worker, args=(2, _free_port(), sizes, out, async_op), nprocs=2, join=True)
     assert out[1] is None
     d, s = out[0]
     want = np.concatenate([np.arange(n * 6, dtype=np.int32).reshape(n, 2, 3) + 1000 * r
