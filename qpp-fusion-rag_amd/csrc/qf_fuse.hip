@@ -31,9 +31,6 @@
 
 namespace qf {
 
-#ifndef QF_JOIN_REV
-#define QF_JOIN_REV 0
-#endif
 constexpr int kRMax = 16;    // runs per query in the LDS join (u16 retriever masks)
 constexpr int kRMaxXl = 32;  // in the workspace kernel (u32 masks)
 constexpr int kNMethods = 9;  // method bits QF_COMBSUM .. QF_WRRF_MUL
@@ -847,11 +844,7 @@ template <class C, int KIND>
 __global__ __launch_bounds__(C::kBlock, KIND == 1 ? C::kMinWaves : (C::kMinWaves < 4 ? C::kMinWaves : 4))
 void join_kernel(FuseParams p) {
   __shared__ JoinShared<C, KIND> sh;
-#if QF_JOIN_REV
-  const int64_t q = p.n_queries - 1 - block_id();
-#else
   const int64_t q = block_id();
-#endif
   if (q >= p.n_queries) return;
   const int N = join_groups<C, KIND>(p, sh, q);
   if (N < 0) return;
@@ -1498,9 +1491,10 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   // Infinity Cache
   const int M = __popc(p.methods);
   const int64_t bid = block_id();
-  const int64_t grp8 = bid >> 3;
+  const int64_t grp8 = bid >> 3, ngroups = (p.n_queries + 7) / 8;
+  if (grp8 >= ngroups * M) return;  // a 2-D grid's padding workgroups (grid_for)
 #if QF_BS_REV
-  const int64_t q = ((p.n_queries + 7) / 8 - 1 - grp8 / M) * 8 + (bid & 7);
+  const int64_t q = (ngroups - 1 - grp8 / M) * 8 + (bid & 7);
 #else
   const int64_t q = (grp8 / M) * 8 + (bid & 7);
 #endif

@@ -295,6 +295,41 @@ def test_grids_beyond_65536_workgroups(gpu):
         assert fused[m][valid].tobytes() == o_fused[valid].tobytes(), name
 
 
+def test_bucket_sort_grid_beyond_65536_workgroups(gpu):
+    """The bucket sort's (query, method) map runs the query groups in reverse: on a 2-D
+    grid (more than 65,536 workgroups) the padding workgroups past the last pair must
+    leave — 33,000 queries x 2 methods with 1,040 entries each (the join + bucket-sort
+    path), checked against the oracle on a sample of queries."""
+    from qppfuse import engine
+    Q, R, K = 33_000, 2, 520
+    ms = ["combsum", "rrf"]
+    off, docid, raw = engine.synth_runs(0, Q, R, K, seed=13)
+    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+    out = engine.fuse(off, docid, micro, R, ms, rrf_k=60, max_entries=R * K)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    uc = out.union_count.cpu().numpy()
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fused = out.fused.cpu().numpy()
+    qs = np.sort(np.random.default_rng(4).choice(Q, 300, replace=False))
+    qs = np.concatenate([[0], qs, [Q - 1]])
+    # the sampled queries as their own run set (queries are independent)
+    lens = np.diff(off_h)
+    sub_off = np.concatenate([[0], np.cumsum(lens.reshape(Q, R)[qs].ravel())])
+    idx = np.concatenate([np.arange(off_h[q * R], off_h[q * R + R]) for q in qs])
+    for m, name in enumerate(ms):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(sub_off, doc_h[idx], sc_h[idx], R, name, 60)
+        np.testing.assert_array_equal(uc[qs], o_uc)
+        for i, q in enumerate(qs):
+            b, n, sb = off_h[q * R], uc[q], sub_off[i * R]
+            np.testing.assert_array_equal(ud[b:b + n], o_ud[sb:sb + n])
+            np.testing.assert_array_equal(perm[m][b:b + n], o_perm[sb:sb + n], err_msg=name)
+            assert fused[m][b:b + n].tobytes() == o_fused[sb:sb + n].tobytes(), name
+
+
 @pytest.mark.parametrize("kind", ["f64", "micro"])
 def test_workspace_path_for_very_large_queries(gpu, kind):
     """Queries beyond the LDS join (more than 10,240 entries, up to 65,535) run the
