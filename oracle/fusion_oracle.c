@@ -13,8 +13,8 @@
  *    count (:327).  Output order = dict insertion (first-seen) order.
  *  - combsum / combmnz / rrf via ranx (src/fusion.py:170-230; ranx>=0.3.16, not
  *    installed here — restated from its published semantics):
- *    per run, per query min-max normalisation (s - min) / (max - min) (0 when
- *    max == min); CombSUM = sum over runs in order; CombMNZ = sum * #runs;
+ *    per run, per query min-max normalisation (s - min) / max(max - min, 1e-9)
+ *    (ranx's "avoid division by zero" denominator; a constant list gives 0); CombSUM = sum over runs in order; CombMNZ = sum * #runs;
  *    RRF = sum of 1 / (k + rank), rank = 1-based position after a stable sort
  *    of the run's list by normalised score, descending.
  *  - write_runfile / _ranx_to_dict ordering (src/fusion.py:475, :488): stable
@@ -27,6 +27,12 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* ranx min-max denominator: max(max - min, 1e-9) (NaN stays NaN). */
+static double ranx_den(double mx, double mn) {
+  const double d = mx - mn;
+  return d < 1e-9 ? 1e-9 : d;
+}
 
 enum { M_COMBSUM = 0, M_COMBMNZ, M_RRF, M_WCOMBSUM, M_WCOMBMNZ, M_WRRF };
 
@@ -116,7 +122,7 @@ int oracle_fuse(int64_t Q, int32_t R, const int64_t* list_off, const uint32_t* d
       }
       if (method == M_RRF) { /* ranx rank: stable sort by normalised score desc */
         for (int64_t i = 0; i < n; ++i) {
-          const double den = mx - mn;
+          const double den = ranx_den(mx, mn);
           items[i].s = den > 0.0 ? (score[a + i] - mn) / den : 0.0;
           items[i].i = (int32_t)i;
         }
@@ -135,7 +141,7 @@ int oracle_fuse(int64_t Q, int32_t R, const int64_t* list_off, const uint32_t* d
         switch (method) {
           case M_COMBSUM:
           case M_COMBMNZ: {
-            const double den = mx - mn;
+            const double den = ranx_den(mx, mn);
             c = den > 0.0 ? (score[a + i] - mn) / den : 0.0;
           } break;
           case M_RRF: c = 1.0 / (double)(rrf_k + t + 1); break;

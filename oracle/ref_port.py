@@ -91,7 +91,7 @@ def _minmax(d: Dict[str, float]) -> Dict[str, float]:
     if not d:
         return {}
     lo, hi = min(d.values()), max(d.values())
-    den = hi - lo
+    den = max(hi - lo, 1e-9)  # ranx min_max_norm's denominator ("avoid division by zero")
     return {doc: ((s - lo) / den if den > 0 else 0.0) for doc, s in d.items()}
 
 

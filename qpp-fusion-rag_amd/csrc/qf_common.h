@@ -190,6 +190,16 @@ __device__ __forceinline__ int64_t block_id() {
   return (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
 }
 
+// ranx's min-max denominator: max(max - min, 1e-9) ("avoid division by zero",
+// ranx/normalization min_max_norm, restated — ranx is not importable here: the
+// rule is parity-unpinned; it only matters for ranges below 1e-9, never on
+// .norm.res input whose smallest non-zero range is 1e-6).  A NaN range stays NaN
+// (the callers' den > 0 test then gives the entry 0, as before).
+__host__ __device__ __forceinline__ double ranx_den(double mx, double mn) {
+  const double d = mx - mn;
+  return d < 1e-9 ? 1e-9 : d;
+}
+
 // ---- correctly rounded quotients without a division --------------------------
 // Markstein: with y = RN(1/b) and q within one ulp of a/b, the residual
 // a - q*b is exact in one fma and RN(q + residual*y) = RN(a/b).  The join uses

@@ -561,8 +561,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       mn = ScoreIn<KIND>::load(p.score, b - 1);
     }
     sh.mn[tid] = mn;
-    sh.den[tid] = mx - mn;
-    sh.rden[tid] = 1.0 / (mx - mn);  // one IEEE division per list (div_by_recip)
+    sh.den[tid] = ranx_den(mx, mn);
+    sh.rden[tid] = 1.0 / sh.den[tid];  // one IEEE division per list (div_by_recip)
     // block-uniform fast paths of the sums: every list already [0, 1] (a .norm.res
     // list: x = s), every weight in div_int's division-free range
     const double aw = fabs(sh.w[tid]);
@@ -1877,8 +1877,8 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
       mn = ScoreIn<KIND>::load(p.score, b - 1);
     }
     s_min[tid] = mn;
-    s_den[tid] = mx - mn;
-    s_rden[tid] = 1.0 / (mx - mn);
+    s_den[tid] = ranx_den(mx, mn);
+    s_rden[tid] = 1.0 / s_den[tid];
   }
   for (int i = tid; i < TS; i += kXlBlock) {
     w.tkey[i] = kEmpty;

@@ -122,6 +122,37 @@ def _csr(lists, device):
     return off, doc, sc, t(off), t(doc.view(np.int32)), t(sc)
 
 
+@pytest.mark.parametrize("max_entries", [8, 2048, 20000])  # small join, LDS join, workspace join
+def test_ranx_minmax_denominator_floor(gpu, max_entries):
+    """ranx's min-max divides by max(max - min, 1e-9): a list whose range is below
+    1e-9 is scaled by 1e-9 (not stretched to [0, 1]), a constant list gives 0."""
+    from qppfuse import engine
+    R = 3
+    lists = [([1, 2, 3], [1.0 + 4e-10, 1.0 + 1e-10, 1.0]),   # range 4e-10 < 1e-9
+             ([2, 4], [0.3, 0.3]),                           # constant
+             ([3, 5, 1], [7.0, 5.0, 2.5])]                   # ordinary
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    out = engine.fuse(doff, ddoc, dsc, R, ["combsum", "combmnz", "rrf"],
+                      max_entries=max_entries)
+    uc = int(out.union_count[0])
+    f = out.fused.cpu().numpy()
+    p = out.perm.cpu().numpy().view(np.uint16)
+    for m, name in enumerate(["combsum", "combmnz", "rrf"]):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name)
+        assert uc == o_uc[0] == 5
+        assert f[m][:uc].tobytes() == o_fused[:uc].tobytes(), name
+        np.testing.assert_array_equal(p[m][:uc], o_perm[:uc])
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    got = dict(zip(ud[p[0][:uc].astype(np.int64)].tolist(), f[0][:uc].tolist()))
+    want = {}
+    for docs, scores in lists:  # the rule itself, in Python floats, runs in order
+        lo, hi = min(scores), max(scores)
+        den = max(hi - lo, 1e-9)
+        for d, x in zip(docs, scores):
+            want[d] = want.get(d, 0.0) + (x - lo) / den
+    assert got == want
+
+
 def test_edge_cases_empty_lists_ties_single(gpu):
     from qppfuse import engine
     R = 3
