@@ -512,6 +512,8 @@ struct JoinShared {
   int64_t off[kRMax + 1];
   double w[kRMax], mn[kRMax], den[kRMax], rden[kRMax];
   int cnt[C::kItems * C::kWaves], gof[C::kItems * C::kWaves];
+  // lane 0's score of every (row, wave): lane 63's successor for the sort check
+  typename ScoreIn<KIND>::raw_t first[C::kItems * C::kWaves + 1];
   int U, status;
   int slow;  // bit 0: a non-empty list is not [0, 1]-normalised; bit 1: a weight needs IEEE division
 };
@@ -587,12 +589,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
   int status = 0;
   uint32_t rj[ITEMS];
+  uint32_t defer = 0u;  // lane 63: rows whose successor (lane 0 of the next wave) is checked below
+  const bool ranx = p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF);
   int r = 0;  // entry e's list; e grows with j, so the search resumes where it stopped
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
     const raw_t nxt = __shfl_down(sc[j], 1, 64);  // entry e + 1, but at lane 63
     rj[j] = 0u;
+    if (lane == 0 && e < N) sh.first[j * WAVES + wid] = sc[j];
     if (e < N) {
       const uint32_t d = dk[j];
       if (d == kEmpty) status = QF_QSTATUS_BADDOC;
@@ -611,10 +616,12 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       // preconditions of the ranx methods / W-RRF (checked once, here)
       const int64_t g = base + e;
       if (g + 1 < sh.off[r + 1]) {
-        if (p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) {
-          const raw_t nx = lane == 63 ? ScoreIn<KIND>::raw(p.score, g + 1) : nxt;
-          // raw compare: m / 1e6 is strictly increasing in the micro-units m
-          if (nx > sc[j]) status = QF_QSTATUS_UNSORTED;
+        if (ranx) {
+          // raw compare: m / 1e6 is strictly increasing in the micro-units m.
+          // Lane 63's successor is lane 0 of the next wave: compared after the
+          // barrier from LDS (a global load here stalled every row)
+          if (lane == 63) defer |= 1u << j;
+          else if (nxt > sc[j]) status = QF_QSTATUS_UNSORTED;
         }
         if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
           status = QF_QSTATUS_RANKORDER;
@@ -623,6 +630,13 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   }
   if (status) atomicMin(&sh.status, status);
   __syncthreads();
+  if (defer) {  // lane 63 only (every sh.first write is behind the barrier)
+    int st = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (((defer >> j) & 1u) && sh.first[j * WAVES + wid + 1] > sc[j]) st = QF_QSTATUS_UNSORTED;
+    if (st) atomicMin(&sh.status, st);  // read after the barriers that follow
+  }
   QF_STAMP(4);
   // ---- number distinct documents in first-seen order; size their groups ------
   uint32_t repm = 0u;
