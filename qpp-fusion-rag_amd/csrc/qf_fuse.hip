@@ -647,7 +647,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     bool rep = false;
     if (e < N) {
       const uint32_t msk = mask_of(dk[j]);
-      rep = (uint32_t)(__ffs(msk) - 1) == rj[j];
+      rj[j] |= msk << 16;  // the final mask, kept: r | mask << 16 (no second LDS read)
+      rep = (uint32_t)(__ffs(msk) - 1) == (rj[j] & 0xFFFFu);
       pc = rep ? (uint32_t)__popc(msk) : 0u;
     }
     repm |= (uint32_t)rep << j;
@@ -683,7 +684,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     const uint64_t b = ballot(rep);
     uint32_t msk = 0u, pc = 0u;
     if (rep) {
-      msk = mask_of(dk[j]);
+      msk = rj[j] >> 16;
       pc = (uint32_t)__popc(msk);
     }
     const uint32_t gpre = wave_incl_scan_dpp(pc) - pc;
@@ -702,8 +703,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     const int e = j * BLOCK + tid;
     if (e < N) {
       const uint32_t gu = tkey[dk[j]];
-      const uint32_t r = rj[j];
-      const uint32_t k = (gu & 0xFFFFu) + (uint32_t)__popc(mask_of(dk[j]) & ((1u << r) - 1u));
+      const uint32_t r = rj[j] & 0xFFFFu;
+      const uint32_t k = (gu & 0xFFFFu) + (uint32_t)__popc((rj[j] >> 16) & ((1u << r) - 1u));
       const uint32_t u = ((repm >> j) & 1u) ? gu >> 16 : 0u;
       dk[j] = k | (u << 16);
     }
@@ -717,7 +718,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
     if (e < N) {
-      const uint32_t k = dk[j] & 0xFFFFu, r = rj[j];
+      const uint32_t k = dk[j] & 0xFFFFu, r = rj[j] & 0xFFFFu;
       gsc[k] = sc[j];
       gpr[k] = (uint32_t)(base + e - sh.off[r]) | (r << 16);
       if ((repm >> j) & 1u) ugo[dk[j] >> 16] = (uint16_t)k;
