@@ -552,16 +552,28 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     return -1;
   }
   const int N = (int)N64;
+  uint32_t dk[ITEMS];
+  raw_t sc[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {  // all loads in flight before the first use
+    const int e = j * BLOCK + tid;
+    dk[j] = e < N ? p.docid[base + e] : kEmpty;
+    sc[j] = e < N ? ScoreIn<KIND>::raw(p.score, base + e) : (raw_t)0;
+  }
+  // the per-list constants after the entries' loads are issued: wave 0's waits on
+  // them then overlap the entries' latency instead of delaying its loads
   if (tid < R) {
     const int64_t a = sh.off[tid], b = sh.off[tid + 1];
-    sh.w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
     // ranx min-max (norm="min-max", the fuse() default); lists are sorted
-    // descending (checked below), so max / min are the end points.
+    // descending (checked below), so max / min are the end points.  The three
+    // loads are issued together (one latency)
+    const double wv = p.weights ? p.weights[q * R + tid] : 1.0;
     double mx = 0.0, mn = 0.0;
     if (b > a) {
       mx = ScoreIn<KIND>::load(p.score, a);
       mn = ScoreIn<KIND>::load(p.score, b - 1);
     }
+    sh.w[tid] = wv;
     sh.mn[tid] = mn;
     sh.den[tid] = ranx_den(mx, mn);
     sh.rden[tid] = 1.0 / sh.den[tid];  // one IEEE division per list (div_by_recip)
@@ -576,14 +588,6 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
   for (int i = tid * 4; i < TS / 2; i += BLOCK * 4)
     *(uint4*)&tmask2[i] = make_uint4(0u, 0u, 0u, 0u);
-  uint32_t dk[ITEMS];
-  raw_t sc[ITEMS];
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {  // all loads in flight before the first use
-    const int e = j * BLOCK + tid;
-    dk[j] = e < N ? p.docid[base + e] : kEmpty;
-    sc[j] = e < N ? ScoreIn<KIND>::raw(p.score, base + e) : (raw_t)0;
-  }
   __syncthreads();
   QF_STAMP(3);
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
