@@ -122,6 +122,14 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     k = n64 < 50 ? (int)n64 : 50;                // QPPBridge.java:141
   }
   const bool act = lane < k;
+  // the query's inputs issued with the scores (one latency, not three: they were
+  // loaded where first used, each a stall of the whole workgroup's phase)
+  // (unconditional: q = 0 for a padding wave, whose values go unused)
+  const int64_t q = lv ? l / R : 0;
+  const int nt_raw = num_terms[q];
+  const double tf0 = text_feat[2 * q], tf1 = text_feat[2 * q + 1];
+  const double uefw = kUefWeight[lane < 20 ? lane : 0];          // UEF's DCG weight
+  const double wsum = kUefWeightSum[(k < 20 ? (k > 0 ? k : 1) : 20) - 1];
   // float32 rounding of the JSON value (Gson getAsFloat), then widened.
   const double x = act ? (double)(float)score[a + lane] : 0.0;
   s_x[w][lane] = x;
@@ -185,8 +193,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   // ---- C (each list's wave): squared deviations around each prefix mean
   // (lane i = prefix i): simple sum -> NQC of the prefix (NQC, CumNQC),
   // compensated average -> population variance (SigmaMax, RSD)
-  const int64_t q = lv ? l / R : 0;
-  const int nt_raw = lv ? num_terms[q] : 1;
   const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
   double mean_i = 0.0;
   if (act) {  // computeFinalSum of prefix i, / (i + 1)
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     }
     t_skew = cube((x - mu) / std_full);
     t_wig = x - baseline;
-    if (lane < 20) t_uw = x * kUefWeight[lane];  // UEF (:349-363)
+    if (lane < 20) t_uw = x * uefw;  // UEF (:349-363)
   }
   // Java adds the x <= 0 terms of SMV / SNQC as "skip": adding +0.0 is the same.
   // col 9: CumNQC (:400-410) sums the NQC of prefix sizes 2..n in order.
@@ -267,7 +273,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   }
   const double cum = s_res[w][0], smv = s_res[w][1], wig = s_res[w][2], skew = s_res[w][3];
   const double snqc = s_res[w][4], util = s_res[w][5];
-  const double wsum = kUefWeightSum[(k < 20 ? k : 20) - 1];
   const double sigmax = s_sigmax[w];
   const double cumnqc = k < 2 ? 0.0 : cum / (double)(k - 1);
   double res[kQppCols];
@@ -278,8 +283,8 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   res[4] = sigmax;
   res[5] = (k < 3 || std_full < 1e-10) ? 0.0 : skew / (double)k;
   res[6] = util / wsum;
-  res[7] = text_feat[2 * q];
-  res[8] = text_feat[2 * q + 1];
+  res[7] = tf0;
+  res[8] = tf1;
   res[9] = cumnqc;
   res[10] = mu <= 0.0 ? 0.0 : snqc / (double)k;
   const double range = mx - mn;
