@@ -1502,7 +1502,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   const uint16_t* bk = (const uint16_t*)bkw;
   __shared__ uint32_t s_wtot[WAVES], s_wmax[WAVES];
   __shared__ double s_wmin_v[WAVES], s_wmax_v[WAVES];
-  __shared__ int s_wnan[WAVES];
+  __shared__ int s_wnan[WAVES], s_gnan;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // block -> (query, method slot): slot-major groups of 8 queries (fuse_kernel's
   // map: query q on XCD q % 8, where the join wrote it), the groups in reverse:
@@ -1535,7 +1535,9 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   for (int i = tid * 4; i < NB / 2 + 8; i += BLOCK * 4)
     *(uint4*)&bkw[i] = make_uint4(0u, 0u, 0u, 0u);
   QF_STAMP(8);
-  {  // score range: f64 min / max (a NaN flagged); per-wave results, one barrier
+  {  // score range: f64 min / max (a NaN flagged).  Every thread's partials go
+     // through sval (unused until the scatter) and wave 0 alone reduces the
+     // 2 x BLOCK of them: one wave's DPP reductions instead of every wave's
     double vmn = INFINITY, vmx = -INFINITY;
     bool nan = false;
 #pragma unroll
@@ -1547,25 +1549,35 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
         nan |= v[j] != v[j];
       }
     }
-    vmn = wave_min_f64_dpp(vmn);
-    vmx = wave_max_f64_dpp(vmx);
+    sval[tid] = vmn;
+    sval[BLOCK + tid] = vmx;
     const bool anynan = ballot(nan) != 0ull;
-    if (lane == 63) {
-      s_wmin_v[wid] = vmn;
-      s_wmax_v[wid] = vmx;
-      s_wnan[wid] = anynan ? 1 : 0;
-    }
+    if (lane == 0) s_wnan[wid] = anynan ? 1 : 0;
   }
   __syncthreads();  // also orders the counters' zeroing before the count
-  QF_STAMP(9);
-  double gmn = s_wmin_v[0], gmx = s_wmax_v[0];
-  int gnan = s_wnan[0];
+  if (wid == 0) {
+    constexpr int PER = BLOCK / 64;
+    double mn = sval[lane * PER], mx = sval[BLOCK + lane * PER];
 #pragma unroll
-  for (int w = 1; w < WAVES; ++w) {
-    gmn = fmin(gmn, s_wmin_v[w]);
-    gmx = fmax(gmx, s_wmax_v[w]);
-    gnan |= s_wnan[w];
+    for (int i = 1; i < PER; ++i) {
+      mn = fmin(mn, sval[lane * PER + i]);
+      mx = fmax(mx, sval[BLOCK + lane * PER + i]);
+    }
+    mn = wave_min_f64_dpp(mn);
+    mx = wave_max_f64_dpp(mx);
+    int anyn = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) anyn |= s_wnan[w];
+    if (lane == 63) {
+      s_wmin_v[0] = mn;
+      s_wmax_v[0] = mx;
+      s_gnan = anyn;
+    }
   }
+  __syncthreads();
+  QF_STAMP(9);
+  const double gmn = s_wmin_v[0], gmx = s_wmax_v[0];
+  const int gnan = s_gnan;
   // folded keys as join_sort_kernel: kmin <-> the largest score, -0.0 == +0.0
   const uint64_t kmin = ~f64_asc_key(gmx), kmax = ~f64_asc_key(gmn);
   const bool nan = gnan != 0;
