@@ -1615,18 +1615,29 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
                : 0u;
     old[j] = atomicAdd(&bkw[ws[j] >> 1], ok ? 1u << ((ws[j] & 1u) * 16u) : 0u);
   }
+  // a bucket above kJsBucketMax items <=> some item arrived at index >= kJsBucketMax
+  bool bigl = false;
 #pragma unroll
-  for (int j = 0; j < ROWS; ++j)
-    ws[j] |= ((old[j] >> ((ws[j] & 1u) * 16u)) & 0xFFFFu) << 16;
+  for (int j = 0; j < ROWS; ++j) {
+    const uint32_t at = (old[j] >> ((ws[j] & 1u) * 16u)) & 0xFFFFu;
+    bigl |= at >= (uint32_t)kJsBucketMax;
+    ws[j] |= at << 16;
+  }
+  {
+    const bool wbig = ballot(bigl) != 0ull;
+    if (lane == 0) s_wmax[wid] = wbig ? 1u : 0u;
+  }
   QF_STAMP(10);
   __syncthreads();
   QF_STAMP(11);
-  // ---- 2. exclusive scan of the counters, largest bucket ---------------------------
-  bool big;
+  // ---- 2. exclusive scan of the counters ---------------------------------------------
+  bool big = false;
+#pragma unroll
+  for (int w = 0; w < WAVES; ++w) big |= s_wmax[w] != 0u;
   {
     constexpr int kPer = NB / BLOCK;  // u16 counters per thread
     static_assert(kPer % 8 == 0 || kPer == 4, "uint4 / uint2 counter loads");
-    uint32_t c[kPer], tot = 0u, mx = 0u;
+    uint32_t c[kPer], tot = 0u;
 #pragma unroll
     for (int i = 0; i < kPer; i += 2) {
       const uint32_t x = bkw[(tid * kPer + i) / 2];
@@ -1635,24 +1646,17 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      mx = max(mx, c[i]);
       const uint32_t x = c[i];
       c[i] = tot;
       tot += x;
     }
     const uint32_t incl = wave_incl_scan_dpp(tot);
     if (lane == 63) s_wtot[wid] = incl;
-    mx = (uint32_t)wave_max_u64_dpp(mx);
-    if (lane == 63) s_wmax[wid] = mx;
     __syncthreads();
     uint32_t pre = incl - tot;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w)
       if (w < wid) pre += s_wtot[w];
-    uint32_t bmax = 0u;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) bmax = max(bmax, s_wmax[w]);
-    big = bmax > (uint32_t)kJsBucketMax;
 #pragma unroll
     for (int i = 0; i < kPer; i += 2)
       bkw[(tid * kPer + i) / 2] = (pre + c[i]) | ((pre + c[i + 1]) << 16);
