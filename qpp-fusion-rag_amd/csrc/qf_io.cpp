@@ -759,45 +759,92 @@ int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const 
   const size_t tl = strlen(tag);
   const int T = std::max(1, omp_get_max_threads());
   const int64_t chunks = std::min<int64_t>(std::max<int64_t>(n_out, 1), (int64_t)T * 8);
-  std::vector<std::string> buf((size_t)chunks);
-#pragma omp parallel for schedule(dynamic, 1)
+  // Each chunk of queries is formatted into a raw buffer sized by an upper bound
+  // (no per-field string appends, no snprintf for the rank), then every chunk is
+  // written at its offset with pwrite, in parallel.
+  std::vector<char*> buf((size_t)chunks, nullptr);
+  std::vector<size_t> len((size_t)chunks, 0);
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
   for (int64_t c = 0; c < chunks; ++c) {
     const int64_t a = n_out * c / chunks, b = n_out * (c + 1) / chunks;
-    std::string& s = buf[(size_t)c];
-    size_t est = 0;
-    for (int64_t i = a; i < b; ++i) est += (size_t)std::max(counts[order[i]], 0) * (48 + tl);
-    s.reserve(est);
-    char line[512];
+    size_t cap = 1 << 16;
     for (int64_t i = a; i < b; ++i) {
+      const int64_t q = order[i];
+      if (counts[q] > 0)
+        cap += (size_t)counts[q] * ((size_t)(qid_off[q + 1] - qid_off[q]) + tl + 48);
+    }
+    char* o = (char*)malloc(cap);
+    if (!o) { err |= 1; continue; }
+    size_t used = 0;
+    for (int64_t i = a; i < b && o; ++i) {
       const int64_t q = order[i];
       const int64_t base = qbase[q];
       const int32_t n = counts[q];
-      const std::string_view qid(qid_chars + qid_off[q], (size_t)(qid_off[q + 1] - qid_off[q]));
+      const char* qs = qid_chars + qid_off[q];
+      const size_t ql = (size_t)(qid_off[q + 1] - qid_off[q]);
       for (int32_t k = 0; k < n; ++k) {
         const uint32_t d = union_docid[base + perm[base + k]];
-        s.append(qid.data(), qid.size());
-        s.append(" Q0 ", 4);
-        s.append(docno_chars + docno_off[d], (size_t)(docno_off[d + 1] - docno_off[d]));
-        size_t o = 0;
-        line[o++] = ' ';
-        o += (size_t)snprintf(line + o, 32, "%d", k + 1);
-        line[o++] = ' ';
-        o += fmt6(fused[base + k], line + o);
-        line[o++] = ' ';
-        s.append(line, o);
-        s.append(tag, tl);
-        s.push_back('\n');
+        const size_t dl = (size_t)(docno_off[d + 1] - docno_off[d]);
+        // a line is at most qid + docno + tag + 430 bytes (rank <= 10 digits, score < 400)
+        if (cap - used < ql + dl + tl + 430) {
+          cap = 2 * cap + ql + dl + tl + 430;
+          char* g = (char*)realloc(o, cap);
+          if (!g) { free(o); o = nullptr; err |= 1; break; }
+          o = g;
+        }
+        char* w = o + used;
+        memcpy(w, qs, ql);
+        w += ql;
+        memcpy(w, " Q0 ", 4);
+        w += 4;
+        memcpy(w, docno_chars + docno_off[d], dl);
+        w += dl;
+        *w++ = ' ';
+        {  // rank k + 1, decimal
+          char t[12];
+          int m = 0;
+          uint32_t v = (uint32_t)k + 1u;
+          do { t[m++] = (char)('0' + v % 10u); v /= 10u; } while (v);
+          while (m) *w++ = t[--m];
+        }
+        *w++ = ' ';
+        w += fmt6(fused[base + k], w);
+        *w++ = ' ';
+        memcpy(w, tag, tl);
+        w += tl;
+        *w++ = '\n';
+        used = (size_t)(w - o);
       }
     }
+    buf[(size_t)c] = o;
+    len[(size_t)c] = o ? used : 0;
   }
-  FILE* fp = fopen(path, "wb");
-  if (!fp) return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(errno));
-  for (auto& s : buf)
-    if (!s.empty() && fwrite(s.data(), 1, s.size(), fp) != s.size()) {
-      fclose(fp);
-      return fail(QFIO_EIO, std::string("short write to ") + path);
+  if (err) {
+    for (char* p : buf) free(p);
+    return fail(QFIO_EIO, "qfio_write_run: out of memory");
+  }
+  std::vector<off_t> at((size_t)chunks + 1, 0);
+  for (int64_t c = 0; c < chunks; ++c) at[(size_t)c + 1] = at[(size_t)c] + (off_t)len[(size_t)c];
+  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) {
+    for (char* p : buf) free(p);
+    return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(errno));
+  }
+  int werr = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : werr)
+  for (int64_t c = 0; c < chunks; ++c) {
+    size_t done = 0;
+    while (done < len[(size_t)c]) {
+      const ssize_t r = pwrite(fd, buf[(size_t)c] + done, len[(size_t)c] - done,
+                               at[(size_t)c] + (off_t)done);
+      if (r <= 0) { werr |= 1; break; }
+      done += (size_t)r;
     }
-  if (fclose(fp) != 0) return fail(QFIO_EIO, std::string("cannot close ") + path);
+    free(buf[(size_t)c]);
+    buf[(size_t)c] = nullptr;
+  }
+  if (close(fd) != 0 || werr) return fail(QFIO_EIO, std::string("short write to ") + path);
   return QFIO_OK;
 }
 
