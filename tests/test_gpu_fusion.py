@@ -114,6 +114,38 @@ def test_fuse_f64_scores_bit_exact(gpu):
             np.testing.assert_array_equal(p[b:b + n], o_perm[b:b + n])
 
 
+def test_bucket_sort_weight_extremes(gpu):
+    """The join + bucket-sort path (1,500 entries per query) with the weights that stress
+    its key: zero weights (hundreds of documents tied at the minimum), weights 1e-12 next
+    to 1 (documents packed just above the minimum), negative weights and -0.0 (negative
+    scores, signed zeros), 1e300 (a range near the f64 limit) — bit-exact vs the oracle."""
+    from qppfuse import engine
+    Q, R, K = 72, 5, 300
+    off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=21)
+    rng = np.random.default_rng(21)
+    cases = [[0.0, 0.0, 0.5, 0.3, 0.0], [1e-12, 1.0, 1.0, 1e-12, 1.0],
+             [-0.5, 0.2, -1.0, 0.0, 0.7], [-0.0] * 5, [1e300, 1e300, 1.0, 1.0, 1.0],
+             list(rng.random(5))]
+    w_h = np.array([cases[q % len(cases)] for q in range(Q)], np.float64).ravel()
+    w = torch.from_numpy(w_h).to(gpu)
+    out = engine.fuse(off, docid, micro, R, ALL, rrf_k=60, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    uc = out.union_count.cpu().numpy()
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fused = out.fused.cpu().numpy()
+    assert (uc > 0).all()
+    for m, name in enumerate(ALL):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60, weights=w_h)
+        np.testing.assert_array_equal(uc, o_uc)
+        for q in range(Q):
+            b, n = off_h[q * R], uc[q]
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=f"{name} q{q}")
+            assert fused[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
 def _csr(lists, device):
     off = np.cumsum([0] + [len(l[0]) for l in lists]).astype(np.int64)
     doc = np.concatenate([np.asarray(l[0], np.uint32) for l in lists] or [np.zeros(0, np.uint32)])
