@@ -652,12 +652,16 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     if (e < N) {
       const uint32_t msk = mask_of(dk[j]);
       rj[j] |= msk << 16;  // the final mask, kept: r | mask << 16 (no second LDS read)
-      rep = (uint32_t)(__ffs(msk) - 1) == (rj[j] & 0xFFFFu);
+      rep = (uint32_t)(__ffs(msk) - 1) == (rj[j] & 0xFu);
       pc = rep ? (uint32_t)__popc(msk) : 0u;
     }
     repm |= (uint32_t)rep << j;
     const uint64_t b = ballot(rep);
-    const uint32_t tot = readlane_u32(wave_incl_scan_dpp(pc), 63);
+    const uint32_t incl = wave_incl_scan_dpp(pc);
+    // the wave-exclusive group prefix, kept for the placement below:
+    // rj = r (4 bits) | prefix (<= 16 x 64, 11 bits) << 4 | mask << 16
+    rj[j] |= (incl - pc) << 4;
+    const uint32_t tot = readlane_u32(incl, 63);
     if (lane == 0) {
       sh.cnt[j * WAVES + wid] = __popcll(b);
       sh.gof[j * WAVES + wid] = (int)tot;
@@ -686,12 +690,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   for (int j = 0; j < ITEMS; ++j) {
     const bool rep = (repm >> j) & 1u;
     const uint64_t b = ballot(rep);
-    uint32_t msk = 0u, pc = 0u;
-    if (rep) {
-      msk = rj[j] >> 16;
-      pc = (uint32_t)__popc(msk);
-    }
-    const uint32_t gpre = wave_incl_scan_dpp(pc) - pc;
+    const uint32_t gpre = (rj[j] >> 4) & 0x7FFu;
     if (rep) {
       const uint32_t u = (uint32_t)sh.cnt[j * WAVES + wid] + mbcnt(b);
       const uint32_t go = (uint32_t)sh.gof[j * WAVES + wid] + gpre;
@@ -707,7 +706,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     const int e = j * BLOCK + tid;
     if (e < N) {
       const uint32_t gu = tkey[dk[j]];
-      const uint32_t r = rj[j] & 0xFFFFu;
+      const uint32_t r = rj[j] & 0xFu;
       const uint32_t k = (gu & 0xFFFFu) + (uint32_t)__popc((rj[j] >> 16) & ((1u << r) - 1u));
       const uint32_t u = ((repm >> j) & 1u) ? gu >> 16 : 0u;
       dk[j] = k | (u << 16);
@@ -722,7 +721,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
     if (e < N) {
-      const uint32_t k = dk[j] & 0xFFFFu, r = rj[j] & 0xFFFFu;
+      const uint32_t k = dk[j] & 0xFFFFu, r = rj[j] & 0xFu;
       gsc[k] = sc[j];
       gpr[k] = (uint32_t)(base + e - sh.off[r]) | (r << 16);
       if ((repm >> j) & 1u) ugo[dk[j] >> 16] = (uint16_t)k;
