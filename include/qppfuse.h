@@ -232,6 +232,38 @@ int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters
                        int32_t n_runs, const int32_t* run_to_booster, double* w_out,
                        void* stream);
 
+/*
+ * FusionMLP learned fusion (src/models/mlp_model.py:254-274 predict, called by
+ * src/fusion.py:429 -> replaces `pred_weights = model.predict(X)` for the MLP model
+ * and the weights' lookup at :440).  Model input i is X[q*x_cols + in_col[i]]
+ * (in_col: DEVICE int32 [widths[0]], _filter_features' column map), rounded to
+ * float32.  n_layers Linear layers, widths[0..n_layers] (HOST array, each <= 512,
+ * outputs <= 32), ReLU between them; params (DEVICE float32) holds layer l's
+ * W [widths[l+1]][widths[l]] then b [widths[l+1]], layer after layer.  The output
+ * goes through softmax and _normalize_weights (src/models/base.py:120-125) in
+ * float32; w_out[q*n_runs + r] = weight of output run_to_output[r] (HOST array), or
+ * 1/widths[n_layers] for -1.  The float32 operation order is fixed (see
+ * csrc/qf_learn.hip); torch's CPU/MPS kernels round differently by a few ulps.
+ */
+int qf_mlp_weights(int64_t n_queries, const double* X, int32_t x_cols, const int32_t* in_col,
+                   int32_t n_layers, const int32_t* widths, const float* params,
+                   int32_t n_runs, const int32_t* run_to_output, double* w_out, void* stream);
+
+/*
+ * qf_fuse(QF_LEARNED) with FusionMLP's float32 weights (src/fusion.py:436-441
+ * under numpy 2: row["score"] * np.float32 is a float32 product).  Bit r of
+ * f32_runs: run r's weight is a float32 model output (its products round to
+ * float32); runs without the bit (unknown to the model: 1.0 / n_retrievers) take
+ * float64 products.  With every run's bit set the groupby sum is float32 Kahan
+ * (pandas' float32 column), otherwise float64 Kahan.  Outputs as qf_fuse, one
+ * method (QF_LEARNED).
+ */
+int qf_fuse_learned_f32(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                        const uint32_t* docid, const void* score, int32_t score_kind,
+                        const double* weights, uint32_t f32_runs, int32_t max_entries,
+                        uint32_t* union_docid, int32_t* union_count, uint16_t* perm,
+                        double* fused, int64_t out_stride, void* stream);
+
 /* ---- IR evaluation (trec_eval semantics, as ir_measures computes them) ---- */
 #define QF_EVAL_NDCG 0 /* nDCG@k   */
 #define QF_EVAL_RR   1 /* RR@k     */

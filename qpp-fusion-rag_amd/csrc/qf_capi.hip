@@ -101,7 +101,7 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
                        int32_t rrf_k, const double* seg_prob, int32_t n_seg, int32_t seg_len,
                        int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
                        uint16_t* perm, double* fused, int64_t out_stride, void* stream,
-                       const char* fn) {
+                       const char* fn, uint32_t learned_f32 = 0u) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "%s: n_retrievers must be in [1, %d]", fn, kMaxR);
   if (methods <= 0 ||
@@ -125,6 +125,11 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
   qf::FuseParams p{n_queries, n_retrievers, list_off,    docid,       score, rank,
                    weights,   methods,      rrf_k,       union_docid, union_count,
                    perm,      fused,        out_stride,  seg_prob,    n_seg, seg_len};
+  if (learned_f32) {
+    const uint32_t all = n_retrievers == 32 ? 0xFFFFFFFFu : (1u << n_retrievers) - 1u;
+    p.learned_f32 = learned_f32 & all;
+    p.learned_sum_f32 = (learned_f32 & all) == all;
+  }
   return check(qf::fuse_launch(p, score_kind, max_entries < 1 ? 1 : max_entries,
                                (hipStream_t)stream),
                fn);
@@ -152,6 +157,17 @@ int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* lis
   return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
                      methods, rrf_k, seg_prob, n_segments, seg_len, max_entries, union_docid,
                      union_count, perm, fused, out_stride, stream, "qf_fuse_probfuse");
+}
+
+int qf_fuse_learned_f32(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                        const uint32_t* docid, const void* score, int32_t score_kind,
+                        const double* weights, uint32_t f32_runs, int32_t max_entries,
+                        uint32_t* union_docid, int32_t* union_count, uint16_t* perm,
+                        double* fused, int64_t out_stride, void* stream) {
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, nullptr,
+                     weights, QF_LEARNED, 60, nullptr, 0, 0, max_entries, union_docid,
+                     union_count, perm, fused, out_stride, stream, "qf_fuse_learned_f32",
+                     f32_runs);
 }
 
 int qf_fused_topk(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
@@ -249,6 +265,48 @@ int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters
   p.n_runs = n_runs;
   p.w_out = w_out;
   return check(qf::learned_weights_launch(p, (hipStream_t)stream), "qf_learned_weights");
+}
+
+int qf_mlp_weights(int64_t n_queries, const double* X, int32_t x_cols, const int32_t* in_col,
+                   int32_t n_layers, const int32_t* widths, const float* params,
+                   int32_t n_runs, const int32_t* run_to_output, double* w_out, void* stream) {
+  if (n_queries < 0 || x_cols <= 0 || n_layers <= 0 || n_layers > qf::kMlpMaxLayers ||
+      !widths || n_runs <= 0 || n_runs > qf::kMaxLearnedRuns || !run_to_output)
+    return fail(QF_EINVAL, "qf_mlp_weights: bad sizes (1..%d layers, 1..%d runs)",
+                qf::kMlpMaxLayers, qf::kMaxLearnedRuns);
+  qf::MlpParams p{};
+  int64_t off = 0;
+  for (int l = 0; l <= n_layers; ++l) {
+    if (widths[l] <= 0 || widths[l] > qf::kMlpMaxWidth)
+      return fail(QF_EINVAL, "qf_mlp_weights: width[%d] = %d outside [1, %d]", l, widths[l],
+                  qf::kMlpMaxWidth);
+    p.width[l] = widths[l];
+    if (l > 0) {
+      p.w_off[l - 1] = off;
+      off += (int64_t)widths[l - 1] * widths[l];
+      p.b_off[l - 1] = off;
+      off += widths[l];
+    }
+  }
+  if (widths[n_layers] > qf::kMlpMaxOut)
+    return fail(QF_EINVAL, "qf_mlp_weights: %d outputs exceed %d", widths[n_layers],
+                qf::kMlpMaxOut);
+  for (int r = 0; r < n_runs; ++r) {
+    if (run_to_output[r] < -1 || run_to_output[r] >= widths[n_layers])
+      return fail(QF_EINVAL, "qf_mlp_weights: run_to_output[%d] out of range", r);
+    p.run_to_output[r] = run_to_output[r];
+  }
+  if (n_queries == 0) return QF_OK;
+  if (!X || !in_col || !params || !w_out) return fail(QF_EINVAL, "qf_mlp_weights: null buffer");
+  p.n_queries = n_queries;
+  p.X = X;
+  p.x_cols = x_cols;
+  p.in_col = in_col;
+  p.n_layers = n_layers;
+  p.params = params;
+  p.n_runs = n_runs;
+  p.w_out = w_out;
+  return check(qf::mlp_weights_launch(p, (hipStream_t)stream), "qf_mlp_weights");
 }
 
 int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,

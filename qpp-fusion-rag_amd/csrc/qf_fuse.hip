@@ -397,6 +397,39 @@ __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
 }
 
 // ---- one document's fused scores --------------------------------------------
+// learned_fusion's row term and groupby-sum step (src/fusion.py:436-441): pandas
+// Kahan summation in the column's dtype.  LightGBM weights are float64; FusionMLP's
+// are float32, and under numpy 2 row["score"] * np.float32 is a float32 product, so
+// its column is float32 (summed in float32) unless some run is unknown to the
+// model (1.0 / n_retrievers: float64 products, a float64 column).
+__device__ __forceinline__ void learned_add(const FuseParams& p, double s, double w, int r,
+                                            double& a, double& c) {
+  if (p.learned_f32 == 0u) {
+    const double y = s * w - c;
+    const double t = a + y;
+    c = (t - a) - y;
+    if (c != c) c = 0.0;  // +-inf contributions (pandas GH#53606)
+    a = t;
+    return;
+  }
+  const double v = ((p.learned_f32 >> r) & 1u) ? (double)((float)s * (float)w) : s * w;
+  if (p.learned_sum_f32) {
+    const float af = (float)a, cf = (float)c;
+    const float y = (float)v - cf;
+    const float t = af + y;
+    float cn = (t - af) - y;
+    if (cn != cn) cn = 0.0f;
+    c = cn;
+    a = t;
+  } else {
+    const double y = v - c;
+    const double t = a + y;
+    c = (t - a) - y;
+    if (c != c) c = 0.0;
+    a = t;
+  }
+}
+
 // Per-list constants of one query (ranx min-max end points, QPP weights, offsets).
 struct ListConsts {
   const int64_t* off;  // [R + 1] absolute list offsets
@@ -448,13 +481,7 @@ struct DocSums {
       if (methods & QF_WRRF_MUL)  // QPPrrf_argmax.py:71: weight * (1.0 / (k + rank))
         a8 += lc.w[r] * recip_int(p.rrf_k + rk);
     }
-    if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
-      const double y = s * lc.w[r] - c6;
-      const double t = a6 + y;
-      c6 = (t - a6) - y;
-      if (c6 != c6) c6 = 0.0;  // +-inf contributions (pandas GH#53606)
-      a6 = t;
-    }
+    if (methods & QF_LEARNED) learned_add(p, s, lc.w[r], r, a6, c6);  // src/fusion.py:436-446
   }
   // cnt: the document's list count (CombMNZ: sum x count, src/fusion.py:327).
   // Output slot of method bit t: the requested methods below it (scalar popcounts).
@@ -834,13 +861,7 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
         if (methods & QF_WRRF_MUL)  // QPPrrf_argmax.py:71: weight * (1.0 / (k + rank))
           a8 += sh.w[r] * recip_int(rrf_k + rk);
       }
-      if (methods & QF_LEARNED) {  // src/fusion.py:436-446: pandas groupby sum (Kahan)
-        const double y = s * sh.w[r] - c6;
-        const double t = a6 + y;
-        c6 = (t - a6) - y;
-        if (c6 != c6) c6 = 0.0;  // +-inf contributions (pandas GH#53606)
-        a6 = t;
-      }
+      if (methods & QF_LEARNED) learned_add(p, s, sh.w[r], r, a6, c6);  // src/fusion.py:436-446
     }
     const double cnt = (double)(ge - gs);  // CombMNZ: sum x count (src/fusion.py:327)
     double* out = p.fused + base + u;

@@ -33,6 +33,10 @@ struct FuseParams {
   int64_t out_stride;
   const double* seg_prob;  // QF_PROBFUSE: [R][n_seg] segment probabilities
   int32_t n_seg, seg_len;  // x and L of ProbFuse.py
+  // QF_LEARNED with FusionMLP's float32 weights (qf_fuse_learned_f32): bit r set =
+  // run r's products are float32; learned_sum_f32 = the groupby sum is float32 Kahan
+  uint32_t learned_f32;
+  int32_t learned_sum_f32;
 };
 
 // IR evaluation (qf_eval): run m, query q reads its ranked list at
@@ -89,6 +93,27 @@ struct LearnedWeightParams {
 };
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st);
 hipError_t learned_weights_launch(const LearnedWeightParams& p, hipStream_t st);
+
+// FusionMLP inference + weights (qf_mlp_weights): Linear layers (ReLU between,
+// Dropout = identity in eval), softmax, _normalize_weights, all in float32.
+constexpr int kMlpMaxLayers = 8;
+constexpr int kMlpMaxWidth = 512;  // inputs and every layer's width
+constexpr int kMlpMaxOut = 32;     // retrievers the model predicts weights for
+struct MlpParams {
+  int64_t n_queries;
+  const double* X;        // [n_queries][x_cols] the learned_fusion feature matrix
+  int32_t x_cols;
+  const int32_t* in_col;  // [width[0]] column of X feeding model input i
+  int32_t n_layers;
+  int32_t width[kMlpMaxLayers + 1];
+  int64_t w_off[kMlpMaxLayers];  // layer l: W [width[l+1]][width[l]] at params + w_off[l],
+  int64_t b_off[kMlpMaxLayers];  //          b [width[l+1]] at params + b_off[l]
+  const float* params;
+  int32_t n_runs;
+  int32_t run_to_output[kMaxLearnedRuns];
+  double* w_out;  // [n_queries][n_runs]
+};
+hipError_t mlp_weights_launch(const MlpParams& p, hipStream_t st);
 
 int fuse_max_entries();
 hipError_t eval_launch(const EvalParams& p, hipStream_t st);

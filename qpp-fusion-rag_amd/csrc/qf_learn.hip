@@ -18,6 +18,17 @@
 // learned_weights_kernel — one thread per query: numpy's clip (NaN kept, -0.0
 //   becomes +0.0 — measured on numpy 2.2), numpy's row sum (0.0 + pairwise_sum: sequential below 8
 //   values, 8 accumulators from 8), the zero guard and the division.
+// mlp_weights_kernel — FusionMLP.predict (src/models/mlp_model.py:254-274), one
+//   wave per query: the selected QPP columns (_filter_features, :104-122) rounded
+//   to float32 (torch.FloatTensor), Linear -> ReLU -> (Dropout: identity in eval)
+//   ... -> Linear, softmax, then _normalize_weights in float32.  The order of every
+//   float32 operation is fixed (no contraction: each product and sum rounds):
+//     y[o] = (sum_i x[i] * W[o][i], i ascending, from +0.0) + b[o]
+//     softmax: m = max z; e = float(exp(double(z - m))); s = sum e (ascending,
+//              from 0); p = e / s
+//   so oracle/mlp_oracle.py restates it bit for bit.  torch's CPU GEMM / softmax
+//   (and the MPS device the reference trained on) accumulate in other orders:
+//   tests/test_gpu_learned.py holds the two within float32 rounding.
 #include <math.h>
 
 #include "../../include/qppfuse.h"
@@ -91,6 +102,84 @@ __global__ __launch_bounds__(256) void learned_weights_kernel(LearnedWeightParam
     const int j = p.run_to_booster[r];
     p.w_out[q * p.n_runs + r] = j >= 0 ? c[j] / s : dflt;
   }
+}
+
+// numpy's float32 pairwise_sum for n < 128 (float32 accumulators)
+__device__ __forceinline__ float np_pairwise_sum_f32(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+constexpr int kMlpWaves = 4;  // queries per workgroup (one wave each)
+
+__global__ __launch_bounds__(64 * kMlpWaves) void mlp_weights_kernel(MlpParams p) {
+#pragma clang fp contract(off)
+  __shared__ float act[kMlpWaves][2][kMlpMaxWidth];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t q = block_id() * kMlpWaves + wid;
+  const bool live = q < p.n_queries;  // every wave reaches every barrier
+  float* cur = act[wid][0];
+  float* nxt = act[wid][1];
+  for (int i = lane; i < p.width[0]; i += 64)
+    cur[i] = live ? (float)p.X[q * p.x_cols + p.in_col[i]] : 0.0f;  // torch.FloatTensor(X)
+  __syncthreads();
+  for (int l = 0; l < p.n_layers; ++l) {
+    const int n_in = p.width[l], n_o = p.width[l + 1];
+    const float* W = p.params + p.w_off[l];
+    const float* b = p.params + p.b_off[l];
+    const bool relu = l + 1 < p.n_layers;
+    for (int o = lane; o < n_o; o += 64) {
+      const float* wr = W + (int64_t)o * n_in;
+      float acc = 0.0f;
+      for (int i = 0; i < n_in; ++i) acc = acc + cur[i] * wr[i];
+      acc = acc + b[o];
+      if (relu && acc < 0.0f) acc = 0.0f;  // nn.ReLU (NaN passes through)
+      nxt[o] = acc;
+    }
+    __syncthreads();
+    float* t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  if (!live || lane != 0) return;
+  const int n_out = p.width[p.n_layers];
+  float e[kMlpMaxOut];
+  float m = cur[0];
+  for (int o = 1; o < n_out; ++o) m = fmaxf(m, cur[o]);
+  float s = 0.0f;
+  for (int o = 0; o < n_out; ++o) {
+    e[o] = (float)exp((double)(cur[o] - m));
+    s = s + e[o];
+  }
+  for (int o = 0; o < n_out; ++o) {
+    const float v = e[o] / s;
+    e[o] = (v > 0.0f || isnan(v)) ? v : 0.0f;  // np.clip(weights, 0, None)
+  }
+  float sum = 0.0f + np_pairwise_sum_f32(e, n_out);
+  if (sum == 0.0f) sum = 1.0f;
+  const double dflt = 1.0 / (double)n_out;  // src/fusion.py:440: 1.0 / n_retrievers
+  for (int r = 0; r < p.n_runs; ++r) {
+    const int j = p.run_to_output[r];
+    p.w_out[q * p.n_runs + r] = j >= 0 ? (double)(e[j] / sum) : dflt;
+  }
+}
+
+hipError_t mlp_weights_launch(const MlpParams& p, hipStream_t st) {
+  if (p.n_queries == 0) return hipSuccess;
+  hipLaunchKernelGGL(mlp_weights_kernel, grid_for((p.n_queries + kMlpWaves - 1) / kMlpWaves),
+                     dim3(64 * kMlpWaves), 0, st, p);
+  return hipGetLastError();
 }
 
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st) {

@@ -52,6 +52,9 @@ SIGNATURES = {
     "qf_gbdt_predict": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp]),
     "qf_learned_weights": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "qf_mlp_weights": (C.c_int, [_i64, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "qf_fuse_learned_f32": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, C.c_uint32, _i32,
+                                      _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
 }
 

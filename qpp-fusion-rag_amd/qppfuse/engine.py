@@ -75,9 +75,12 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
          methods, rrf_k: int = 60, weights: Optional[torch.Tensor] = None,
          rank: Optional[torch.Tensor] = None, max_entries: Optional[int] = None,
          out: Optional[FuseOut] = None, seg_prob: Optional[torch.Tensor] = None,
-         n_segments: int = 0, seg_len: int = 0) -> FuseOut:
+         n_segments: int = 0, seg_len: int = 0,
+         learned_f32: Optional[int] = None) -> FuseOut:
     """qf_fuse over every query of a packed run set (see include/qppfuse.h); with
-    "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table."""
+    "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table;
+    methods == ["learned"] with learned_f32 (run bitmask: float32 model weights,
+    FusionMLP), qf_fuse_learned_f32."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
@@ -100,6 +103,14 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
                   _ptr(rank), _ptr(weights), mask, int(rrf_k), _ptr(seg_prob), int(n_segments),
                   int(seg_len), int(max_entries), _ptr(out.union_docid), _ptr(out.union_count),
                   _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], _stream())
+        return out
+    if learned_f32 is not None:
+        if mask != _lib.LEARNED:
+            raise ValueError("learned_f32 applies to methods == ['learned'] only")
+        _lib.call("qf_fuse_learned_f32", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
+                  _ptr(weights), int(learned_f32) & 0xFFFFFFFF, int(max_entries),
+                  _ptr(out.union_docid), _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused),
+                  out.fused.shape[1], _stream())
         return out
     _lib.call("qf_fuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
               _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
@@ -228,3 +239,24 @@ def learned_weights(pred: torch.Tensor, run_to_booster) -> torch.Tensor:
     _lib.call("qf_learned_weights", Q, _ptr(pred.contiguous()), B, len(rb), rb.ctypes.data,
               _ptr(w), _stream())
     return w
+
+
+def mlp_weights(X: torch.Tensor, model, run_to_output) -> torch.Tensor:
+    """qf_mlp_weights: [Q * R] float32 FusionMLP run weights (as float64) from
+    learned_fusion's feature matrix X [Q, n_qpp * n_retrievers] (qppfuse.mlp.MLPModel)."""
+    import numpy as np
+    dev = require_device()
+    if X.dtype != torch.float64 or X.dim() != 2:
+        raise ValueError("X must be float64 [n_queries, n_qpp * n_retrievers]")
+    cols = model.input_columns()
+    if cols.size and int(cols.max()) >= X.shape[1]:
+        raise ValueError(f"the model reads column {int(cols.max())} of a {X.shape[1]}-column X")
+    d = model.to_device(dev)
+    widths = np.ascontiguousarray(model.widths(), dtype=np.int32)
+    ro = np.ascontiguousarray(run_to_output, dtype=np.int32)
+    Q = X.shape[0]
+    w = torch.empty(max(Q * len(ro), 1), dtype=torch.float64, device=dev)
+    _lib.call("qf_mlp_weights", Q, _ptr(X.contiguous()), X.shape[1], _ptr(d["in_col"]),
+              len(widths) - 1, widths.ctypes.data, _ptr(d["params"]), len(ro), ro.ctypes.data,
+              _ptr(w), _stream())
+    return w[:Q * len(ro)]

@@ -241,7 +241,8 @@ def _weights(rs: RunSet, qpp_data, qpp_index: int) -> np.ndarray:
     return w
 
 
-def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np.ndarray]):
+def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np.ndarray],
+            learned_f32: Optional[int] = None):
     import torch
     engine.require_device()
     d = rs.to_device()
@@ -250,7 +251,8 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
     else:
         wd = torch.from_numpy(weights).to(d["list_off"].device)
     out = engine.fuse(d["list_off"], d["docid"], d["score"], rs.n_rankers, list(methods),
-                      rrf_k=rrf_k, weights=wd, rank=d["rank"], max_entries=rs.max_entries())
+                      rrf_k=rrf_k, weights=wd, rank=d["rank"], max_entries=rs.max_entries(),
+                      learned_f32=learned_f32)
     counts = out.union_count.cpu().numpy()[:rs.n_queries]
     bad = np.nonzero(counts < 0)[0]
     if bad.size:
@@ -333,27 +335,36 @@ def weighted_rrf(runs, qpp_data, qpp_index: int = None, k: int = None) -> FusedR
 
 def learned_fusion(runs: Dict[str, pd.DataFrame], qpp_data, model_path: str,
                    retrievers: Optional[List[str]] = None) -> FusedRun:
-    """Fusion with per-query weights from the learned LightGBM model (src/fusion.py:387-448).
+    """Fusion with per-query weights from a learned model (src/fusion.py:387-448).
 
-    The model pickle is read statically (qppfuse.lgbm: no unpickling); the 13·R
-    QPP features go through the boosters on device (qf_gbdt_predict), the
-    predictions are normalised as BaseFusionModel._normalize_weights does
-    (qf_learned_weights), and qf_fuse(QF_LEARNED) forms Σ score·w per document in
-    pandas' groupby-sum order.  Lists come back in docno order, as the
-    reference's groupby returns them."""
+    The model pickle is read statically (qppfuse.lgbm / qppfuse.mlp: no
+    unpickling).  LightGBM (MultiOutputLGBM / PerRetrieverLGBM): the 13·R QPP
+    features go through the boosters on device (qf_gbdt_predict) and are
+    normalised as BaseFusionModel._normalize_weights does (qf_learned_weights).
+    FusionMLP: the selected QPP columns go through the MLP, softmax and the same
+    normalisation in float32 (qf_mlp_weights), and the row products are float32
+    as numpy 2 forms row["score"] * np.float32 (qf_fuse_learned_f32).  Then
+    qf_fuse(QF_LEARNED) forms Σ score·w per document in pandas' groupby-sum order.
+    Lists come back in docno order, as the reference's groupby returns them."""
     import torch
-    from . import lgbm
+    from . import lgbm, mlp
     print(f"[fusion] Running learned fusion from {model_path}...")
     key = (os.path.abspath(model_path), os.path.getmtime(model_path))
     cached = _MODELS.get(key)
     if cached is None:
-        model = lgbm.load_fusion_model(model_path)
-        cached = _MODELS[key] = (model, lgbm.pack_model(model))
+        if mlp.model_kind(model_path) == "FusionMLP":
+            cached = (mlp.load_mlp_model(model_path), None)
+        else:
+            model = lgbm.load_fusion_model(model_path)
+            cached = (model, lgbm.pack_model(model))
+        _MODELS[key] = cached
     model, packed = cached
+    is_mlp = packed is None
     retrievers = list(retrievers or model.retrievers)
     n_qpp = model.n_qpp
-    if len(retrievers) != len(model.boosters):
-        raise ValueError(f"the model predicts {len(model.boosters)} weights but "
+    n_out = model.n_outputs if is_mlp else len(model.boosters)
+    if len(retrievers) != n_out:
+        raise ValueError(f"the model predicts {n_out} weights but "
                          f"{len(retrievers)} retrievers were given")
     rs = _pack(runs)
     Q = rs.n_queries
@@ -366,20 +377,25 @@ def learned_fusion(runs: Dict[str, pd.DataFrame], qpp_data, model_path: str,
             if retriever in qd:
                 X[i, j * n_qpp:(j + 1) * n_qpp] = qd[retriever][:n_qpp]
     dev = engine.require_device()
-    pred = engine.gbdt_predict(torch.from_numpy(X).to(dev), packed)
     # a docno repeated inside one list adds every row (the groupby sum,
     # src/fusion.py:440-441): repeated rows go to virtual runs of their ranker
     rv = _derived(rs, "rows")
     names = [rs.rankers[b] for b in rv.base_ranker] if rv.base_ranker is not None else rs.rankers
-    run_to_booster = [retrievers.index(r) if r in retrievers else -1 for r in names]
-    w = engine.learned_weights(pred, run_to_booster)
-    res = _launch(rv, ["learned"], config.fusion.rrf_k, w)
+    run_to_out = [retrievers.index(r) if r in retrievers else -1 for r in names]
+    Xd = torch.from_numpy(X).to(dev)
+    if is_mlp:
+        w = engine.mlp_weights(Xd, model, run_to_out)
+        f32 = sum(1 << r for r, j in enumerate(run_to_out) if j >= 0)
+        res = _launch(rv, ["learned"], config.fusion.rrf_k, w, learned_f32=f32)
+    else:
+        w = engine.learned_weights(engine.gbdt_predict(Xd, packed), run_to_out)
+        res = _launch(rv, ["learned"], config.fusion.rrf_k, w)
     fused = res["learned"]
     print(f"[fusion] Learned fusion done: {len(fused)} queries")
     return fused
 
 
-_MODELS: Dict[tuple, tuple] = {}  # (path, mtime) -> (FusionModel, PackedModel)
+_MODELS: Dict[tuple, tuple] = {}  # (path, mtime) -> (FusionModel, PackedModel) | (MLPModel, None)
 
 
 # ------------------------------------------------------------------ output ---

@@ -20,6 +20,7 @@ objective leaves it as is.
 """
 from __future__ import annotations
 
+import io
 import pickletools
 import re
 from dataclasses import dataclass, field
@@ -56,6 +57,12 @@ def read_pickle_static(path) -> Any:
     PERSID produce or annotate Opaque placeholders, so nothing from the file is
     ever imported or executed."""
     data = open(path, "rb").read()
+    obj, _ = read_pickle_bytes(data, 0, str(path))
+    return obj
+
+
+def read_pickle_bytes(data: bytes, start: int = 0, what: str = "pickle") -> tuple:
+    """read_pickle_static over data[start:]: (object, offset just past its STOP)."""
     stack: list = []
     memo: Dict[int, Any] = {}
 
@@ -67,12 +74,14 @@ def read_pickle_static(path) -> Any:
         del stack[i:]
         return items
 
-    for op, arg, _ in pickletools.genops(data):
+    f = io.BytesIO(data)
+    f.seek(start)
+    for op, arg, pos in pickletools.genops(f):  # pos: absolute offset (f.tell())
         n = op.name
         if n in ("PROTO", "FRAME"):
             continue
         if n == "STOP":
-            return stack.pop()
+            return stack.pop(), pos + 1
         if n == "MARK":
             stack.append(_MARK)
         elif n in ("EMPTY_DICT",):
@@ -159,7 +168,7 @@ def read_pickle_static(path) -> Any:
                 obj.state = state
         elif n in ("PERSID", "BINPERSID"):
             pid = stack.pop() if n == "BINPERSID" else arg
-            stack.append(Opaque("persistent_id", str(pid)))
+            stack.append(Opaque("persistent_id", str(pid), (pid,)))
         elif n == "POP":
             stack.pop()
         elif n == "POP_MARK":
@@ -167,8 +176,8 @@ def read_pickle_static(path) -> Any:
         elif n == "DUP":
             stack.append(stack[-1])
         else:
-            raise ValueError(f"unsupported pickle opcode {n} in {path}")
-    raise ValueError(f"{path}: pickle without STOP")
+            raise ValueError(f"unsupported pickle opcode {n} in {what}")
+    raise ValueError(f"{what}: pickle without STOP")
 
 
 def _append(obj, items):
@@ -324,9 +333,8 @@ def load_fusion_model(path) -> FusionModel:
         boosters = [_booster_of(models[r]) for r in retrievers]
     else:
         raise NotImplementedError(
-            f"learned fusion model '{model_type}' is not supported on device (LightGBM "
-            f"MultiOutputLGBM / PerRetrieverLGBM only; the reference's FusionMLP pins "
-            f"device='mps', src/models/mlp_model.py:78)")
+            f"learned fusion model '{model_type}' is not a LightGBM model (MultiOutputLGBM / "
+            f"PerRetrieverLGBM; FusionMLP pickles load through qppfuse.mlp.load_mlp_model)")
     if len(boosters) != len(retrievers):
         raise ValueError("model has a different number of boosters and retrievers")
     return FusionModel(model_type, retrievers, n_qpp, boosters)

@@ -143,3 +143,122 @@ def test_learned_fusion_18_runs_and_duplicates(gpu, dups):
     assert list(got.keys()) == sorted(want.keys())
     for q in want:
         assert got[q] == want[q], q
+
+
+# ---- FusionMLP (src/models/mlp_model.py:254-274 through src/fusion.py:387-448) ----
+
+MLP_GOLD = Path(__file__).resolve().parent / "golden" / "mlp"
+MLP_DS = ["nq", "hotpotqa", "scifact"]
+
+
+def _mlp(ds):
+    from qppfuse import mlp
+    return mlp.load_mlp_fixture(MLP_GOLD / f"{ds}_fusion_mlp.json.gz")
+
+
+def _mlp_want(m, X, rb):
+    from oracle import mlp_oracle
+    w = mlp_oracle.predict(m.layers, m.retrievers, m.n_qpp, m.qpp_indices, X)
+    n = len(m.retrievers)
+    return np.column_stack([w[:, j].astype(np.float64) if j >= 0 else np.full(len(X), 1.0 / n)
+                            for j in rb])
+
+
+@pytest.mark.parametrize("ds", MLP_DS)
+def test_mlp_weights_match_restatement(gpu, ds):
+    """qf_mlp_weights == the float32 restatement bit for bit (zeros, constant rows,
+    out-of-range features that saturate the softmax)."""
+    from qppfuse import engine
+    m = _mlp(ds)
+    rng = np.random.default_rng(40)
+    X = _X(rng, 700, m.n_qpp * len(m.retrievers))
+    X[:20] *= 1e3
+    X[20:40] = -X[20:40]
+    X[40] = 0.0
+    rb = [4, -1, 0, 1, 2, 3]
+    got = engine.mlp_weights(torch.from_numpy(X).to(gpu), m, rb).cpu().numpy().reshape(700, 6)
+    assert got.tobytes() == _mlp_want(m, X, rb).tobytes()
+
+
+def test_mlp_weights_wide_model_all_features(gpu):
+    """Every QPP column as input (no _filter_features), layers wider than a wave
+    (128 and 96 lanes' worth of outputs), six outputs: == the restatement."""
+    from qppfuse import engine, mlp
+    rng = np.random.default_rng(41)
+    rets = [f"r{i}" for i in range(6)]
+    widths = [6 * 13, 128, 96, 6]
+    layers = [((rng.standard_normal((o, i)) / np.sqrt(i)).astype(np.float32),
+               (0.1 * rng.standard_normal(o)).astype(np.float32))
+              for i, o in zip(widths[:-1], widths[1:])]
+    m = mlp.MLPModel(rets, 13, list(range(13)), layers)
+    m.validate()
+    X = _X(rng, 300, 6 * 13)
+    rb = list(range(6))
+    got = engine.mlp_weights(torch.from_numpy(X).to(gpu), m, rb).cpu().numpy().reshape(300, 6)
+    assert got.tobytes() == _mlp_want(m, X, rb).tobytes()
+
+
+@pytest.mark.parametrize("ds", MLP_DS)
+def test_mlp_weights_vs_reference_predict(gpu, ds):
+    """Against the reference's own FusionMLP.predict (torch CPU): float32 rounding."""
+    from qppfuse import engine
+    from tests.test_mlp_host import W_ULPS, _arr, _gold, ulp_diff
+    e = _gold()[ds]
+    m = _mlp(ds)
+    X = _arr(e["X"], "<f8", (e["n_rows"], e["cols"]))
+    want = _arr(e["predict"], "<f4", (e["n_rows"], -1))
+    got = engine.mlp_weights(torch.from_numpy(X.copy()).to(gpu), m,
+                             list(range(5))).cpu().numpy().reshape(e["n_rows"], 5)
+    assert np.array_equal(got.astype(np.float32).astype(np.float64), got)  # float32 values
+    assert ulp_diff(got, want).max() <= W_ULPS
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_mlp_learned_fusion_vs_reference(gpu, case, tmp_path):
+    """learned_fusion with the NQ FusionMLP: bit for bit the reference's pandas calls
+    on the restatement's weights (float32 products and a float32 groupby sum for the
+    known rankers; a float64 column once a ranker is unknown), and within float32
+    rounding of the reference's own learned_fusion output."""
+    from oracle import mlp_oracle
+    from qppfuse import fusion
+    from tests.test_mlp_host import _frames, _gold, assert_fused_close
+    c = _gold()["nq"]["fusion"][case]
+    m = _mlp("nq")
+    runs = _frames(c["runs"])
+    got = fusion.learned_fusion(runs, c["qpp"], str(MLP_GOLD / "nq_fusion_mlp.json.gz"))
+    wd = mlp_oracle.weights_dict(runs, c["qpp"], m)
+    want = ref_port.learned_fusion_from_weights(runs, wd, len(m.retrievers))
+    assert list(got.keys()) == sorted(want.keys())
+    for q in want:
+        assert got[q] == want[q], q
+    assert_fused_close(got, c["fused"])
+    p = tmp_path / "learned_mlp.res"
+    fusion.write_runfile(got, str(p), "learned_mlp")
+    assert p.read_text() == ref_port.runfile_text(want, "learned_mlp")
+
+
+@pytest.mark.parametrize("extra", [0, 13])
+def test_mlp_learned_fusion_duplicates(gpu, extra):
+    """Docnos repeated inside a list (virtual runs: every row adds) with only known
+    rankers (float32 column) and with 13 unknown rankers (18 runs, workspace join,
+    float64 column): == the reference's pandas calls bit for bit."""
+    from oracle import mlp_oracle
+    from qppfuse import fusion
+    rng = np.random.default_rng(50 + extra)
+    m = _mlp("scifact")
+    qids = [f"test{i}" for i in range(25)]
+    rankers = list(m.retrievers) + [f"X{i:02d}" for i in range(extra)]
+    runs = _runs(rng, qids, rankers, 30)
+    for r in rankers[::2]:
+        df = runs[r]
+        dup = df.sample(frac=0.2, random_state=int(rng.integers(1 << 30))).copy()
+        dup["score"] = np.round(rng.uniform(0, 1, len(dup)), 6)
+        runs[r] = pd.concat([df, dup], ignore_index=True)
+    qpp = {q: {r: [float(np.round(v, 6)) for v in rng.uniform(0, 1, 13)]
+               for r in m.retrievers} for q in qids}
+    got = fusion.learned_fusion(runs, qpp, str(MLP_GOLD / "scifact_fusion_mlp.json.gz"))
+    wd = mlp_oracle.weights_dict(runs, qpp, m)
+    want = ref_port.learned_fusion_from_weights(runs, wd, len(m.retrievers))
+    assert list(got.keys()) == sorted(want.keys())
+    for q in want:
+        assert got[q] == want[q], q
