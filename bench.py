@@ -373,7 +373,10 @@ def check_parity(p: Pipeline, nq: int):
     h = host_sample(p, nq)
     sc = h["micro"].astype(np.float64) / 1e6
     uc = p.out.union_count[:nq].cpu().numpy()
-    ok = True
+    # the step's min-max micro-units vs the oracle's normalize_scores + "%.6f"
+    o_norm = coracle.minmax_per_query(h["raw"], h["off"])
+    o_micro = np.array([int(f"{v:.6f}".replace(".", "")) for v in o_norm], np.int64)
+    ok = bool(np.array_equal(h["micro"].astype(np.int64), o_micro))
     for m, name in enumerate(p.methods):
         if name not in METHODS:  # learned fusion: checked by tests/test_gpu_learned.py
             continue
@@ -540,6 +543,24 @@ def timed_loop(p: Pipeline, steps: int, world: int, dev) -> float:
     return elapsed
 
 
+def copy_ceiling_gbs(dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
+    """Measured device-to-device copy rate (read + write bytes / s): the practical HBM
+    ceiling next to the 8 TB/s spec peak."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    s1.record()
+    torch.cuda.synchronize()
+    ms = s0.elapsed_time(s1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
 def progress(msg: str):
     """One line on stderr per phase (long runs are not silent; stdout stays one JSON line)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -587,6 +608,7 @@ def main():
     achieved = fbytes / (fuse_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args)
     valu = pmc_valu(args)
+    copy_gbs = copy_ceiling_gbs(dev)
     progress(f"rank {rank}: {elapsed / args.steps * 1e3:.3f} ms/step; parity + NDCG checks")
     parity = check_parity(p, min(args.check, p.Q)) if args.check > 0 else None
     ndcg_vals, eval_ms = ndcg_device(p)
@@ -640,7 +662,9 @@ def main():
                          # the roof it actually meets: VALU issue
                          "valu_issue_frac": None if valu is None else round(
                              valu / N_SIMDS / (fuse_ms * 1e6) / VALU_PEAK_PER_SIMD_NS, 4),
-                         "valu_insts_per_launch": valu},
+                         "valu_insts_per_launch": valu,
+                         "copy_ceiling_gbs": round(copy_gbs, 1),
+                         "frac_of_copy_ceiling": round(achieved / copy_gbs, 4)},
             "cpu_baseline": cpu,
             "parity_vs_oracle": {"queries": min(args.check, p.Q), "bit_exact": parity},
             "ndcg10": {m: round(float(np.nanmean(ndcg_vals[i])), 6)
