@@ -1,0 +1,56 @@
+"""One rank of tests/test_gpu_rccl.py (started by torch.distributed.run, backend nccl =
+RCCL): the path's two collectives on device buffers — the QPP [min, -max] MIN
+all-reduce and the fused top-k gather (async, waited on the stream as bench.py
+pipelines it) — checked against the local values.  Prints "rccl-ok" on success."""
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (ROOT, ROOT / "qpp-fusion-rag_amd"):
+    sys.path.insert(0, str(p))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    local = int(os.environ["LOCAL_RANK"])
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    assert dist.get_backend() == "nccl"
+    world, rank = dist.get_world_size(), dist.get_rank()
+    from qppfuse import engine
+    from qppfuse.dist import PendingGather
+    Q, R, K = 48, 5, 1000
+    off, docid, raw = engine.synth_runs(rank * Q, Q, R, K, seed=11)
+    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+    nt = torch.full((Q,), 4, dtype=torch.int32, device=dev)
+    tf = torch.rand((Q, 2), dtype=torch.float64, device=dev)
+    qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
+    mm = engine.qpp_colminmax(qraw, off, R)
+    want = mm.clone()
+    work = dist.all_reduce(mm, op=dist.ReduceOp.MIN, async_op=True)
+    work.wait()
+    assert torch.equal(mm, want) if world == 1 else bool((mm <= want).all())
+    w = engine.qpp_normalize(qraw, mm, off, R, "minmax", 5)["weights"]
+    out = engine.fuse(off, docid, micro, R, ["combsum", "rrf", "wcombsum"], 60, weights=w,
+                      max_entries=R * K)
+    d, s = engine.fused_topk(out, off, R, 100)
+    dl = [torch.empty_like(d) for _ in range(world)] if rank == 0 else None
+    sl = [torch.empty_like(s) for _ in range(world)] if rank == 0 else None
+    works = [dist.gather(d, dl, dst=0, async_op=True), dist.gather(s, sl, dst=0, async_op=True)]
+    got = PendingGather(works, dl, sl, [Q] * world).wait()
+    torch.cuda.synchronize()
+    if rank == 0:
+        gd, gs = got
+        assert gd.shape == (world * Q, 3, 100)
+        assert torch.equal(gd[:Q], d) and torch.equal(gs[:Q].view(torch.int64), s.view(torch.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+    print("rccl-ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()
