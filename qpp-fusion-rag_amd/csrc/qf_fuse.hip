@@ -896,6 +896,11 @@ void join_kernel(FuseParams p) {
 // ============================================================================
 // fuse_kernel
 // ============================================================================
+// The bucket sorts' limits (join_sort_kernel / bucket_sort_kernel below): unions
+// up to kJsUMax; a (query, method) they leave unsorted has perm[0] = kJsUnsorted.
+constexpr int kJsUMax = 3072;
+constexpr uint16_t kJsUnsorted = 0xFFFF;
+
 template <int BLOCK, int ITEMS, int MINW>
 struct SortCfg {
   static constexpr int kBlock = BLOCK, kItems = ITEMS, kWaves = BLOCK / 64, kMinWaves = MINW;
@@ -1074,8 +1079,10 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_kernel(FuseParam
 // workgroup per CU, each listing the (query, method) pairs of its stride
 // that qualify (one parallel load of their counts) and sorting them in turn —
 // so a batch without large queries costs a few microseconds, not one
-// dispatched workgroup per pair.
-template <class C>
+// dispatched workgroup per pair.  FB: the same pass also takes the pairs the
+// bucket sort left unsorted (perm[0] marked, U <= kJsUMax) — what
+// a separate fallback kernel did, without its launch and scan (~5 us).
+template <class C, bool FB = false>
 __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(FuseParams p,
                                                                             int umin) {
   __shared__ SortShared<C> sh;
@@ -1090,8 +1097,12 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
     __syncthreads();
     const int64_t idx = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
     if (idx < pairs) {
-      const int U = p.union_count[idx / M];
-      if (U >= umin && U <= C::kUMax) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
+      const int64_t q = idx / M;
+      const int U = p.union_count[q];
+      bool take = U >= umin && U <= C::kUMax;
+      if (FB && U > 1 && U <= kJsUMax)
+        take = p.perm[(idx % M) * p.out_stride + p.list_off[q * p.R]] == kJsUnsorted;
+      if (take) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
     }
     __syncthreads();
     const int n = s_n;
@@ -1134,14 +1145,13 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 // Its cost per item is the size of its bucket (C2 with QPP or random weights:
 // 2-2.5 on average, largest buckets ~10-60; tools/bucket_stats.py).  A bucket
 // above kJsBucketMax or a non-finite / NaN score range leaves the (query,
-// method) to fuse_fallback_kernel's LSD window sort (the same order).
+// method) to the LSD window sort of fuse_large_kernel's fallback pass (the same
+// order).
 // Unions above kJsUMax are stored unsorted for fuse_large_kernel.
 // ============================================================================
 constexpr int kJsBits = 12;
 constexpr int kJsBuckets = 1 << kJsBits;
-constexpr int kJsUMax = 3072;
 constexpr int kJsBucketMax = 128;
-constexpr uint16_t kJsUnsorted = 0xFFFF;  // perm[ms][0] of a (query, method) left unsorted
 constexpr int kJsMethods = QF_COMBSUM | QF_COMBMNZ | QF_RRF | QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF;
 
 template <int BLOCK>
@@ -1349,7 +1359,7 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
     const double delta = rng * 0x1p-12;
     const float ftop = (float)(rng + delta);
     // a finite range without NaN (a NaN's key lies beyond +-inf's) and a positive
-    // delta: the bucket sort; otherwise fuse_fallback_kernel's LSD window sort
+    // delta: the bucket sort; otherwise the fallback pass's LSD window sort
     bool fast = isfinite(rng) && isfinite(ftop) && delta > 0.0 && !s_nan[ms];
     const uint32_t b0 = __float_as_uint((float)delta);
     const uint32_t span = __float_as_uint(ftop) - b0;
@@ -1465,7 +1475,7 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
       QF_STAMP(2);
     } else {
       // ---- fallback: the scores go out unsorted (by u), perm[0] marked; the LSD
-      // window sort of fuse_fallback_kernel finishes this (query, method) ---------
+      // window sort of fuse_large_kernel's fallback pass finishes this (query, method) ---------
 #pragma unroll
       for (int j = 0; j < ROWS; ++j) {
         const int u = (wid * rows + j) * 64 + lane;
@@ -1486,7 +1496,7 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
 // (scores by position f64, u by position u16, 2^BITS bucket counters).  Small
 // enough to keep 4 workgroups (32 waves) per CU.  A (query, method) it cannot
 // order (a bucket above kJsBucketMax, a non-finite range, a NaN) gets its perm[0]
-// marked for fuse_fallback_kernel; its scores stay unsorted in place.
+// marked for fuse_large_kernel's fallback pass; its scores stay unsorted in place.
 // ============================================================================
 #ifndef QF_BS_REV
 #define QF_BS_REV 1
@@ -1747,43 +1757,6 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     }
   }
   QF_STAMP(15);
-}
-
-// The (query, method) pairs join_sort_kernel left unsorted (a bucket above
-// kJsBucketMax, or a non-finite score range): a persistent grid like
-// fuse_large_kernel's lists the marked pairs of its stride and sorts them with
-// the LSD window sort (sort_one), which overwrites the marker.
-template <class C>
-__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_fallback_kernel(FuseParams p) {
-  __shared__ SortShared<C> sh;
-  __shared__ int s_list[C::kBlock];
-  __shared__ int s_n;
-  const int tid = threadIdx.x;
-  const int M = __popc(p.methods);
-  const int64_t pairs = p.n_queries * M;
-  const int64_t span = (int64_t)gridDim.x * C::kBlock;
-  for (int64_t c0 = 0; c0 < pairs; c0 += span) {
-    if (tid == 0) s_n = 0;
-    __syncthreads();
-    const int64_t idx = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
-    if (idx < pairs) {
-      const int64_t q = idx / M;
-      const int ms = (int)(idx % M);
-      const int U = p.union_count[q];
-      if (U > 1 && U <= kJsUMax &&
-          p.perm[(int64_t)ms * p.out_stride + p.list_off[q * p.R]] == kJsUnsorted)
-        s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
-    }
-    __syncthreads();
-    const int n = s_n;
-    for (int t = 0; t < n; ++t) {
-      const int64_t id = c0 + s_list[t];
-      const int64_t q = id / M;
-      const int ms = (int)(id % M);
-      sort_one<C>(p, sh, ms, p.union_count[q], p.list_off[q * p.R], false);
-      __syncthreads();
-    }
-  }
 }
 
 // ============================================================================
@@ -2126,7 +2099,6 @@ using SortS = SortCfg<256, 4, 4>;     // U <= 1024
 using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
 using SortXL = SortCfg<1024, 10, 2>;  // U <= 10240
-using SortFb = SortCfg<512, 6, 4>;    // join_sort_kernel's fallback (U <= 3072; no spills)
 
 int fuse_max_entries() { return kXlNMax; }
 
@@ -2145,13 +2117,13 @@ static void launch_sort(const FuseParams& p, int umin, hipStream_t st) {
                      p, umin);
 }
 
-template <class S>
+template <class S, bool FB = false>
 static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st, int per_cu) {
   const int64_t pairs = p.n_queries * __builtin_popcount((unsigned)p.methods);
   const int64_t cap = 256 * per_cu;  // resident workgroups (LDS / VGPR-bound)
   const int64_t grid = pairs < cap ? pairs : cap;
-  hipLaunchKernelGGL((fuse_large_kernel<S>), dim3((unsigned)grid), dim3(S::kBlock), 0, st, p,
-                     umin);
+  hipLaunchKernelGGL((fuse_large_kernel<S, FB>), dim3((unsigned)grid), dim3(S::kBlock), 0, st,
+                     p, umin);
 }
 
 // Queries above the LDS join (QF_QSTATUS_TOOBIG after it): the workspace join,
@@ -2204,12 +2176,9 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     if (jsb == 11) hipLaunchKernelGGL((bucket_sort_kernel<512, 11>), g, dim3(512), 0, st, p);
     else if (jsb == 12) hipLaunchKernelGGL((bucket_sort_kernel<512, 12>), g, dim3(512), 0, st, p);
     else hipLaunchKernelGGL((bucket_sort_kernel<512, 13>), g, dim3(512), 0, st, p);
-    launch_sort_large<SortL>(p, kJsUMax + 1, st, 1);
+    // unions above kJsUMax and the pairs the bucket sort marked: one pass
+    launch_sort_large<SortL, true>(p, kJsUMax + 1, st, 1);
     if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
-    const int64_t pairs = p.n_queries * M;
-    const int64_t gf = pairs < 1024 ? pairs : 1024;
-    hipLaunchKernelGGL((fuse_fallback_kernel<SortFb>), dim3((unsigned)(gf > 0 ? gf : 1)),
-                       dim3(SortFb::kBlock), 0, st, p);
     return hipGetLastError();
   }
   if (kind == 1 && p.R <= kRMax && max_entries <= 5120 && max_entries > JoinS::kNMax &&
@@ -2220,13 +2189,7 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
       hipLaunchKernelGGL((join_sort_kernel<512>), grid_for(p.n_queries), dim3(512), 0, st, p);
     else
       hipLaunchKernelGGL((join_sort_kernel<1024>), grid_for(p.n_queries), dim3(1024), 0, st, p);
-    launch_sort_large<SortL>(p, kJsUMax + 1, st, 1);
-    {
-      const int64_t pairs = p.n_queries * __builtin_popcount((unsigned)p.methods);
-      const int64_t g = pairs < 1024 ? pairs : 1024;  // 4 per CU, resident together
-      hipLaunchKernelGGL((fuse_fallback_kernel<SortFb>), dim3((unsigned)(g > 0 ? g : 1)),
-                         dim3(SortFb::kBlock), 0, st, p);
-    }
+    launch_sort_large<SortL, true>(p, kJsUMax + 1, st, 1);
     return hipGetLastError();
   }
   if (p.R > kRMax) {
