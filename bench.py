@@ -517,7 +517,10 @@ def pmc_traffic(args, kernel_substr="qf_fuse (sum of its kernels)"):
     data = json.loads(files[-1].read_text())
     for name, d in data.items():
         if kernel_substr in name and d.get("hbm_bytes"):
-            return d["hbm_bytes"], f"{files[-1].name}: FETCH_SIZE+WRITE_SIZE x1024"
+            if "fetch_calibration" not in data:  # an old summary: FETCH_SIZE uncorrected
+                return d["hbm_bytes"], f"{files[-1].name}: FETCH_SIZE+WRITE_SIZE x1024"
+            return d["hbm_bytes"], (f"{files[-1].name}: (FETCH_SIZE x2 + WRITE_SIZE) x1024 "
+                                    f"(gfx950 FETCH correction, checked on the min-max kernel)")
     return None, None
 
 

@@ -571,3 +571,71 @@ def test_api_with_18_rankers_matches_port(gpu):
         want = ref_port.ranx_fusion(frames, method, 60)
         for q in want:
             assert got[q] == want[q], (method, q)
+
+
+@pytest.mark.parametrize("methods", [["combmnz"], ["combmnz", "rrf"], ["wcombsum", "wcombmnz"],
+                                     ["combsum", "combmnz", "wcombmnz"],
+                                     ["combsum", "wcombsum", "wcombmnz", "wrrf"]])
+def test_method_subsets_bit_exact(gpu, methods):
+    """Subsets of the six methods (output slots shift with the mask; CombMNZ with and
+    without its CombSUM) bit-exact vs the oracle on the join + bucket-sort path (5 x
+    1,000 entries)."""
+    from qppfuse import engine
+    Q, R, K = 96, 5, 1000
+    off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=31)
+    rng = np.random.default_rng(31)
+    w = torch.from_numpy(rng.random(Q * R).round(6)).to(gpu)
+    out = engine.fuse(off, docid, micro, R, methods, rrf_k=60, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    uc = out.union_count.cpu().numpy()
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fused = out.fused.cpu().numpy()
+    slot = {m: i for i, m in enumerate(sorted(methods, key=ALL.index))}
+    for name in methods:
+        _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60,
+                                                weights=w.cpu().numpy())
+        np.testing.assert_array_equal(uc, o_uc)
+        m = slot[name]
+        for q in range(Q):
+            b, n = off_h[q * R], uc[q]
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=f"{name} q{q}")
+            assert fused[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
+@pytest.mark.parametrize("n", [700, 2561, 3072, 3073, 5120])
+@pytest.mark.parametrize("overlap", [1.0, 0.02])
+@pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform",
+                                  "huge_and_inf"])
+def test_two_runs_on_adversarial_keys(gpu, kind, overlap, n):
+    """W-CombSUM + W-CombMNZ over two runs sharing a fraction of their documents, on the
+    adversarial keys: the join + bucket-sort path, its fallback pass (a bucket above
+    128 items, a non-finite range) and, for unions above 3,072 (up to 10,140),
+    fuse_large_kernel — bit-exact vs the oracle."""
+    from qppfuse import engine
+    rng = np.random.default_rng(hash((kind, n, overlap)) & 0xFFFF)
+    s1, s2 = _sort_case(kind, n, rng), _sort_case(kind, n, rng)
+    if kind == "huge_and_inf":  # no inf - inf = NaN in a shared document's sum
+        s1, s2 = np.abs(s1), np.abs(s2)
+    d1 = np.arange(n, dtype=np.uint32) * 7 + 3
+    shared = int(n * overlap)
+    d2 = np.concatenate([d1[:shared][rng.permutation(shared)],
+                         np.arange(n - shared, dtype=np.uint32) * 7 + 5])
+    off = np.array([0, n, 2 * n], np.int64)
+    doc = np.concatenate([d1, d2])
+    sc = np.concatenate([s1, s2])
+    t = lambda a: torch.from_numpy(a).to(gpu)
+    w_h = np.array([1.0, 0.75])
+    ms = ["wcombsum", "wcombmnz"]
+    out = engine.fuse(t(off), t(doc.view(np.int32)), t(sc), 2, ms, weights=t(w_h),
+                      max_entries=2 * n)
+    uc = int(out.union_count[0])
+    perm = out.perm.cpu().numpy().view(np.uint16)
+    fused = out.fused.cpu().numpy()
+    for m, name in enumerate(ms):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, 2, name, 60, weights=w_h)
+        assert uc == o_uc[0] == 2 * n - shared
+        np.testing.assert_array_equal(perm[m][:uc], o_perm[:uc], err_msg=name)
+        assert fused[m][:uc].tobytes() == o_fused[:uc].tobytes(), name

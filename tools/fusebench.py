@@ -3,12 +3,16 @@ import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
+import os
 import torch
-from qppfuse import engine
+from qppfuse import engine, _lib
+if os.environ.get("QF_LIB"):  # a development build of the same sources
+    _lib.LIB_PATH = Path(os.environ["QF_LIB"])
 Q, R, K = 3452, 5, 1000
 dev = torch.device("cuda", 0)
 off, docid, raw = engine.synth_runs(0, Q, R, K)
 _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+torch.manual_seed(7)
 w = torch.rand(Q * R, dtype=torch.float64, device=dev)
 M = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
 out = engine.alloc_fuse_out(Q, Q * R * K, engine.methods_mask(M), dev)
