@@ -1586,12 +1586,15 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   }
   __syncthreads();  // also orders the counters' zeroing before the count
   if (wid == 0) {
+    // lane-contiguous reads (i * 64 + lane): a lane stride of PER doubles hit 4 of
+    // the 64 banks, a 16-way conflict on every read of the block's critical path.
+    // min / max do not depend on the order (the folded keys below equate -0.0, +0.0)
     constexpr int PER = BLOCK / 64;
-    double mn = sval[lane * PER], mx = sval[BLOCK + lane * PER];
+    double mn = sval[lane], mx = sval[BLOCK + lane];
 #pragma unroll
     for (int i = 1; i < PER; ++i) {
-      mn = fmin(mn, sval[lane * PER + i]);
-      mx = fmax(mx, sval[BLOCK + lane * PER + i]);
+      mn = fmin(mn, sval[i * 64 + lane]);
+      mx = fmax(mx, sval[BLOCK + i * 64 + lane]);
     }
     mn = wave_min_f64_dpp(mn);
     mx = wave_max_f64_dpp(mx);
