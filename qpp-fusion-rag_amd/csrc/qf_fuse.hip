@@ -696,6 +696,9 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   }
   __syncthreads();
   if (wid == 0) {  // exclusive scans over the (row, wave) chunks, in entry order
+    // the block waits on this wave: raised issue priority over the CU's other
+    // workgroups (as the QPP kernel's serial chains)
+    __builtin_amdgcn_s_setprio(3);
     uint32_t c1 = 0, c2 = 0;
     for (int c0 = 0; c0 < ITEMS * WAVES; c0 += 64) {
       const int i = c0 + lane;
@@ -710,6 +713,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       c2 += readlane_u32(i2, 63);
     }
     if (lane == 0) sh.U = (int)c1;
+    __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
   QF_STAMP(5);
@@ -1586,6 +1590,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   }
   __syncthreads();  // also orders the counters' zeroing before the count
   if (wid == 0) {
+    __builtin_amdgcn_s_setprio(3);  // the block waits on this wave (see the join's scans)
     // lane-contiguous reads (i * 64 + lane): a lane stride of PER doubles hit 4 of
     // the 64 banks, a 16-way conflict on every read of the block's critical path.
     // min / max do not depend on the order (the folded keys below equate -0.0, +0.0)
@@ -1606,6 +1611,7 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
       s_wmax_v[0] = mx;
       s_gnan = anyn;
     }
+    __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
   QF_STAMP(9);

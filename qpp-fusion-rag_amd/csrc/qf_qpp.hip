@@ -92,6 +92,23 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // owns prefix i); the sums Java forms left to right are serial chains, and those
 // run batched: one wave, one lane per (list, chain), so a chain costs one lane
 // of one instruction instead of a whole wave's.
+#ifdef QF_STAMPS
+// Diagnostic build only (tools/qpp_stamps.py): per-workgroup phase cycles of wave 0.
+constexpr int kQppStampBlocks = 4096, kQppStampSlots = 8;
+__device__ unsigned long long g_qpp_stamps[kQppStampBlocks * kQppStampSlots];
+#define QPP_STAMP_INIT() unsigned long long _qs_prev = __builtin_amdgcn_s_memtime()
+#define QPP_STAMP(slot)                                                             \
+  do {                                                                              \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                     \
+    if (threadIdx.x == 0 && block_id() < kQppStampBlocks)                           \
+      g_qpp_stamps[block_id() * kQppStampSlots + (slot)] += _t - _qs_prev;          \
+    _qs_prev = _t;                                                                  \
+  } while (0)
+#else
+#define QPP_STAMP_INIT()
+#define QPP_STAMP(slot)
+#endif
+
 constexpr int kQppLists = 8;
 constexpr int kQppBlock = 64 * kQppLists;
 constexpr int kChains = 6;   // cum, smv, wig, skew, snqc, uw
@@ -113,6 +130,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t l = block_id() * kQppLists + w;
   const bool lv = l < n_lists;  // every wave stays for the barriers
+  QPP_STAMP_INIT();
   int k = 0;
   int64_t a = 0;
   if (lv) {
@@ -141,11 +159,17 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     s_fmask[w] = fmask;
   }
   __syncthreads();
+  QPP_STAMP(1);
 
   // ---- B (lane = list): the serial chains that need only rsv, on two waves at once.
   // The serial loops run to kQppK unrolled, their LDS loads issued unconditionally
   // (rows are kRow long; values past k unused) and only the arithmetic predicated,
   // so a chain does not wait one LDS latency per element; every sum keeps its order.
+  // The chains are the workgroup's critical path (its other six waves wait at the
+  // barrier) while the CU's other workgroups keep the SIMD busy: the chain waves run
+  // at raised issue priority (s_setprio), so each dependent step issues as soon as
+  // its operands are ready instead of queueing behind other waves' instructions.
+  if (w <= 1) __builtin_amdgcn_s_setprio(3);
   if (w == 0 && lane < kQppLists) {
     // Java's compensated prefix sums (DoubleStream.average of rsv[0..i]): the
     // chain keeps only the Kahan state; computeFinalSum and the division by
@@ -188,7 +212,9 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     }
     s_sigmax[lane] = sigmax;
   }
+  if (w <= 1) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
+  QPP_STAMP(2);
 
   // ---- C (each list's wave): squared deviations around each prefix mean
   // (lane i = prefix i): simple sum -> NQC of the prefix (NQC, CumNQC),
@@ -247,9 +273,11 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   const double mx = wave_max(act ? x : -INFINITY);
   const double mn = wave_min(act ? x : INFINITY);
   __syncthreads();
+  QPP_STAMP(3);
 
   // ---- D (wave 0, lane = list * 8 + chain): the left-to-right sums, all chains
   // of all lists at once
+  if (w == 0) __builtin_amdgcn_s_setprio(3);  // the critical path again (see B)
   if (w == 0 && (lane & 7) < kChains) {
     const int ll = lane >> 3, c = lane & 7;
     const int kl = s_k[ll];
@@ -263,7 +291,9 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     }
     s_res[ll][c] = acc;
   }
+  if (w == 0) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
+  QPP_STAMP(4);
 
   if (!lv) return;
   double* o = out + l * kQppCols;
@@ -582,3 +612,17 @@ hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64
 }
 
 }  // namespace qf
+
+#ifdef QF_STAMPS
+extern "C" int qf_debug_qpp_stamps(unsigned long long* host, int n, int clear) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(qf::g_qpp_stamps), sizeof(unsigned long long) * n) !=
+      hipSuccess)
+    return 1;
+  if (clear) {
+    static unsigned long long zeros[qf::kQppStampBlocks * qf::kQppStampSlots];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(qf::g_qpp_stamps), zeros, sizeof zeros) != hipSuccess)
+      return 1;
+  }
+  return 0;
+}
+#endif
