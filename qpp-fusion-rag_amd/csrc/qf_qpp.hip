@@ -125,6 +125,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   __shared__ double s_t[kQppLists][kChains][kRow];  // per-element terms of the chains
   __shared__ double s_res[kQppLists][kChains];      // chain sums
   __shared__ double s_sigmax[kQppLists];
+  __shared__ double s_mf[kQppLists];  // SigmaX's compensated mean over F (pass 1)
   __shared__ unsigned long long s_fmask[kQppLists];
   __shared__ int s_k[kQppLists];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -187,11 +188,13 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       }
     }
   } else if (w == 1 && lane < kQppLists) {
-    // SigmaX: compensated mean over F, then the compensated mean of (x - mean)^2
+    // SigmaX, pass 1: the compensated mean over F.  Pass 2 (the compensated mean of
+    // (x - mean)^2) runs in D beside the left-to-right sums: the two passes in a row
+    // were this phase's critical path (100 steps against the prefix chain's 50)
     const int kl = s_k[lane];
     const uint64_t fm = s_fmask[lane];
     const int nf = __popcll(fm);
-    double sigmax = 0.0;
+    double mf = 0.0;
     if (kl >= 2 && nf >= 2) {
       Kahan kf;
       kahan_init(kf);
@@ -200,17 +203,9 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
         const double v = s_x[lane][j];
         if (j < kl && ((fm >> j) & 1ull)) kahan_add(kf, v);
       }
-      const double mf = kahan_final(kf) / (double)nf;
-      Kahan kfv;
-      kahan_init(kfv);
-#pragma unroll
-      for (int j = 0; j < kQppK; ++j) {
-        const double dv = s_x[lane][j] - mf;
-        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
-      }
-      sigmax = sqrt(kahan_final(kfv) / (double)nf);
+      mf = kahan_final(kf) / (double)nf;
     }
-    s_sigmax[lane] = sigmax;
+    s_mf[lane] = mf;
   }
   if (w <= 1) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
@@ -277,7 +272,25 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
 
   // ---- D (wave 0, lane = list * 8 + chain): the left-to-right sums, all chains
   // of all lists at once
-  if (w == 0) __builtin_amdgcn_s_setprio(3);  // the critical path again (see B)
+  if (w <= 1) __builtin_amdgcn_s_setprio(3);  // the critical path again (see B)
+  if (w == 1 && lane < kQppLists) {  // SigmaX, pass 2 (pass 1 in B)
+    const int kl = s_k[lane];
+    const uint64_t fm = s_fmask[lane];
+    const int nf = __popcll(fm);
+    double sigmax = 0.0;
+    if (kl >= 2 && nf >= 2) {
+      const double mf = s_mf[lane];
+      Kahan kfv;
+      kahan_init(kfv);
+#pragma unroll
+      for (int j = 0; j < kQppK; ++j) {
+        const double dv = s_x[lane][j] - mf;
+        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
+      }
+      sigmax = sqrt(kahan_final(kfv) / (double)nf);
+    }
+    s_sigmax[lane] = sigmax;
+  }
   if (w == 0 && (lane & 7) < kChains) {
     const int ll = lane >> 3, c = lane & 7;
     const int kl = s_k[ll];
@@ -291,7 +304,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     }
     s_res[ll][c] = acc;
   }
-  if (w == 0) __builtin_amdgcn_s_setprio(0);
+  if (w <= 1) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   QPP_STAMP(4);
 
