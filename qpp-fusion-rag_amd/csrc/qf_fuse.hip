@@ -1505,6 +1505,14 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
 #ifndef QF_BS_REV
 #define QF_BS_REV 1
 #endif
+// delta = range / 2^QF_BS_DELTA_SHIFT: the float-bit key resolves the scores over
+// about QF_BS_DELTA_SHIFT binades above the minimum
+#ifndef QF_BS_DELTA_SHIFT
+#define QF_BS_DELTA_SHIFT 12
+#endif
+#ifndef QF_BS_RETRY_SHIFT  // the recount's finer delta (a bucket overflowed)
+#define QF_BS_RETRY_SHIFT 20
+#endif
 template <int BLOCK, int BITS>
 struct BsCfg {
   static constexpr int kWaves = BLOCK / 64;
@@ -1630,49 +1638,73 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   }
   const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
   const double rng = smax - smin;
-  const double delta = rng * 0x1p-12;
-  const float ftop = (float)(rng + delta);
-  if (!(isfinite(rng) && isfinite(ftop) && delta > 0.0) || nan) {  // uniform
+  int ush = 0;  // U - 1 >> ush < MINSUB
+  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
+  // A bucket above kJsBucketMax items (documents packed just above the minimum by a
+  // run with a tiny weight) is counted again once with delta 2^8 times finer (~20
+  // binades above the minimum) before the pair is left to the fallback pass: the
+  // finer key alone costs ~7 % on the usual fused distributions, the fallback
+  // pass's LSD sort much more on the few it catches
+  double delta;
+  uint32_t b0;
+  int bsh;
+  uint32_t ws[ROWS], old[ROWS];
+  // count with delta = range / 2^shift; returns -1 for a range the key cannot take
+  // (the pair is marked), else whether some bucket is above kJsBucketMax.  A lambda
+  // called twice, not a loop: the loop kept values live across it (VGPR spills)
+  auto count = [&](const int shift) -> int {
+    delta = ldexp(rng, -shift);
+    const float ftop = (float)(rng + delta);
+    if (!(isfinite(rng) && isfinite(ftop) && delta > 0.0) || nan) return -1;  // uniform
+    b0 = __float_as_uint((float)delta);
+    const uint32_t span = __float_as_uint(ftop) - b0;
+    bsh = span >= (uint32_t)NB ? (32 - __clz((int)span)) - BITS : 0;
+    if ((span >> bsh) >= (uint32_t)MINBASE) ++bsh;
+    // ---- 1. count ------------------------------------------------------------------
+    // every row's atomic issued before any result is used; rows past U add 0 to
+    // bucket 0 (no branches around the atomics, one wait)
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = (wid * rows + j) * 64 + lane;
+      const bool ok = j < rows && u < U;
+      ws[j] = ok ? bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, ush, smin, delta, b0, bsh)
+                 : 0u;
+      old[j] = atomicAdd(&bkw[ws[j] >> 1], ok ? 1u << ((ws[j] & 1u) * 16u) : 0u);
+    }
+    // a bucket above kJsBucketMax items <=> some item arrived at index >= kJsBucketMax
+    bool bigl = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const uint32_t at = (old[j] >> ((ws[j] & 1u) * 16u)) & 0xFFFFu;
+      bigl |= at >= (uint32_t)kJsBucketMax;
+      ws[j] |= at << 16;
+    }
+    {
+      const bool wbig = ballot(bigl) != 0ull;
+      if (lane == 0) s_wmax[wid] = wbig ? 1u : 0u;
+    }
+    QF_STAMP(10);
+    __syncthreads();
+    QF_STAMP(11);
+    bool anybig = false;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) anybig |= s_wmax[w] != 0u;
+    return anybig ? 1 : 0;
+  };
+  int cs = count(QF_BS_DELTA_SHIFT);
+  if (cs == 1) {  // uniform: every wave has read the flags; zero the counters, recount
+    __syncthreads();
+    for (int i = tid * 4; i < NB / 2 + 8; i += BLOCK * 4)
+      *(uint4*)&bkw[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    cs = count(QF_BS_RETRY_SHIFT);
+  }
+  if (cs < 0) {  // uniform
     if (tid == 0) outp[0] = kJsUnsorted;
     return;
   }
-  const uint32_t b0 = __float_as_uint((float)delta);
-  const uint32_t span = __float_as_uint(ftop) - b0;
-  int bsh = span >= (uint32_t)NB ? (32 - __clz((int)span)) - BITS : 0;
-  if ((span >> bsh) >= (uint32_t)MINBASE) ++bsh;
-  int ush = 0;  // U - 1 >> ush < MINSUB
-  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
-  // ---- 1. count ------------------------------------------------------------------
-  // every row's atomic issued before any result is used; rows past U add 0 to
-  // bucket 0 (no branches around the atomics, one wait)
-  uint32_t ws[ROWS], old[ROWS];
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int u = (wid * rows + j) * 64 + lane;
-    const bool ok = j < rows && u < U;
-    ws[j] = ok ? bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, ush, smin, delta, b0, bsh)
-               : 0u;
-    old[j] = atomicAdd(&bkw[ws[j] >> 1], ok ? 1u << ((ws[j] & 1u) * 16u) : 0u);
-  }
-  // a bucket above kJsBucketMax items <=> some item arrived at index >= kJsBucketMax
-  bool bigl = false;
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const uint32_t at = (old[j] >> ((ws[j] & 1u) * 16u)) & 0xFFFFu;
-    bigl |= at >= (uint32_t)kJsBucketMax;
-    ws[j] |= at << 16;
-  }
-  {
-    const bool wbig = ballot(bigl) != 0ull;
-    if (lane == 0) s_wmax[wid] = wbig ? 1u : 0u;
-  }
-  QF_STAMP(10);
-  __syncthreads();
-  QF_STAMP(11);
+  const bool big = cs != 0;
   // ---- 2. exclusive scan of the counters ---------------------------------------------
-  bool big = false;
-#pragma unroll
-  for (int w = 0; w < WAVES; ++w) big |= s_wmax[w] != 0u;
   {
     constexpr int kPer = NB / BLOCK;  // u16 counters per thread
     static_assert(kPer % 8 == 0 || kPer == 4, "uint4 / uint2 counter loads");

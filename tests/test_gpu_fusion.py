@@ -123,7 +123,9 @@ def test_bucket_sort_weight_extremes(gpu):
     Q, R, K = 72, 5, 300
     off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=21)
     rng = np.random.default_rng(21)
-    cases = [[0.0, 0.0, 0.5, 0.3, 0.0], [1e-12, 1.0, 1.0, 1e-12, 1.0],
+    # 1e-6 next to 1: the first count overflows a bucket, the finer recount does not;
+    # 1e-12 next to 1: both overflow, the fallback pass sorts the pair
+    cases = [[0.0, 0.0, 0.5, 0.3, 0.0], [1e-12, 1.0, 1.0, 1e-12, 1.0], [1e-6, 1.0, 0.5, 1e-6, 1.0],
              [-0.5, 0.2, -1.0, 0.0, 0.7], [-0.0] * 5, [1e300, 1e300, 1.0, 1.0, 1.0],
              list(rng.random(5))]
     w_h = np.array([cases[q % len(cases)] for q in range(Q)], np.float64).ravel()
