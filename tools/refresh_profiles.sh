@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-end evidence on one GPU box: GPU tests, smoke, the default bench line, every
+# other BASELINE config's line, the end-to-end drop-in timing and the rocprofv3
+# passes.  Each GPU step has its own time limit; the first failure ends the call.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+O=gpurun_out/refresh
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 300 python -u bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; exit 1; }
+for w in c1 c3 c4 c5; do
+  timeout -k 10 300 python -u bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
+done
+timeout -k 10 300 python -u tools/e2e.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }
+bash tools/profile.sh $O/prof
+echo refresh-done
