@@ -382,12 +382,13 @@ def check_parity(p: Pipeline, nq: int):
             continue
         _, o_uc, o_perm, o_fused = coracle.fuse(h["off"], h["docid"], sc, p.R, name, 60,
                                                 weights=h["w"])
-        f = p.out.fused[m, : nq * p.R * p.K].cpu().numpy()
+        f = p.out.fused[m, : nq * p.R * p.K].cpu().numpy()  # by first-seen index u
         pm = p.out.perm[m, : nq * p.R * p.K].cpu().numpy().view(np.uint16)
         ok &= bool(np.array_equal(uc, o_uc))
         for q in range(nq):
             b, n = h["off"][q * p.R], uc[q]
-            ok &= f[b:b + n].tobytes() == o_fused[b:b + n].tobytes()
+            ranked = f[b + pm[b:b + n].astype(np.int64)]  # rank order, as the oracle's
+            ok &= ranked.tobytes() == o_fused[b:b + n].tobytes()
             ok &= bool(np.array_equal(pm[b:b + n], o_perm[b:b + n]))
     return ok
 

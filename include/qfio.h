@@ -79,8 +79,9 @@ size_t qfio_format_score(double x, char* out);
 /*
  * write_runfile for one fused run (qf_fuse outputs copied to the host):
  * queries order[0..n_out) (indices into qbase / counts / qid strings), for each
- * its counts[q] documents union_docid[qbase[q] + perm[qbase[q] + k]] with rank
- * k + 1 and score fused[qbase[q] + k]; one line "qid Q0 docno rank score tag".
+ * its counts[q] documents u = qbase[q] + perm[qbase[q] + k] with rank k + 1:
+ * docno union_docid[u], score fused[u] (qf_fuse's layout: scores in first-seen
+ * order, perm ranks them); one line "qid Q0 docno rank score tag".
  */
 int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
                    const int32_t* counts, const uint32_t* union_docid, const uint16_t* perm,

@@ -148,7 +148,8 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
  * Multi-method rank fusion of every query: a join kernel (one workgroup per
  * query: LDS hash join over docids, contribution groups in first-seen order,
  * the ordered sums of every requested method) and a sort kernel (one workgroup
- * per (query, method): stable LDS radix sort by fused score, in place).
+ * per (query, method): stable LDS bucket sort by fused score, which writes the
+ * rank order as perm).
  * Queries of 10,241 .. qf_max_entries_per_query() (65,535) entries take a third
  * kernel (the same join in a global workspace + a bitonic sort), launched only
  * when max_entries > 10,240 (or n_retrievers > 16), with a workspace allocated and freed stream-ordered
@@ -168,9 +169,12 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
  *                  (retriever order, then list position), u = 0..U_q-1
  *   union_count[q] = U_q (or a negative QF_QSTATUS_* code)
  *   for the m-th requested method (ascending bit order), at offset m*out_stride:
- *     perm[...]  — u of the i-th fused document (uint16)
- *     fused[...] — its fused score (double), sorted descending; ties keep
- *                  first-seen order (Python's stable sort, src/fusion.py:475,488)
+ *     fused[... + u] — document u's fused score (double), first-seen order
+ *     perm[... + i]  — the u of rank i: scores descending, ties in first-seen
+ *                      order (Python's stable sort, src/fusion.py:475,488)
+ *   so rank i of query q is union_docid[b + perm[b + i]] with score
+ *   fused[b + perm[b + i]], b = list_off[q*R] (+ m*out_stride for perm / fused).
+ *   The scores are written once, by the join; the sort writes only perm.
  */
 int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const uint32_t* docid, const void* score, int32_t score_kind,

@@ -43,7 +43,8 @@ struct EvalRun {
   // equality class of a score: the "%.6f" value write_runfile prints (text
   // runs), else the double itself (-0.0 == +0.0)
   __device__ __forceinline__ long long micro(int64_t base, int i) const {
-    const double s = score[base + i];
+    // qf_fuse output (perm given): its scores are by u, ranked through perm
+    const double s = perm ? score[base + perm[base + i]] : score[base + i];
     return text ? round6(s) : (long long)f64_asc_key(s);
   }
 };

@@ -366,33 +366,19 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
   }
 }
 
-// Sorted items -> perm (u of rank i) and the fused score (read back from
-// fused[u] with its sign, -0.0 included, before the block overwrites fused in
-// place).
+// Sorted items -> perm (u of rank i).  The scores stay where the join left them,
+// by u: the ranked list is fused[perm[i]] (include/qppfuse.h).
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
-                                          const uint32_t (&item)[ITEMS], uint16_t* operm,
-                                          double* io) {
+                                          const uint32_t (&item)[ITEMS], uint16_t* operm) {
   int ro = sx.rows;
   asm volatile("" : "+s"(ro));
-  double v[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int i = (sx.wid * ro + j) * 64 + sx.lane;
-    v[j] = (j < ro && i < sx.U) ? io[item[j] & kUMask] : 0.0;
-  }
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) asm volatile("" ::"v"(v[j]));  // loads done before the barrier
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const int i = (sx.wid * ro + j) * 64 + sx.lane;
-    if (j < ro && i < sx.U) {
-      // final outputs, not re-read by the device: non-temporal, so they do not
-      // evict the unsorted scores other workgroups are about to gather
-      __builtin_nontemporal_store((uint16_t)(item[j] & kUMask), &operm[i]);
-      __builtin_nontemporal_store(v[j], &io[i]);
-    }
+    // final outputs, not re-read by the device: non-temporal, so they do not evict
+    // the unsorted scores other workgroups are about to gather
+    if (j < ro && i < sx.U) __builtin_nontemporal_store((uint16_t)(item[j] & kUMask), &operm[i]);
   }
 }
 
@@ -1048,7 +1034,7 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
   QF_STAMP(0);
   if (hb_full > 0) sort_desc(sx, item, hb - lo, exact, hb_full);  // else all keys equal
   QF_STAMP(1);
-  write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base, io);
+  write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base);
   QF_STAMP(2);
 }
 // Method bit of output slot ms.
@@ -1473,7 +1459,7 @@ __global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
           }
           const uint32_t P = lo + before;
           __builtin_nontemporal_store((uint16_t)ui, &outp[P]);
-          __builtin_nontemporal_store(vi, &outv[P]);
+          __builtin_nontemporal_store(vi, &outv[ui]);  // scores stay by u (perm ranks them)
         }
       }
       QF_STAMP(2);
@@ -1757,13 +1743,11 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
   // Every row's position before any global store: a store in flight would make
   // the next row's loop wait for it.)
   uint32_t P[ROWS], uo[ROWS];
-  double vo[ROWS];
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int i = (wid * rows + j) * 64 + lane;
     P[j] = 0u;
     uo[j] = 0u;
-    vo[j] = 0.0;
     if (j < rows && i < U) {
       const double vi = sval[i];
       const uint32_t ui = su[i];
@@ -1784,7 +1768,6 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
       }
       P[j] = lo + before;
       uo[j] = ui;
-      vo[j] = vi;
     }
   }
   QF_STAMP(2);
@@ -1794,7 +1777,6 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
     const int i = (wid * rows + j) * 64 + lane;
     if (j < rows && i < U) {
       __builtin_nontemporal_store((uint16_t)uo[j], &outp[P[j]]);
-      __builtin_nontemporal_store(vo[j], &io[P[j]]);
     }
   }
   QF_STAMP(15);
@@ -2090,7 +2072,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     for (int i = tid; i < (int)U; i += kXlBlock) {
       const uint32_t u = (uint32_t)(w.stie[i] & 0xFFFFu);
       pm[i] = (uint16_t)u;
-      io[i] = w.sval[u];
     }
     xl_sync();
     QF_STAMP(9);
@@ -2290,7 +2271,7 @@ __global__ __launch_bounds__(256) void topk_kernel(int64_t n_queries, int32_t R,
     double sc = __longlong_as_double(0x7FF8000000000000ll);
     if (i < n) {
       d = union_docid[base + pm[i]];
-      sc = fz[i];
+      sc = fz[pm[i]];  // scores by u, ranked through perm
     }
     out_docid[row * k + i] = d;
     out_score[row * k + i] = sc;

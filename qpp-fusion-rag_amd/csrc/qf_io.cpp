@@ -784,7 +784,8 @@ int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const 
       const char* qs = qid_chars + qid_off[q];
       const size_t ql = (size_t)(qid_off[q + 1] - qid_off[q]);
       for (int32_t k = 0; k < n; ++k) {
-        const uint32_t d = union_docid[base + perm[base + k]];
+        const int64_t u = base + perm[base + k];  // rank k's first-seen index
+        const uint32_t d = union_docid[u];
         const size_t dl = (size_t)(docno_off[d + 1] - docno_off[d]);
         // a line is at most qid + docno + tag + 430 bytes (rank <= 10 digits, score < 400)
         if (cap - used < ql + dl + tl + 430) {
@@ -809,7 +810,7 @@ int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const 
           while (m) *w++ = t[--m];
         }
         *w++ = ' ';
-        w += fmt6(fused[base + k], w);
+        w += fmt6(fused[u], w);
         *w++ = ' ';
         memcpy(w, tag, tl);
         w += tl;

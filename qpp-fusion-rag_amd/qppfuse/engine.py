@@ -53,12 +53,38 @@ def method_names(mask: int):
 
 @dataclass
 class FuseOut:
-    """Device outputs of qf_fuse for one launch shape."""
+    """Device outputs of qf_fuse for one launch shape.  Per query, at its first
+    entry's offset b: union_docid[b + u] and fused[m, b + u] in first-seen order
+    (u < union_count), and perm[m, b + i] = the u of rank i — a ranked list is
+    fused[m, b + perm[m, b + i]] (include/qppfuse.h)."""
     union_docid: torch.Tensor  # int32 view of uint32 [E]
     union_count: torch.Tensor  # int32 [Q]
     perm: torch.Tensor         # int16 view of uint16 [M, E]
     fused: torch.Tensor        # float64 [M, E]
     methods: list
+    list_off: Optional[torch.Tensor] = None  # the last launch's run set (ranked_fused)
+    n_retrievers: int = 0
+
+    def ranked_fused(self) -> torch.Tensor:
+        """[M, E] scores in rank order (rank i of a query at b + i; entries past its
+        union are 0): fused gathered through perm on the device."""
+        R, off = self.n_retrievers, self.list_off
+        Q = (off.numel() - 1) // R
+        E = self.fused.shape[1]
+        qoff = off[::R][:Q + 1].to(torch.int64)
+        n_q = qoff[1:] - qoff[:-1]
+        q_of_e = torch.repeat_interleave(torch.arange(Q, device=off.device), n_q)
+        pos = torch.arange(int(qoff[-1]), device=off.device) - qoff[:-1][q_of_e]
+        ok = pos < self.union_count[:Q].to(torch.int64)[q_of_e]
+        base = qoff[:-1][q_of_e]
+        out = torch.zeros_like(self.fused)
+        n = int(qoff[-1])
+        for m in range(self.fused.shape[0]):
+            u = self.perm[m, :n].to(torch.int64) & 0xFFFF
+            idx = torch.where(ok, base + u, torch.zeros_like(u))
+            out[m, :n] = torch.where(ok, self.fused[m].gather(0, idx),
+                                     torch.zeros((), dtype=torch.float64, device=off.device))
+        return out[:, :E]
 
 
 def alloc_fuse_out(n_queries: int, n_entries: int, mask: int, device) -> FuseOut:
@@ -96,6 +122,7 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
         raise ValueError("max_entries (largest per-query entry count) is required")
     if out is None:
         out = alloc_fuse_out(Q, E, mask, dev)
+    out.list_off, out.n_retrievers = list_off, R
     if mask & _lib.PROBFUSE:
         if seg_prob is None or seg_prob.dtype != torch.float64 or seg_prob.numel() != R * n_segments:
             raise ValueError("probfuse needs seg_prob: float64 [n_retrievers * n_segments]")

@@ -95,7 +95,9 @@ def qid_sort_key(x: str):
 
 
 class FusedRun(Mapping):
-    """{qid: [(docno, score)]} backed by the kernel's packed output arrays."""
+    """{qid: [(docno, score)]} backed by the kernel's packed output arrays: per query
+    (at qbase), the union's docids and fused scores in first-seen order, and perm,
+    the first-seen indices in rank order (include/qppfuse.h)."""
 
     def __init__(self, qids, docnos, qbase, counts, union_docid, perm, fused, order: str,
                  runset: Optional[RunSet] = None):
@@ -124,18 +126,16 @@ class FusedRun(Mapping):
         i = self._index[qid]
         b, n = int(self._qbase[i]), int(self._counts[i])
         p = self._perm[b:b + n].astype(np.int64)
-        return self._udoc[b + p], self._fused[b:b + n]
+        return self._udoc[b + p], self._fused[b + p]
 
     def __getitem__(self, qid) -> List[Tuple[str, float]]:
         i = self._index[qid]
         b, n = int(self._qbase[i]), int(self._counts[i])
-        p = self._perm[b:b + n].astype(np.int64)
-        s = self._fused[b:b + n]
         if self.order == "sorted":
+            p = self._perm[b:b + n].astype(np.int64)
             docs = self._docnos[self._udoc[b + p]]
-            return list(zip(docs.tolist(), s.tolist()))
-        by_u = np.empty(n, dtype=np.float64)
-        by_u[p] = s
+            return list(zip(docs.tolist(), self._fused[b + p].tolist()))
+        by_u = self._fused[b:b + n]
         ids = self._udoc[b:b + n]
         if self.order == "docno":  # ids are interned in docno order
             o = np.argsort(ids, kind="stable")

@@ -135,7 +135,7 @@ def _device_fuse(rs, method: str, weights=None, k: int = 60, seg=None):
 def _ranked(rs, counts, udoc, perm, fused, qi):
     b, n = int(rs.list_off[qi * rs.n_rankers]), int(counts[qi])
     p = perm[b:b + n].astype(np.int64)
-    return rs.docnos[udoc[b + p]], fused[b:b + n]
+    return rs.docnos[udoc[b + p]], fused[b + p]  # scores by u, ranked through perm
 
 
 def build_probfuse_run(runs_test, P_probs, x=25, L=100, run_tag="probFuse") -> pd.DataFrame:

@@ -140,8 +140,8 @@ def test_write_run_matches_python_writer(tmp_path):
     want = []
     for q in order:
         for k in range(counts[q]):
-            d = docnos[ud[qbase[q] + perm[qbase[q] + k]]]
-            want.append(f"{qids[q]} Q0 {d} {k + 1} {fused[qbase[q] + k]:.6f} tag-1\n")
+            u = qbase[q] + perm[qbase[q] + k]  # qf_fuse's layout: scores by u, perm ranks
+            want.append(f"{qids[q]} Q0 {docnos[ud[u]]} {k + 1} {fused[u]:.6f} tag-1\n")
     assert out.read_text() == "".join(want)
 
 

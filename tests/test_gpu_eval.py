@@ -51,7 +51,7 @@ def test_eval_of_fused_outputs_matches_oracle(gpu, text):
                           (t(qo), t(qd.view(np.int32)), t(qr)), int(np.diff(qo).max()),
                           MEASURES, text_scores=text).cpu().numpy()
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     for m in range(len(methods)):
         # the oracle gets plain ranked lists (docid, score) and sorts them itself
         roff = np.zeros(Q + 1, np.int64)

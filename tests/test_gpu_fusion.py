@@ -85,7 +85,7 @@ def test_fuse_all_methods_bit_exact_vs_c_oracle(gpu, shape):
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     uc = out.union_count.cpu().numpy()
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     assert (uc > 0).all()
     for m, name in enumerate(ALL):
         o_ud, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60, weights=w_h)
@@ -106,7 +106,7 @@ def test_fuse_f64_scores_bit_exact(gpu):
     uc = out.union_count.cpu().numpy()
     for m, name in enumerate(["combsum", "combmnz", "rrf"]):
         _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, raw_h, R, name)
-        f = out.fused.cpu().numpy()[m]
+        f = out.ranked_fused().cpu().numpy()[m]
         p = out.perm.cpu().numpy().view(np.uint16)[m]
         for q in range(Q):
             b, n = off_h[q * R], uc[q]
@@ -137,7 +137,7 @@ def test_bucket_sort_weight_extremes(gpu):
     sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uc = out.union_count.cpu().numpy()
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     assert (uc > 0).all()
     for m, name in enumerate(ALL):
         _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60, weights=w_h)
@@ -169,7 +169,7 @@ def test_ranx_minmax_denominator_floor(gpu, max_entries):
     out = engine.fuse(doff, ddoc, dsc, R, ["combsum", "combmnz", "rrf"],
                       max_entries=max_entries)
     uc = int(out.union_count[0])
-    f = out.fused.cpu().numpy()
+    f = out.ranked_fused().cpu().numpy()
     p = out.perm.cpu().numpy().view(np.uint16)
     for m, name in enumerate(["combsum", "combmnz", "rrf"]):
         _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name)
@@ -207,7 +207,7 @@ def test_edge_cases_empty_lists_ties_single(gpu):
         np.testing.assert_array_equal(out.perm.cpu().numpy().view(np.uint16)[m][:off[-1]][
             np.concatenate([np.arange(off[q * R], off[q * R] + uc[q]) for q in range(3)])],
             o_perm[np.concatenate([np.arange(off[q * R], off[q * R] + uc[q]) for q in range(3)])])
-        f = out.fused.cpu().numpy()[m]
+        f = out.ranked_fused().cpu().numpy()[m]
         for q in range(3):
             b, n = off[q * R], uc[q]
             assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
@@ -232,7 +232,7 @@ def test_kernel_capacity_boundaries(gpu, n_entries):
         _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name)
         assert uc[0] == o_uc[0]
         n = uc[0]
-        assert out.fused.cpu().numpy()[m][:n].tobytes() == o_fused[:n].tobytes()
+        assert out.ranked_fused().cpu().numpy()[m][:n].tobytes() == o_fused[:n].tobytes()
         np.testing.assert_array_equal(out.perm.cpu().numpy().view(np.uint16)[m][:n], o_perm[:n])
 
 
@@ -292,7 +292,7 @@ def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
                       max_entries=n)
     assert int(out.union_count[0]) == n
     perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
-    fused = out.fused.cpu().numpy()[0][:n]
+    fused = out.ranked_fused().cpu().numpy()[0][:n]
     want = np.argsort(-s, kind="stable")
     np.testing.assert_array_equal(perm, want)
     # defaultdict(float) accumulation: 0.0 + 1.0 * s, so -0.0 comes out as +0.0
@@ -313,7 +313,7 @@ def test_fused_topk_compaction(gpu, k):
     off_h, uc = off.cpu().numpy(), out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fz = out.fused.cpu().numpy()
+    fz = out.ranked_fused().cpu().numpy()
     for q in range(Q):
         b, n = off_h[q * R], min(k, uc[q])
         for m in range(len(ms)):
@@ -347,7 +347,7 @@ def test_grids_beyond_65536_workgroups(gpu):
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     E = Q * R * K
     qb = np.repeat(off_h[0:-1:R][:Q], R * K)
     valid = (np.arange(E) - qb) < np.repeat(uc, R * K)
@@ -378,7 +378,7 @@ def test_bucket_sort_grid_beyond_65536_workgroups(gpu):
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     qs = np.sort(np.random.default_rng(4).choice(Q, 300, replace=False))
     qs = np.concatenate([[0], qs, [Q - 1]])
     # the sampled queries as their own run set (queries are independent)
@@ -426,7 +426,7 @@ def test_workspace_path_for_very_large_queries(gpu, kind):
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fz = out.fused.cpu().numpy()
+    fz = out.ranked_fused().cpu().numpy()
     for m, name in enumerate(ALL):
         o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
                                                    rank=rank)
@@ -467,7 +467,7 @@ def test_workspace_path_learned_ties_by_docid(gpu, K):
     want = np.lexsort((ud, -unsorted))
     perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
     np.testing.assert_array_equal(perm, want)
-    assert out.fused.cpu().numpy()[0][:n].tobytes() == unsorted[want].tobytes()
+    assert out.ranked_fused().cpu().numpy()[0][:n].tobytes() == unsorted[want].tobytes()
 
 
 @pytest.mark.parametrize("R,K", [(17, 300), (32, 40), (20, 700)])
@@ -494,7 +494,7 @@ def test_more_than_16_runs_take_the_workspace_join(gpu, R, K):
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fz = out.fused.cpu().numpy()
+    fz = out.ranked_fused().cpu().numpy()
     for m, name in enumerate(ALL):
         o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
                                                    rank=rank)
@@ -526,7 +526,7 @@ def test_workspace_join_reports_queries_beyond_max_entries(gpu):
     for q in (0, 2):
         b, n = off[q * R], uc[q]
         assert n == o_uc[q] > 0
-        assert out.fused.cpu().numpy()[0][b:b + n].tobytes() == o_fused[b:b + n].tobytes()
+        assert out.ranked_fused().cpu().numpy()[0][b:b + n].tobytes() == o_fused[b:b + n].tobytes()
 
 
 def test_more_than_32_runs_are_rejected(gpu):
@@ -594,7 +594,7 @@ def test_method_subsets_bit_exact(gpu, methods):
     sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uc = out.union_count.cpu().numpy()
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     slot = {m: i for i, m in enumerate(sorted(methods, key=ALL.index))}
     for name in methods:
         _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60,
@@ -635,7 +635,7 @@ def test_two_runs_on_adversarial_keys(gpu, kind, overlap, n):
                       max_entries=2 * n)
     uc = int(out.union_count[0])
     perm = out.perm.cpu().numpy().view(np.uint16)
-    fused = out.fused.cpu().numpy()
+    fused = out.ranked_fused().cpu().numpy()
     for m, name in enumerate(ms):
         _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, 2, name, 60, weights=w_h)
         assert uc == o_uc[0] == 2 * n - shared
