@@ -19,7 +19,7 @@ off = p.off.cpu().numpy()
 out = {"uc": uc, "off": off, "micro": p.micro.cpu().numpy(),
        "docid": p.docid.cpu().numpy(), "w": p.w.cpu().numpy()}
 for m, name in enumerate(bench.METHODS):
-    out[name] = p.out.fused[m].cpu().numpy()
+    out[name] = p.out.ranked_fused()[m].cpu().numpy()  # rank order
     out[name + "_perm"] = p.out.perm[m].cpu().numpy()
 Path("gpurun_out").mkdir(exist_ok=True)
 np.savez_compressed("gpurun_out/fused_c2.npz", **out)

@@ -19,7 +19,7 @@ torch.cuda.synchronize()
 off_h = off.cpu().numpy(); doc_h = docid.cpu().numpy().view(np.uint32)
 sc = micro.cpu().numpy().astype(np.float64) / 1e6
 uc = out.union_count.cpu().numpy()
-perm = out.perm.cpu().numpy().view(np.uint16); fz = out.fused.cpu().numpy()
+perm = out.perm.cpu().numpy().view(np.uint16); fz = out.ranked_fused().cpu().numpy()
 bad = 0
 for m, name in enumerate(methods):
     _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc, R, name, 60, weights=w.cpu().numpy())

@@ -53,13 +53,14 @@ doc_h = docid.cpu().numpy().view(np.uint32)[: off_h[-1]]
 sc_h = micro.cpu().numpy()[: off_h[-1]].astype(np.float64) / 1e6
 w_h = w.cpu().numpy()[: n * R]
 uc = o.union_count.cpu().numpy()
+rf = o.ranked_fused().cpu().numpy()  # scores in rank order (qf_fuse keeps them by u)
 ok = True
 for m, name in enumerate(ms):
     _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60, weights=w_h)
     for q in range(n):
         b, u = off_h[q * R], o_uc[q]
         ok &= bool(uc[q] == u)
-        ok &= o.fused[m, b:b + u].cpu().numpy().tobytes() == o_fused[b:b + u].tobytes()
+        ok &= rf[m, b:b + u].tobytes() == o_fused[b:b + u].tobytes()
 res["parity_queries"] = n
 res["bit_exact"] = ok
 res["mean_union"] = float(uc.mean())
