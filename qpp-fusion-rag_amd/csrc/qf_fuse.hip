@@ -711,7 +711,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     if (rep) {
       const uint32_t u = (uint32_t)sh.cnt[j * WAVES + wid] + mbcnt(b);
       const uint32_t go = (uint32_t)sh.gof[j * WAVES + wid] + gpre;
-      p.union_docid[base + u] = tkey[dk[j]];
+      // not re-read by the sort kernels: non-temporal (keeps the scores in the MALL)
+      __builtin_nontemporal_store(tkey[dk[j]], &p.union_docid[base + u]);
       tkey[dk[j]] = go | (u << 16);  // slot -> group offset | u (the docid is dead)
     }
   }
