@@ -641,3 +641,41 @@ def test_two_runs_on_adversarial_keys(gpu, kind, overlap, n):
         assert uc == o_uc[0] == 2 * n - shared
         np.testing.assert_array_equal(perm[m][:uc], o_perm[:uc], err_msg=name)
         assert fused[m][:uc].tobytes() == o_fused[:uc].tobytes(), name
+
+
+@pytest.mark.gpu
+def test_one_kernel_join_sort_path(gpu):
+    """join_sort_kernel (QF_JS_BLOCK=512: join, sums and every method's sort in one
+    workgroup per query — the measured-slower alternative kept for A/B) bit-exact vs
+    the oracle; the switch is read once per process, so it runs in a child."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n" % (str(root), str(root / "qpp-fusion-rag_amd")) +
+        "import numpy as np, torch\n"
+        "from qppfuse import engine\n"
+        "from oracle import _loader as coracle\n"
+        "Q, R, K = 48, 5, 1000\n"
+        "off, docid, raw = engine.synth_runs(0, Q, R, K, seed=5)\n"
+        "_, micro = engine.minmax_per_query(raw, off, want_norm=False)\n"
+        "w = torch.rand(Q * R, dtype=torch.float64, device=off.device)\n"
+        "ms = ['combsum', 'combmnz', 'rrf', 'wcombsum', 'wcombmnz', 'wrrf']\n"
+        "out = engine.fuse(off, docid, micro, R, ms, weights=w, max_entries=R * K)\n"
+        "f = out.ranked_fused().cpu().numpy(); p = out.perm.cpu().numpy().view(np.uint16)\n"
+        "uc = out.union_count.cpu().numpy(); o = off.cpu().numpy()\n"
+        "d = docid.cpu().numpy().view(np.uint32); s = micro.cpu().numpy() / 1e6\n"
+        "for m, name in enumerate(ms):\n"
+        "    _, ouc, op, of = coracle.fuse(o, d, s, R, name, 60, weights=w.cpu().numpy())\n"
+        "    assert np.array_equal(uc, ouc)\n"
+        "    for q in range(Q):\n"
+        "        b, n = o[q * R], uc[q]\n"
+        "        assert f[m, b:b + n].tobytes() == of[b:b + n].tobytes(), (name, q)\n"
+        "        assert np.array_equal(p[m, b:b + n], op[b:b + n]), (name, q)\n"
+        "print('js-ok')\n")
+    env = dict(__import__("os").environ, QF_JS_BLOCK="512")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "js-ok" in r.stdout
