@@ -27,6 +27,7 @@ METHOD_BITS = {"combsum": COMBSUM, "combmnz": COMBMNZ, "rrf": RRF,
 SCORE_F64, SCORE_MICRO = 0, 1
 NORM_NONE, NORM_MINMAX, NORM_ZSCORE = 0, 1, 2
 QPP_COLS = 13
+MAX_RUNS = 32  # qf_fuse: retriever masks are 32-bit (include/qppfuse.h)
 EVAL_NDCG, EVAL_RR, EVAL_R, EVAL_P, EVAL_AP = range(5)
 EVAL_MAX_METRICS, EVAL_MAX_QRELS = 16, 256
 

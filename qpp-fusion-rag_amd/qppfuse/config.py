@@ -133,12 +133,14 @@ def _merge(base: Dict[str, Any], over: Dict[str, Any]) -> Dict[str, Any]:
 
 
 def find_config_file() -> Optional[Path]:
+    """QPPFUSE_CONFIG, else <PROJECT_ROOT>/config/defaults.yaml (the reference reads
+    <project_root>/config/defaults.yaml only, src/config.py:100-146) — never a file
+    that merely happens to sit in the working directory."""
     cands = []
     if os.environ.get("QPPFUSE_CONFIG"):
         cands.append(Path(os.environ["QPPFUSE_CONFIG"]))
     if os.environ.get("PROJECT_ROOT"):
         cands.append(Path(os.environ["PROJECT_ROOT"]) / "config" / "defaults.yaml")
-    cands.append(Path.cwd() / "config" / "defaults.yaml")
     for c in cands:
         if c.is_file():
             return c
@@ -155,12 +157,12 @@ class Config(Section):
 
     def load(self, path: Optional[os.PathLike] = None) -> "Config":
         """(Re)load from `path`, else from find_config_file(), else the built-in values."""
-        import yaml
         p = Path(path) if path is not None else find_config_file()
         if p is not None and not p.is_file():
             raise ConfigError(f"Configuration file not found: {p}")
         raw = {}
         if p is not None:
+            import yaml  # only when a file is actually read
             with open(p, "r") as fh:
                 raw = yaml.safe_load(fh) or {}
         raw = expand_env_vars({k: raw[k] for k in _SECTIONS if k in raw})

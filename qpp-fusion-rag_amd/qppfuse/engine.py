@@ -134,6 +134,8 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
     if learned_f32 is not None:
         if mask != _lib.LEARNED:
             raise ValueError("learned_f32 applies to methods == ['learned'] only")
+        if int(learned_f32) >> R:
+            raise ValueError(f"learned_f32 names runs beyond the {R} of the run set")
         _lib.call("qf_fuse_learned_f32", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
                   _ptr(weights), int(learned_f32) & 0xFFFFFFFF, int(max_entries),
                   _ptr(out.union_docid), _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused),

@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import pandas as pd
 
-from . import engine
+from . import _lib, engine
 from .config import ConfigError, config
 from .config import get_qpp_index as _cfg_qpp_index
 from .data_utils import load_qpp_scores as _load_qpp
@@ -152,6 +152,20 @@ class FusedRun(Mapping):
 _PACK_CACHE: Dict[tuple, tuple] = {}  # frames' identity -> (content fingerprint, RunSet)
 
 
+class _Pinned:
+    """A column digest that also holds what it hashed; equal when the digests are."""
+    __slots__ = ("h", "ref")
+
+    def __init__(self, h, ref):
+        self.h, self.ref = h, ref
+
+    def __eq__(self, other):
+        return isinstance(other, _Pinned) and other.h == self.h
+
+    def __hash__(self):
+        return self.h
+
+
 def _column_digest(col):
     """xxh3 of one column's contents: the values of a numeric column, the object
     pointers of an object column (str objects are immutable, so an unchanged
@@ -169,10 +183,14 @@ def _column_digest(col):
     if a.dtype == object:
         if len(a) == 0:
             return 0
+        # pinned: a copy of the column's references keeps every hashed str alive,
+        # so no later value can reuse one of these addresses (A -> B -> C at A's
+        # address would otherwise fingerprint as unchanged)
+        a = a.copy()
         ptrs = (ctypes.c_uint64 * len(a)).from_address(a.ctypes.data)
         h = xxhash.xxh3_64_intdigest(memoryview(ptrs).cast("B"))
         del ptrs
-        return h
+        return _Pinned(h, a)
     return xxhash.xxh3_64_intdigest(memoryview(a).cast("B"))
 
 
@@ -214,12 +232,25 @@ def _derived(rs: RunSet, what: str) -> RunSet:
             d = dedupe_keep_last(rs)
             cache[what] = d if d.canonical else reorder(d, "score")
         elif what == "rows":      # every row, file order (src/fusion.py:272-277)
-            cache[what] = expand_duplicates(rs)
+            cache[what] = _check_runs(rs, expand_duplicates(rs))
         elif what == "rank":      # every row, rank order (src/fusion.py:372)
-            cache[what] = expand_duplicates(rs if rs.canonical else reorder(rs, "rank"))
+            cache[what] = _check_runs(rs, expand_duplicates(rs if rs.canonical
+                                                           else reorder(rs, "rank")))
         else:
             raise ValueError(what)
     return cache[what]
+
+
+def _check_runs(rs: RunSet, rv: RunSet) -> RunSet:
+    """A docno repeated d times inside one list becomes d virtual runs of its
+    ranker: say so when that takes the run set past the kernels' 32 runs."""
+    if rv.n_rankers > _lib.MAX_RUNS:
+        depth = int(np.bincount(rv.base_ranker).max()) if rv.base_ranker is not None else 1
+        raise ValueError(
+            f"{rs.n_rankers} runs with docnos repeated up to {depth} times inside one list "
+            f"expand to {rv.n_rankers} runs (every repeated row is summed as the reference's "
+            f"loops sum it); at most {_lib.MAX_RUNS} are supported")
+    return rv
 
 
 def _expand_weights(weights: Optional[np.ndarray], rs: RunSet, rv: RunSet):

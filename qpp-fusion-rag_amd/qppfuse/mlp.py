@@ -125,6 +125,14 @@ def decode_tensor(t) -> np.ndarray:
     if not (isinstance(st, Opaque) and st.name == "_load_from_bytes"):
         raise NotImplementedError("tensor storage is not an inline byte stream")
     flat = decode_storage(st.args[0])
+    # the geometry comes from the file: check it lies inside the storage before
+    # as_strided (which would read out of bounds on a corrupt or hostile pickle)
+    if len(size) != len(stride):
+        raise ValueError("tensor size / stride rank mismatch")
+    if offset < 0 or offset > len(flat) or any(s < 0 for s in size) or any(s < 0 for s in stride):
+        raise ValueError("tensor offset / size / stride out of range")
+    if all(s > 0 for s in size) and offset + sum((s - 1) * st_ for s, st_ in zip(size, stride)) >= len(flat):
+        raise ValueError("tensor view extends past its storage")
     it = flat.itemsize
     view = np.lib.stride_tricks.as_strided(flat[offset:], shape=size,
                                            strides=tuple(s * it for s in stride))

@@ -152,6 +152,10 @@ def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, Li
     n_cols = arr.shape[1]
     if n_cols > config.qpp.n_methods:  # method_values[i] of the reference (src/qpp.py:347-350)
         raise IndexError("list index out of range")
+    if method == "minmax" and (n_cols < config.qpp.n_methods or not qids):
+        # the reference's minmax takes np.array([]).min() of every column no row
+        # fills (config.qpp.methods shorter than n_methods, src/qpp.py:347-357)
+        raise ValueError("zero-size array to reduction operation minimum which has no identity")
     # the kernels normalise 13 independent columns per row: pad to a multiple
     width = -(-max(n_cols, 1) // _lib.QPP_COLS) * _lib.QPP_COLS
     arr = np.ascontiguousarray(np.pad(arr, ((0, 0), (0, width - n_cols)))

@@ -28,6 +28,11 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden3():
+    return json.loads((GOLDEN / "reference_round3.json").read_text())
+
+
+@pytest.fixture(scope="session")
 def gpu():
     import torch
     if not torch.cuda.is_available():

@@ -435,5 +435,73 @@ def round2(mods):
     print("round-2 fixtures written to", OUT)
 
 
+def round3(mods):
+    """Fixtures added in round 3 (reference_round3.json):
+      write_run   scripts/02_retrieve.py:65-82 on {qid: RetrieverResult} — the
+                  reference's own RetrieverResult and BaseRetriever.normalize_scores
+                  (src/retrievers/base.py:14-21,60-73), and the 12-line loop of
+                  write_run restated here (02_retrieve.py imports faiss at :34, not
+                  installed).  Raw, unrounded scores (BM25-like, dense-like,
+                  negative MonoT5-like), ties, a constant list, an empty list, one
+                  entry; normalize True and False; the bytes written.
+    """
+    base = mods["base"]
+    rng = random.Random(20251214)
+
+    def restated_write_run(results, output_path, retriever_name, normalize=False):
+        os.makedirs(os.path.dirname(output_path), exist_ok=True)
+        with open(output_path, "w") as f:
+            for qid in sorted(results.keys(),
+                              key=lambda x: int(x.replace("test", "")) if x.startswith("test") else x):
+                docs = results[qid].results
+                if normalize:
+                    docs = base.BaseRetriever.normalize_scores(docs)
+                for docno, score, rank in docs:
+                    f.write(f"{qid} Q0 {docno} {rank} {score:.6f} {retriever_name}\n")
+
+    def lists(kind, n_q):
+        out = {}
+        for q in range(n_q):
+            qid = f"test{rng.randrange(0, 5000)}"
+            while qid in out:
+                qid = f"test{rng.randrange(0, 5000)}"
+            k = rng.choice((1, 2, 7, 25, 60))
+            if kind == "bm25":
+                sc = sorted((rng.gammavariate(2.0, 6.0) + 5.0 for _ in range(k)), reverse=True)
+            elif kind == "dense":
+                sc = sorted((0.5 + 0.4 * rng.betavariate(5, 2) for _ in range(k)), reverse=True)
+            elif kind == "monot5":
+                sc = sorted((-rng.expovariate(0.3) for _ in range(k)), reverse=True)
+            else:  # ties and a constant list
+                v = [rng.choice((0.25, 0.5, 1.0 / 3.0)) for _ in range(k)]
+                sc = sorted(v, reverse=True) if q % 2 else [v[0]] * k
+            docs = [(f"doc{rng.randrange(10 ** 6)}", s, i + 1) for i, s in enumerate(sc)]
+            out[qid] = docs
+        out[f"test{5000 + n_q}"] = []  # a query with no documents
+        return out
+
+    cases = []
+    for kind, name in (("bm25", "BM25"), ("dense", "BGE"), ("monot5", "BM25_MonoT5"),
+                       ("ties", "Splade")):
+        raw = lists(kind, 9)
+        for normalize in (True, False):
+            res = {q: base.RetrieverResult(qid=q, results=list(d), retriever_name=name)
+                   for q, d in raw.items()}
+            tmp = Path(tempfile.mkdtemp(prefix="qppfuse_wr_"))
+            path = tmp / "runs" / "nested" / f"{name}{'.norm' if normalize else ''}.res"
+            restated_write_run(res, str(path), name, normalize=normalize)
+            cases.append({"kind": kind, "retriever_name": name, "normalize": normalize,
+                          "results": {q: [[d, hx(s), r] for d, s, r in docs] for q, docs in raw.items()},
+                          "expected": path.read_text()})
+            shutil.rmtree(tmp)
+    (OUT / "reference_round3.json").write_text(json.dumps({"write_run": cases}, indent=1,
+                                                          sort_keys=True))
+    print("round-3 fixtures written to", OUT)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--round3"]:
+        round3(load_reference())
+    else:
+        main()
+        round3(load_reference())

@@ -56,14 +56,29 @@ def test_normalize_scores_matches_reference_golden(gpu, golden):
         assert normalize_scores(src) == want
 
 
+def test_write_run_reference_drop_in(gpu, golden3, tmp_path):
+    """scripts/02_retrieve.py:65-82 as the reference calls it: {qid: RetrieverResult}
+    into a directory that does not exist yet; bytes == the reference's own output
+    (tests/golden/make_golden.py round3: base.py's RetrieverResult + normalize_scores)."""
+    from qppfuse.retrieval import RetrieverResult, write_run
+    for i, case in enumerate(golden3["write_run"]):
+        res = {q: RetrieverResult(qid=q, results=[(d, unhex(s), r) for d, s, r in docs],
+                                  retriever_name=case["retriever_name"])
+               for q, docs in case["results"].items()}
+        p = tmp_path / f"c{i}" / "runs" / "nested" / "X.res"
+        write_run(res, str(p), case["retriever_name"], normalize=case["normalize"])
+        assert p.read_text() == case["expected"], (case["kind"], case["normalize"])
+
+
 def test_write_run_normalized_text(gpu, tmp_path):
-    from qppfuse.retrieval import write_run
+    from qppfuse.retrieval import RetrieverResult, write_run
     rng = np.random.default_rng(2)
     results = {f"test{i}": [(f"d{j}", float(s), j + 1) for j, s in
                             enumerate(sorted(rng.gamma(2, 6, 20), reverse=True))]
                for i in range(12)}
     p = tmp_path / "X.norm.res"
-    write_run(results, str(p), "X", normalize=True)
+    write_run({q: RetrieverResult(q, d, "X") for q, d in results.items()}, str(p), "X",
+              normalize=True)
     from oracle import ref_port
     want = []
     for qid in sorted(results, key=ref_port.qid_sort_key):

@@ -138,3 +138,32 @@ def test_oracle_learned_fusion_vs_reference(case):
     vals = [float(s) for lst in got.values() for _, s in lst]
     f32 = all(float(np.float32(v)) == v for v in vals)
     assert f32 == (not c["extra"])
+
+
+@pytest.mark.parametrize("offset,size,stride", [
+    (0, (3, 4), (4, 1)),      # the whole storage: accepted
+    (0, (3, 5), (4, 1)),      # one element past the end
+    (13, (1,), (1,)),         # offset past the storage
+    (-1, (2,), (1,)),         # negative offset
+    (0, (2, 2), (-1, 1)),     # negative stride
+    (0, (4,), (1, 1)),        # rank mismatch
+    (11, (2,), (1,)),         # starts inside, runs past
+    (0, (0, 99), (99, 1)),    # an empty view: nothing read
+])
+def test_decode_tensor_checks_geometry(monkeypatch, offset, size, stride):
+    """A tampered size / stride / offset in the pickle must not reach as_strided
+    (an out-of-bounds read): ValueError instead."""
+    from qppfuse import mlp
+    from qppfuse.lgbm import Opaque
+    monkeypatch.setattr(mlp, "decode_storage", lambda blob: np.arange(12, dtype=np.float32))
+    t = Opaque("torch._utils", "_rebuild_tensor_v2",
+               (Opaque("torch.storage", "_load_from_bytes", (b"",)), offset, size, stride))
+    ok = (offset, size, stride) in [(0, (3, 4), (4, 1)), (0, (0, 99), (99, 1))]
+    if ok:
+        a = mlp.decode_tensor(t)
+        assert a.shape == size
+        if a.size:
+            assert a.tobytes() == np.arange(12, dtype=np.float32).reshape(3, 4).tobytes()
+    else:
+        with pytest.raises(ValueError):
+            mlp.decode_tensor(t)
