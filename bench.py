@@ -226,7 +226,12 @@ class Pipeline:
             self.run_to_booster = [model.retrievers.index(n) if n in model.retrievers else -1
                                    for n in names]
         self.ev = []
-        self.pending = None  # the previous step's top-k gather (dist.PendingGather)
+        self.pending = None  # the previous step's top-k gather (dist.TopkGather handle)
+        self.gather, self.n_step = None, 0
+        if world > 1 and args.gather_topk > 0:  # every buffer of the gather, made once
+            from qppfuse.dist import TopkGather
+            self.gather = TopkGather(self.shard_sizes, len(self.methods), args.gather_topk, dev,
+                                     dst=0)
         torch.cuda.synchronize()
 
     def step(self, timed=False):
@@ -265,16 +270,17 @@ class Pipeline:
         if timed:
             t1.record()
             self.ev.append((t0, t1))
-        if a.gather_topk > 0:  # the final fused top-k of every shard onto rank 0 (RCCL)
-            from qppfuse.dist import gather_fused_topk
+        if self.gather is not None and a.gather_topk > 0:  # the fused top-k onto rank 0 (RCCL)
             # pipelined: this step's gather runs on the communicator's stream beside
             # the next step's kernels; the previous step's is waited for here, after
-            # this step's kernels are queued (its top-k buffers are its own)
+            # this step's kernels are queued.  Two buffer sets alternate: the top-k
+            # kernel writes this step's rows straight into set n % 2 (no pad, no cat)
             if self.pending is not None:
                 self.gathered = self.pending.wait()
-            d, sc = e.fused_topk(self.out, self.off, self.R, a.gather_topk)
-            self.pending = gather_fused_topk(d, sc, dst=0, sizes=self.shard_sizes,
-                                             async_op=True)
+            e.fused_topk(self.out, self.off, self.R, a.gather_topk,
+                         dest=self.gather.buffers(self.n_step))
+            self.pending = self.gather.start(self.n_step)
+            self.n_step += 1
         self.w = w
 
     def drain(self):
@@ -393,7 +399,7 @@ def check_parity(p: Pipeline, nq: int):
     return ok
 
 
-CPU_SAMPLE_PER_WORKER = {"c1": 1000, "c2": 25, "c3": 60, "c4": 60, "c5": 0}
+CPU_SAMPLE_PER_WORKER = {"c1": 1000, "c2": 25, "c3": 60, "c4": 60, "c5": 25}
 
 
 def _port_frames(h, R, names, q0, qids):
@@ -436,7 +442,20 @@ def _cpu_worker(job):
     t["qpp"] = time.perf_counter() - t0
     for m in methods:
         t1 = time.perf_counter()
-        ref_port.fuse(frames, m, qpp, qpp_index, 60)
+        if m == "learned":  # src/fusion.py:387-448: .qpp round trip, GBDT, weighted groupby-sum
+            from oracle import lgbm_oracle
+            from qppfuse import lgbm
+            model = lgbm.load_fusion_model(ROOT / "tests" / "golden" / "lgbm" /
+                                           "nq_fusion_multioutput.json.gz")
+            norm = {}
+            for name in names:  # per .qpp file: min-max over its queries, "%.6f" text
+                col = ref_port.normalize_qpp({q: qpp[q][name] for q in qids}, "minmax")
+                for q in qids:
+                    norm.setdefault(q, {})[name] = [float(f"{x:.6f}") for x in col[q]]
+            wd = lgbm_oracle.weights_dict(frames, norm, model)
+            ref_port.learned_fusion_from_weights(frames, wd, len(model.retrievers))
+        else:
+            ref_port.fuse(frames, m, qpp, qpp_index, 60)
         t[m] = time.perf_counter() - t1
     rows = int(sum(len(df) for df in frames.values()))
     return nq, time.perf_counter() - t0, t, rows
@@ -484,6 +503,19 @@ def cpu_baseline_native(p: Pipeline, nq: int):
                     np.repeat(h["tf"][:, 1], p.R))
     dt = time.perf_counter() - t0
     return nq / dt
+
+
+def cpu_calibration():
+    """The newest committed tools/calibrate_cpu.py result: reference / port time ratio
+    of weighted_combsum / weighted_rrf, measured side by side on the build host."""
+    files = sorted((ROOT / "profiles").glob("r*_cpu_calibration.json"))
+    if not files:
+        return None
+    d = json.loads(files[-1].read_text())
+    return {"ratio": d["ratio"], "ratio_reference_over_port": d["ratio_reference_over_port"],
+            "reference_us_per_row": d["reference_us_per_row"],
+            "port_us_per_row": d["port_us_per_row"], "host": d["host"],
+            "source": f"profiles/{files[-1].name} (tools/calibrate_cpu.py)"}
 
 
 VALU_PEAK_PER_SIMD_NS = 0.5208  # tools/valu_peak.hip on MI355X (profiles/r01_valu.json)
@@ -622,7 +654,7 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        ported = all(m in METHODS for m in p.methods)
+        ported = all(m in METHODS or m == "learned" for m in p.methods)
         per_worker = (CPU_SAMPLE_PER_WORKER[args.workload] if args.cpu_sample is None
                       else args.cpu_sample)
         if world == 1 and per_worker > 0 and ported:
@@ -638,6 +670,10 @@ def main():
                              f"ranx-equivalent dict loops), {c['workers']} single-threaded "
                              f"processes, {c['wall_s']} s wall",
                    **{k: v for k, v in c.items() if k not in ("value", "workers")}}
+            cal = cpu_calibration()
+            if cal is not None:  # the port vs the reference itself, timed on one host
+                cpu["calibration"] = cal
+                cpu["reference_equivalent_value"] = round(c["value"] / cal["ratio"], 4)
             if args.native_sample > 0:
                 cpu["native_c_oracle_value"] = round(
                     cpu_baseline_native(p, min(args.native_sample, p.Q)), 2)
@@ -678,7 +714,7 @@ def main():
                        for i, m in enumerate(p.methods)},
             "ndcg10_eval_ms": round(eval_ms, 4),
         }
-        if world == 1 and args.ndcg_sample > 0 and ported:
+        if world == 1 and args.ndcg_sample > 0 and all(m in METHODS for m in p.methods):
             nq = min(args.ndcg_sample, p.Q)
             dq, dm = ndcg_delta(p, ndcg_vals, nq)
             result["ndcg10_delta_vs_ref"] = {

@@ -22,7 +22,30 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+
+/* Gson's getAsFloat of the number json.dumps wrote (QPPBridge.java:67-70,
+ * src/qpp.py:130-147): Float.parseFloat(repr(d)) — repr is the shortest decimal
+ * that reads back as d (the correctly rounded %.{p}g for the smallest such p),
+ * and strtof rounds a decimal correctly.  (float)d differs only when d is
+ * exactly halfway between two floats, so the text path runs only there and
+ * outside the float normal range. */
+static double java_float(double d) {
+  uint64_t b;
+  memcpy(&b, &d, 8);
+  const unsigned e = (unsigned)((b >> 52) & 0x7FF);
+  const int normal32 = e >= 1023 - 126 && e <= 1023 + 127;
+  const int midpoint = (b & 0x1FFFFFFFull) == 0x10000000ull;
+  if (!(midpoint || !normal32) || !isfinite(d) || d == 0.0) return (double)(float)d;
+  char buf[64];
+  for (int p = 1; p <= 17; ++p) {
+    snprintf(buf, sizeof buf, "%.*g", p, d);
+    if (strtod(buf, NULL) == d) break;
+  }
+  return (double)strtof(buf, NULL);
+}
 
 typedef struct { double s, c, simple; } kahan_t;
 
@@ -170,7 +193,7 @@ void oracle_qpp_raw(const double* score, const int64_t* list_off, int64_t n_list
     double* o = out + l * 13;
     if (n64 <= 0) { for (int c = 0; c < 13; ++c) o[c] = 0.0; continue; }
     int k = n64 < 50 ? (int)n64 : 50;
-    for (int i = 0; i < k; ++i) r[i] = (double)(float)score[list_off[l] + i];
+    for (int i = 0; i < k; ++i) r[i] = java_float(score[list_off[l] + i]);
     int nt = num_terms_raw[l] > 1 ? num_terms_raw[l] : 1;
     o[0] = computeNQC(r, k);
     o[1] = computeSMV(r, k);

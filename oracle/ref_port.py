@@ -169,8 +169,19 @@ def _jdk_average(vals, default):
 
 
 def _f32(x: float) -> float:
-    import struct
-    return struct.unpack("f", struct.pack("f", x))[0]
+    """Gson's getAsFloat of the JSON number json.dumps wrote (QPPBridge.java:67-70,
+    src/qpp.py:130-147): Float.parseFloat(repr(x)), a correctly rounded
+    decimal -> float conversion — glibc's strtof is one (ISO C / IEEE 754)."""
+    import ctypes
+    global _STRTOF
+    if _STRTOF is None:
+        _STRTOF = ctypes.CDLL(None).strtof
+        _STRTOF.restype = ctypes.c_float
+        _STRTOF.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    return float(_STRTOF(repr(float(x)).encode(), None))
+
+
+_STRTOF = None
 
 
 def java_qpp(num_terms_raw: int, maxidf: float, avgidf: float, scores) -> Dict[str, float]:

@@ -603,6 +603,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     *(uint4*)&tmask2[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   QF_STAMP(3);
+#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 1  // development: phase VALU
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
+    if (acc == 12345u) p.union_count[q] = 0;
+    return -1;
+  }
+#endif
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
   int status = 0;
   uint32_t rj[ITEMS];
@@ -655,6 +664,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     if (st) atomicMin(&sh.status, st);  // read after the barriers that follow
   }
   QF_STAMP(4);
+#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 2  // development: phase VALU
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
+    if (acc == 12345u) p.union_count[q] = 0;
+    return -1;
+  }
+#endif
   // ---- number distinct documents in first-seen order; size their groups ------
   uint32_t repm = 0u;
 #pragma unroll
@@ -703,6 +721,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   }
   __syncthreads();
   QF_STAMP(5);
+#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 3  // development: phase VALU
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
+    if (acc == 12345u) p.union_count[q] = 0;
+    return -1;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const bool rep = (repm >> j) & 1u;
@@ -732,6 +759,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   }
   __syncthreads();  // the hash table is dead; its LDS becomes the groups
   QF_STAMP(6);
+#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 4  // development: phase VALU
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
+    if (acc == 12345u) p.union_count[q] = 0;
+    return -1;
+  }
+#endif
   raw_t* gsc = (raw_t*)(smem + L::kGscOff);
   uint32_t* gpr = (uint32_t*)(smem + L::kGprOff);
   uint16_t* ugo = (uint16_t*)(smem + L::kGoOff);
@@ -747,11 +783,65 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   }
   __syncthreads();
   QF_STAMP(7);
+#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 5  // development: phase VALU
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
+    if (acc == 12345u) p.union_count[q] = 0;
+    return -1;
+  }
+#endif
   return N;
 }
 
 constexpr int kFastSumMethods = QF_COMBSUM | QF_COMBMNZ | QF_RRF | QF_WCOMBSUM | QF_WCOMBMNZ |
                                 QF_WRRF;
+
+// The fast path of store_unsorted_sums: MS = the method set when known at compile
+// time (0: read it from p.methods).
+template <int MS, class C, int KIND, int EXTRA>
+__device__ __forceinline__ void fast_sums(const FuseParams& p, JoinShared<C, KIND, EXTRA>& sh,
+                                          int N, const int (&slot)[kNMethods]) {
+  constexpr int BLOCK = C::kBlock;
+  using L = JoinLds<C, KIND>;
+  using raw_t = typename L::raw_t;
+  const int tid = threadIdx.x;
+  const int64_t base = sh.off[0];
+  const int U = sh.U;
+  const raw_t* gsc = (const raw_t*)(sh.smem + L::kGscOff);
+  const uint32_t* gpr = (const uint32_t*)(sh.smem + L::kGprOff);
+  const uint16_t* ugo = (const uint16_t*)(sh.smem + L::kGoOff);
+  const int methods = MS ? MS : p.methods, rrf_k = p.rrf_k;
+  for (int u = tid; u < U; u += BLOCK) {
+    const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0;
+    for (int k = gs; k < ge; ++k) {
+      const double s = ScoreIn<KIND>::val(gsc[k]);
+      const uint32_t q2 = gpr[k];
+      const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
+      const int n = rrf_k + pos + 1;
+      const double y = (methods & (QF_RRF | QF_WRRF)) ? recip_small(n) : 0.0;
+      const double w = sh.w[r];
+      if (methods & (QF_COMBSUM | QF_COMBMNZ)) a0 += s;  // (s - 0.0) / 1.0 == s
+      if (methods & QF_RRF) a1 += y;
+      if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += w * s;
+      if (methods & QF_WRRF) {  // div_small(w, n) with the same reciprocal
+        const double qt = w * y;
+        a5 += fma(fma(-qt, (double)n, w), y, qt);
+      }
+    }
+    const double cnt = (double)(ge - gs);
+    double* out = p.fused + base + u;
+    const int64_t st = p.out_stride;
+    if (methods & QF_COMBSUM) out[slot[0] * st] = a0;
+    if (methods & QF_COMBMNZ) out[slot[1] * st] = a0 * cnt;
+    if (methods & QF_RRF) out[slot[2] * st] = a1;
+    if (methods & QF_WCOMBSUM) out[slot[3] * st] = a2;
+    if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
+    if (methods & QF_WRRF) out[slot[5] * st] = a5;
+  }
+}
 
 // Every document's fused score for every requested method, from the groups the
 // join left in LDS, stored unsorted at fused[slot][base + u] (the sort kernels
@@ -782,35 +872,18 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
   const bool fast = KIND == 1 && sh.slow == 0 && !p.rank && (methods & ~kFastSumMethods) == 0 &&
                     rrf_k >= 0 && rrf_k + N + 1 <= (1 << 24);
   if (fast) {
-    for (int u = tid; u < U; u += BLOCK) {
-      const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a5 = 0.0;
-      for (int k = gs; k < ge; ++k) {
-        const double s = ScoreIn<KIND>::val(gsc[k]);
-        const uint32_t q2 = gpr[k];
-        const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
-        const int n = rrf_k + pos + 1;
-        const double y = (methods & (QF_RRF | QF_WRRF)) ? recip_small(n) : 0.0;
-        const double w = sh.w[r];
-        if (methods & (QF_COMBSUM | QF_COMBMNZ)) a0 += s;  // (s - 0.0) / 1.0 == s
-        if (methods & QF_RRF) a1 += y;
-        if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2 += w * s;
-        if (methods & QF_WRRF) {  // div_small(w, n) with the same reciprocal
-          const double qt = w * y;
-          a5 += fma(fma(-qt, (double)n, w), y, qt);
-        }
-      }
-      const double cnt = (double)(ge - gs);
-      double* out = p.fused + base + u;
-      const int64_t st = p.out_stride;
-      if (methods & QF_COMBSUM) out[slot[0] * st] = a0;
-      if (methods & QF_COMBMNZ) out[slot[1] * st] = a0 * cnt;
-      if (methods & QF_RRF) out[slot[2] * st] = a1;
-      if (methods & QF_WCOMBSUM) out[slot[3] * st] = a2;
-      if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
-      if (methods & QF_WRRF) out[slot[5] * st] = a5;
+    // the method set as a compile-time constant for the common sets (C2's six,
+    // CombSUM + RRF, W-CombSUM, single methods): a run-time set turns every
+    // accumulation into an add plus two selects (34 -> ~24 instructions per entry)
+    switch (methods) {
+      case kFastSumMethods: fast_sums<kFastSumMethods>(p, sh, N, slot); return;
+      case QF_COMBSUM | QF_RRF: fast_sums<QF_COMBSUM | QF_RRF>(p, sh, N, slot); return;
+      case QF_WCOMBSUM: fast_sums<QF_WCOMBSUM>(p, sh, N, slot); return;
+      case QF_COMBSUM: fast_sums<QF_COMBSUM>(p, sh, N, slot); return;
+      case QF_RRF: fast_sums<QF_RRF>(p, sh, N, slot); return;
+      case QF_WRRF: fast_sums<QF_WRRF>(p, sh, N, slot); return;
+      default: fast_sums<0>(p, sh, N, slot); return;
     }
-    return;
   }
   for (int u = tid; u < U; u += BLOCK) {
     const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
@@ -1784,6 +1857,416 @@ __global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
 }
 
 // ============================================================================
+// bsort_kernel — the bucket sort of bucket_sort_kernel with its instruction count
+// cut (it is VALU-issue-bound: ~128 wave-instructions per 64 items there):
+//  * the key is one f64 add and an integer shift: x = v + c (c = delta - smin,
+//    when smin + c >= delta / 2; else (v - smin) + delta), and the high word of x's
+//    bits (x > 0: its bits ascend with x) shifted right — no f64 -> f32 convert;
+//    every step is monotone, so the bucket is non-increasing in v;
+//  * u32 bucket counters (one atomic add, its return value the arrival index),
+//    overlaid on the scores' LDS, which is free until the scatter;
+//  * the scatter keeps each item's (arrival index, bucket size) and stores them by
+//    position, so the rank phase reads lo / hi instead of recomputing the key and
+//    reading the starts.
+// Same order (score descending, ties in first-seen u order), same protocol
+// (perm[0] = kJsUnsorted for the fallback pass).
+// LDS: region A 24 KB (range partials [0, 8 KB) + counters [8 KB, 24 KB); then the
+// scores by position), region B 6 KB (u by position), region C 8 KB (bucket
+// starts; then (arrival, size) by position).  38.9 KB: 4 workgroups per CU.
+// ============================================================================
+// Raw v_min_f64 / v_max_f64, without fmin / fmax's NaN canonicalisation (three
+// more instructions per call): the callers flag NaNs themselves and discard the
+// range when one is present.
+__device__ __forceinline__ double raw_min_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double raw_max_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// a == s ? if_eq : if_ne as one compare and one v_cndmask (the compiler turns
+// the plain ternary into a branch around the f64 key arithmetic, ~6 more
+// instructions per item; s_nop 1: the VCC-write -> lane-select wait states).
+__device__ __forceinline__ uint32_t sel_if_eq_f64(double a, double s, uint32_t if_eq,
+                                                  uint32_t if_ne) {
+  uint32_t r;
+  asm("v_cmp_eq_f64_e32 vcc, %1, %2\n\ts_nop 1\n\tv_cndmask_b32_e32 %0, %4, %3, vcc"
+      : "=v"(r)
+      : "s"(s), "v"(a), "v"(if_eq), "v"(if_ne)
+      : "vcc");
+  return r;
+}
+
+// delta = range / 2^8: with the multiply-scaled key, 8 binades above the minimum
+// balance the buckets best on the C2 fusions (tools/bsort_sim.py: the rank loop's
+// largest bucket per 64 positions 4.3 -> 3.5 against the shifted 12-binade key)
+#ifndef QF_BSORT_DELTA_SHIFT
+#define QF_BSORT_DELTA_SHIFT 8
+#endif
+// BYDOC: learned fusion's slot, whose ties go in docid (= docno) order — the
+// reference's groupby returns each query's list in docno order before
+// write_runfile sorts it stably (src/fusion.py:441-446, 475-488): the docids are
+// loaded with the scores, the minimum's sub-buckets split by docid, the rank
+// compares docids (a u32 by position: 12 KB more LDS, 3 workgroups per CU).
+// Without BYDOC the learned slot is skipped (its own launch takes it).
+template <int BLOCK, int BITS, bool BYDOC>
+__global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams p) {
+  constexpr int WAVES = BLOCK / 64, ROWS = (kJsUMax + BLOCK - 1) / BLOCK, NB = 1 << BITS;
+  constexpr int MINSUB = NB / 16, MINBASE = NB - MINSUB;
+  static_assert(2 * BLOCK * 8 + 4 * NB <= 8 * kJsUMax, "partials + counters overlay the scores");
+  static_assert(2 * kJsUMax <= 2 * NB, "(arrival, size) by position overlays the starts");
+  // regions A (scores by position) and B (u by position) in one array: the spare
+  // counter cnt[NB] lies at the start of B
+  __shared__ __attribute__((aligned(16))) double sval[kJsUMax + kJsUMax / 4];
+  uint16_t* su = (uint16_t*)(sval + kJsUMax);                          // region B
+  __shared__ __attribute__((aligned(16))) uint16_t bk[NB + 8];       // region C
+  uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                       // [NB + 1] u32
+  __shared__ uint32_t sd[BYDOC ? kJsUMax : 1];  // docid by position (BYDOC)
+  __shared__ uint32_t s_wtot[WAVES], s_big[WAVES];
+  __shared__ double s_mn, s_mx;
+  __shared__ int s_wnan[WAVES], s_nan;
+  __shared__ uint32_t s_dmn, s_dmx;
+  // wid is wave-uniform: readfirstlane puts it (and every row base derived from
+  // it) in SGPRs, so the per-row address arithmetic is scalar
+  const int tid = threadIdx.x, lane = tid & 63,
+            wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // BYDOC: one workgroup per query for the learned slot only
+  const int M = BYDOC ? 1 : __popc(p.methods);
+  const int64_t bid = block_id();
+  const int64_t grp8 = bid >> 3, ngroups = (p.n_queries + 7) / 8;
+  if (grp8 >= ngroups * M) return;  // a 2-D grid's padding workgroups (grid_for)
+  // groups of 8 queries (query q on XCD q % 8, where the join wrote it), in
+  // reverse: the join's last-written scores are the likeliest still cached.
+  // grp8 / M by a scalar multiply-high (M <= 9: exact below 2^20 groups), not the
+  // compiler's VALU division sequence
+  int64_t gq;
+  if (M == 1) {
+    gq = grp8;
+  } else if (grp8 < (1 << 20)) {  // M in [2, 9]: magic = ceil(2^32 / M) fits 32 bits
+    const uint32_t magic = 0xFFFFFFFFu / (uint32_t)M + 1u;
+    gq = (int64_t)__umulhi((uint32_t)grp8, magic);
+  } else {
+    gq = grp8 / M;
+  }
+  const int64_t q = (ngroups - 1 - gq) * 8 + (bid & 7);
+  const int ms = BYDOC ? __popc(p.methods & (QF_LEARNED - 1)) : (int)(grp8 - gq * M);
+  if (!BYDOC && (p.methods & QF_LEARNED) && ms == __popc(p.methods & (QF_LEARNED - 1))) return;
+  if (q >= p.n_queries) return;
+  const int U = p.union_count[q];
+  const int64_t base = p.list_off[q * p.R];
+  if (U < 1 || U > kJsUMax) return;  // error / fuse_large_kernel's
+  double* io = p.fused + (int64_t)ms * p.out_stride + base;
+  uint16_t* outp = p.perm + (int64_t)ms * p.out_stride + base;
+  const int rows = (U + BLOCK - 1) / BLOCK;
+  const int wbase = wid * rows * 64;  // this wave's items: [wbase, wbase + rows * 64)
+  double v[ROWS];
+  uint32_t d[BYDOC ? ROWS : 1];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {  // every row's load in flight before the first use
+    const int u = wbase + j * 64 + lane;
+    v[j] = (j < rows && u < U) ? io[u] : 0.0;
+    if (BYDOC) d[j] = (j < rows && u < U) ? p.union_docid[base + u] : 0u;
+  }
+  {  // zero the counters (region A beyond the partials)
+    uint4* c4 = (uint4*)cnt;
+#pragma unroll
+    for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  {  // score range (NaN flagged): every thread's partials, reduced by wave 0
+    double vmn = INFINITY, vmx = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = wbase + j * 64 + lane;
+      if (j < rows && u < U) {
+        vmn = raw_min_f64(vmn, v[j]);
+        vmx = raw_max_f64(vmx, v[j]);
+        nan |= v[j] != v[j];
+      }
+    }
+    sval[tid] = vmn;
+    sval[BLOCK + tid] = vmx;
+    if (BYDOC) {  // docid range: partials in region B (free until the scatter)
+      uint32_t dmn = ~0u, dmx = 0u;
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = wbase + j * 64 + lane;
+        if (j < rows && u < U) {
+          dmn = min(dmn, d[j]);
+          dmx = max(dmx, d[j]);
+        }
+      }
+      ((uint32_t*)su)[tid] = dmn;
+      ((uint32_t*)su)[BLOCK + tid] = dmx;
+    }
+    const bool anynan = ballot(nan) != 0ull;
+    if (lane == 0) s_wnan[wid] = anynan ? 1 : 0;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    __builtin_amdgcn_s_setprio(3);  // the block waits on this wave
+    double mn = sval[lane], mx = sval[BLOCK + lane];
+#pragma unroll
+    for (int i = 1; i < WAVES; ++i) {
+      mn = raw_min_f64(mn, sval[i * 64 + lane]);
+      mx = raw_max_f64(mx, sval[BLOCK + i * 64 + lane]);
+    }
+    mn = wave_min_f64_dpp(mn);
+    mx = wave_max_f64_dpp(mx);
+    uint32_t dmn = 0u, dmx = 0u;
+    if (BYDOC) {
+      const uint32_t* sp = (const uint32_t*)su;
+      dmn = sp[lane];
+      dmx = sp[BLOCK + lane];
+#pragma unroll
+      for (int i = 1; i < WAVES; ++i) {
+        dmn = min(dmn, sp[i * 64 + lane]);
+        dmx = max(dmx, sp[BLOCK + i * 64 + lane]);
+      }
+      dmn = (uint32_t)wave_min_u64_dpp(dmn);
+      dmx = (uint32_t)wave_max_u64_dpp(dmx);
+    }
+    int anyn = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) anyn |= s_wnan[w];
+    if (lane == 63) {
+      s_mn = mn;
+      s_mx = mx;
+      s_nan = anyn;
+      s_dmn = dmn;
+      s_dmx = dmx;
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __syncthreads();
+  // folded keys: -0.0 == +0.0
+  const uint64_t kmin = ~f64_asc_key(s_mx), kmax = ~f64_asc_key(s_mn);
+  const bool nan = s_nan != 0;
+  if (!BYDOC && kmax == kmin && !nan) {  // every score equal: first-seen order
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = wbase + j * 64 + lane;
+      if (j < rows && u < U) __builtin_nontemporal_store((uint16_t)u, &outp[u]);
+    }
+    return;
+  }
+  const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
+  const double rng = smax - smin;
+#if defined(QF_BS_STOP) && QF_BS_STOP == 1
+  if (smin == 12345.0) outp[0] = 0;
+  return;
+#endif
+  int ush = 0;  // U - 1 >> ush < MINSUB
+  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
+  const uint32_t dmin = BYDOC ? s_dmn : 0u;
+  int dsh = 0;  // BYDOC: (dmax - dmin) >> dsh < MINSUB
+  if (BYDOC)
+    while (((s_dmx - dmin) >> dsh) >= (uint32_t)MINSUB) ++dsh;
+  // the minimum's sub-bucket of row j: MINBASE + (wbase + 64 j + lane) >> ush, with
+  // 64-aligned row bases and ush <= 6 (U <= kJsUMax): a per-lane part + a row part
+  static_assert(((kJsUMax - 1) >> 6) < MINSUB, "ush <= 6");
+  const uint32_t lane_sub = (uint32_t)lane >> ush;
+  uint32_t ws[ROWS];  // bucket | arrival index << 16
+  // count with delta = range / 2^shift: -1 = a range the key cannot take (the
+  // pair is marked), else whether some bucket exceeds kJsBucketMax
+  // one row pass of the count: CF = the v + c form.  Every row's atomic is issued
+  // before any result is used (one wait); a lane past U adds to the spare counter
+  // cnt[NB] (in region B, free until the scatter), so no branch surrounds them
+  auto count_rows = [&](auto cf, double c, double delta, uint32_t b0, uint32_t scale) -> bool {
+    constexpr bool CF = decltype(cf)::value;
+    uint32_t old[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (j < rows) {  // uniform
+        const int u = wbase + j * 64 + lane;
+        const double x = CF ? v[j] + c : (v[j] - smin) + delta;
+        const uint32_t hx = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
+        const uint32_t minb = BYDOC ? (uint32_t)MINBASE + ((d[j] - dmin) >> dsh)
+                                    : (uint32_t)MINBASE + ((uint32_t)(wbase + 64 * j) >> ush) + lane_sub;
+        const uint32_t key = __umulhi(hx - b0, scale);  // < MINBASE, non-decreasing in x
+        uint32_t b = sel_if_eq_f64(v[j], smin, minb, (uint32_t)(MINBASE - 1) - key);
+        b = u < U ? b : (uint32_t)NB;
+        ws[j] = b;
+        old[j] = atomicAdd(&cnt[b], 1u);
+      }
+    }
+    bool bigl = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (j < rows) {
+        bigl |= (old[j] >= (uint32_t)kJsBucketMax) & (ws[j] < (uint32_t)NB);
+        ws[j] |= old[j] << 16;
+      }
+    }
+    return bigl;
+  };
+  // count with delta = range / 2^shift: -1 = a range the key cannot take (the
+  // pair is marked), else whether some bucket exceeds kJsBucketMax
+  auto count = [&](const int shift) -> int {
+    // BYDOC with every score equal: every item is a minimum (by docid); any
+    // positive delta gives the (unused) key a valid range
+    const double delta = (BYDOC && rng == 0.0) ? 1.0 : ldexp(rng, -shift);
+    if (!(isfinite(rng) && delta > 0.0) || nan) return -1;  // uniform
+    const double c = delta - smin;
+    // x = v + c when that keeps x >= delta / 2 > 0 for every v >= smin (monotone
+    // rounding: x(v) >= x(smin)); else the exact-difference form
+    const bool cform = isfinite(c) && (smin + c) >= 0.5 * delta;
+    const double xmin = cform ? smin + c : delta;
+    const double xmax = cform ? smax + c : rng + delta;
+    if (!isfinite(xmax)) return -1;
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)((uint64_t)__double_as_longlong(xmin) >> 32));
+    const uint32_t top = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)((uint64_t)__double_as_longlong(xmax) >> 32));
+    // key = (hx - b0) * scale >> 32 spreads the span over all MINBASE buckets (a
+    // power-of-two shift would use 1/2-1 of them): scale = floor(MINBASE * 2^32 / span),
+    // one below for rounding, so the largest key is MINBASE - 1 at most
+    const uint32_t span = top - b0 + 1u;
+    const uint32_t scale =
+        span <= (uint32_t)MINBASE ? 0xFFFFFFFFu
+                                  : (uint32_t)((double)MINBASE * 4294967296.0 / (double)span) - 1u;
+    const bool bigl = cform ? count_rows(std::true_type{}, c, delta, b0, scale)
+                            : count_rows(std::false_type{}, c, delta, b0, scale);
+    {
+      const bool wbig = ballot(bigl) != 0ull;
+      if (lane == 0) s_big[wid] = wbig ? 1u : 0u;
+    }
+    __syncthreads();
+    bool anybig = false;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) anybig |= s_big[w] != 0u;
+    return anybig ? 1 : 0;
+  };
+  int cs = count(QF_BSORT_DELTA_SHIFT);
+  if (cs == 1) {  // uniform: every wave has read the flags; zero the counters, recount
+    __syncthreads();
+    uint4* c4 = (uint4*)cnt;
+    for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    cs = count(QF_BS_RETRY_SHIFT);
+  }
+  if (cs != 0) {  // uniform: a range the key cannot take, or a bucket still too big
+    if (tid == 0) outp[0] = kJsUnsorted;
+    return;
+  }
+#if defined(QF_BS_STOP) && QF_BS_STOP == 2
+  if (ws[0] == 12345u) outp[0] = 0;
+  return;
+#endif
+  // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
+  {
+    constexpr int kPer = NB / BLOCK;  // counters per thread
+    static_assert(kPer == 8, "two uint4 counter loads per thread");
+    const uint4 c0 = ((const uint4*)cnt)[tid * 2], c1 = ((const uint4*)cnt)[tid * 2 + 1];
+    uint32_t c[kPer] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    uint32_t tot = 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t x = c[i];
+      c[i] = tot;
+      tot += x;
+    }
+    const uint32_t incl = wave_incl_scan_dpp(tot);
+    if (lane == 63) s_wtot[wid] = incl;
+    __syncthreads();  // also: every counter read before the scatter overwrites them
+    uint32_t pre = incl - tot;
+#pragma unroll
+    for (int w = 0; w < WAVES - 1; ++w) pre += w < wid ? s_wtot[w] : 0u;
+    ((uint4*)bk)[tid] = make_uint4((pre + c[0]) | ((pre + c[1]) << 16),
+                                   (pre + c[2]) | ((pre + c[3]) << 16),
+                                   (pre + c[4]) | ((pre + c[5]) << 16),
+                                   (pre + c[6]) | ((pre + c[7]) << 16));
+    if (tid == 0) bk[NB] = (uint16_t)U;
+  }
+  __syncthreads();
+#if defined(QF_BS_STOP) && QF_BS_STOP == 3
+  if (bk[tid] == 12345u) outp[0] = 0;
+  return;
+#endif
+  // ---- scatter: value and u by position; (arrival, bucket size) kept ---------------
+  uint32_t pa[ROWS];  // position | (arrival | size << 8) << 16
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = wbase + j * 64 + lane;
+    if (j < rows && u < U) {
+      const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
+      const uint32_t st = bk[b], nx = bk[b + 1];
+      const uint32_t pos = st + at;
+      sval[pos] = v[j];
+      su[pos] = (uint16_t)u;
+      if (BYDOC) sd[pos] = d[j];
+      pa[j] = pos | ((at | ((nx - st) << 8)) << 16);
+    }
+  }
+  __syncthreads();  // the starts are dead: (arrival, size) by position over them
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = wbase + j * 64 + lane;
+    if (j < rows && u < U) bk[pa[j] & 0xFFFFu] = (uint16_t)(pa[j] >> 16);
+  }
+  __syncthreads();
+#if defined(QF_BS_STOP) && QF_BS_STOP == 4
+  if (bk[tid] == 12345u) outp[0] = 0;
+  return;
+#endif
+  // ---- rank inside the bucket, in position order --------------------------------------
+  uint32_t P[ROWS], uo[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = wbase + j * 64 + lane;
+    P[j] = 0u;
+    uo[j] = 0u;
+    if (j < rows && i < U) {
+      const double vi = sval[i];
+      const uint32_t ui = su[i], s = bk[i];
+      // the tie-break key: u (first-seen order) or, BYDOC, the docid
+      const uint32_t ti = BYDOC ? sd[i] : ui;
+      const uint32_t lo = (uint32_t)i - (s & 0xFFu), hi = lo + (s >> 8);
+      uint32_t before = 0u;
+      // the bucket's members by pointer (two per step; a bucket of one: nothing to
+      // count): no index arithmetic inside the loop
+      const uint32_t k0 = hi - lo > 1u ? lo : hi;
+      const double* pv = sval + k0;
+      const double* const pend = sval + hi;
+      const double* const plast = pend - 1;  // a pair remains while pv < plast
+      const auto* pt = (BYDOC ? (const void*)(sd + k0) : (const void*)(su + k0));
+      using tkey_t = typename std::conditional<BYDOC, uint32_t, uint16_t>::type;
+      const tkey_t* tp = (const tkey_t*)pt;
+      for (; pv < plast; pv += 2, tp += 2) {
+        const double v0 = pv[0], v1 = pv[1];
+        const uint32_t t0 = tp[0], t1 = tp[1];
+        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (t0 < ti))) +
+                  (uint32_t)((v1 > vi) | ((v1 == vi) & (t1 < ti)));
+      }
+      if (pv < pend) {
+        const double v0 = pv[0];
+        const uint32_t t0 = tp[0];
+        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (t0 < ti)));
+      }
+      P[j] = lo + before;
+      uo[j] = ui;
+    }
+  }
+  // ---- outputs (every row's position before any store) ----------------------------------
+#if defined(QF_BS_STOP) && QF_BS_STOP == 5
+  uint32_t acc = 0u;
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) acc += P[j] ^ uo[j];
+  if (acc == 12345u) outp[0] = 0;
+  return;
+#endif
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = wbase + j * 64 + lane;
+    if (j < rows && i < U) __builtin_nontemporal_store((uint16_t)uo[j], &outp[P[j]]);
+  }
+}
+
+// ============================================================================
 // join_sort_xl_kernel — queries beyond the LDS join (JoinXL::kNMax < N <= 65,535,
 // e.g. 16 runs x top-4000): the same algorithm with its tables in a global
 // workspace, one 1,024-thread workgroup per query.
@@ -2179,7 +2662,7 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
 static int js_block() {
   static const int b = [] {
     const char* e = std::getenv("QF_JS_BLOCK");
-    return e ? std::atoi(e) : 12;
+    return e ? std::atoi(e) : 14;
   }();
   return b;
 }
@@ -2188,15 +2671,22 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
   void* ws = nullptr;
   hipError_t e = hipSuccess;
   const int jsb = js_block();
-  if ((jsb == 11 || jsb == 12 || jsb == 13) && p.R <= kRMax && max_entries <= JoinXL::kNMax &&
-      max_entries > JoinS::kNMax && !(p.methods & QF_LEARNED)) {
+  if (((jsb == 11 || jsb == 12 || jsb == 13) && !(p.methods & QF_LEARNED) || jsb == 14) &&
+      p.R <= kRMax && max_entries <= JoinXL::kNMax && max_entries > JoinS::kNMax) {
     // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
     if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
     else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
     else launch_join<JoinXL>(p, kind, st);
     const int M = __builtin_popcount((unsigned)p.methods);
     const dim3 g = grid_for((p.n_queries + 7) / 8 * 8 * M);
-    if (jsb == 11) hipLaunchKernelGGL((bucket_sort_kernel<512, 11>), g, dim3(512), 0, st, p);
+    if (jsb == 14) {
+      if (p.methods & ~QF_LEARNED)
+        hipLaunchKernelGGL((bsort_kernel<512, 12, false>), g, dim3(512), 0, st, p);
+      if (p.methods & QF_LEARNED)
+        hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),
+                           dim3(512), 0, st, p);
+    }
+    else if (jsb == 11) hipLaunchKernelGGL((bucket_sort_kernel<512, 11>), g, dim3(512), 0, st, p);
     else if (jsb == 12) hipLaunchKernelGGL((bucket_sort_kernel<512, 12>), g, dim3(512), 0, st, p);
     else hipLaunchKernelGGL((bucket_sort_kernel<512, 13>), g, dim3(512), 0, st, p);
     // unions above kJsUMax and the pairs the bucket sort marked: one pass

@@ -11,10 +11,10 @@
 //   weight of run r = pred[q][model index of r], or 1/n_retrievers for a run the
 //   model does not know (src/fusion.py:440)
 //
-// gbdt_predict_kernel — one thread per (row, booster): walks that booster's
-//   first best_iteration trees (LightGBM NumericalDecision; see qppfuse/lgbm.py)
-//   and adds the leaf values in tree order from 0.0, as GBDT::PredictRaw does.
-//   The model (≈4.5 k nodes for the reference's NQ model) stays in L1/L2.
+// gbdt_predict_kernel — one wave per row: the lanes walk the model's trees
+//   (LightGBM NumericalDecision; see qppfuse/lgbm.py), then each booster's leaf
+//   values are added in tree order from 0.0, as GBDT::PredictRaw does.  The
+//   model (≈4.5 k nodes for the reference's NQ model) stays in L1/L2.
 // learned_weights_kernel — one thread per query: numpy's clip (NaN kept, -0.0
 //   becomes +0.0 — measured on numpy 2.2), numpy's row sum (0.0 + pairwise_sum: sequential below 8
 //   values, 8 accumulators from 8), the zero guard and the division.
@@ -37,37 +37,70 @@
 
 namespace qf {
 
-__global__ __launch_bounds__(256) void gbdt_predict_kernel(GbdtParams p) {
-  const int64_t idx = block_id() * blockDim.x + threadIdx.x;
-  if (idx >= p.n_rows * p.n_boosters) return;
-  const int64_t row = idx / p.n_boosters;
-  const int b = (int)(idx % p.n_boosters);
-  const double* x = p.X + row * p.n_features;
+// One wave per row: the lanes walk the model's trees in parallel (tree c0 + lane
+// of each 64-tree chunk, the row's features staged in LDS), then lane b adds
+// booster b's leaf values of the chunk in tree order onto its running sum — the
+// serial GBDT::PredictRaw sum from 0.0, tree by tree, bit for bit.  (Was: one
+// thread per (row, booster) walking its ~30 trees serially — C5: 17,260 threads,
+// ~270 waves on 256 CUs, each a chain of ~30 tree walks of dependent loads.)
+constexpr int kGbdtWaves = 4;
+constexpr int kGbdtMaxFeatures = 256;  // staged in LDS; more features: read from X
+
+__device__ __forceinline__ double gbdt_walk(const GbdtParams& p, const double* x, int t) {
   const double kZero = (double)1e-35f;  // LightGBM kZeroThreshold (a float)
-  double s = 0.0;
-  for (int t = p.tree_off[b]; t < p.tree_off[b + 1]; ++t) {
-    const int nb = p.node_off[t], lb = p.leaf_off[t];
-    int leaf = 0;
-    if (p.leaf_off[t + 1] - lb > 1) {
-      int node = 0;
-      while (node >= 0) {
-        const int k = nb + node;
-        double fv = x[p.feature[k]];
-        const int dt = p.dtype[k];
-        const int missing = (dt >> 2) & 3;  // 0 none, 1 zero, 2 NaN
-        if (isnan(fv) && missing != 2) fv = 0.0;
-        bool left;
-        if ((missing == 1 && fv >= -kZero && fv <= kZero) || (missing == 2 && isnan(fv)))
-          left = (dt & 2) != 0;  // default side
-        else
-          left = fv <= p.threshold[k];
-        node = left ? p.left[k] : p.right[k];
-      }
-      leaf = ~node;
+  const int nb = p.node_off[t], lb = p.leaf_off[t];
+  int leaf = 0;
+  if (p.leaf_off[t + 1] - lb > 1) {
+    int node = 0;
+    while (node >= 0) {
+      const int k = nb + node;
+      double fv = x[p.feature[k]];
+      const int dt = p.dtype[k];
+      const int missing = (dt >> 2) & 3;  // 0 none, 1 zero, 2 NaN
+      if (isnan(fv) && missing != 2) fv = 0.0;
+      bool left;
+      if ((missing == 1 && fv >= -kZero && fv <= kZero) || (missing == 2 && isnan(fv)))
+        left = (dt & 2) != 0;  // default side
+      else
+        left = fv <= p.threshold[k];
+      node = left ? p.left[k] : p.right[k];
     }
-    s += p.leaf_value[lb + leaf];
+    leaf = ~node;
   }
-  p.out[idx] = s;
+  return p.leaf_value[lb + leaf];
+}
+
+__global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParams p) {
+  __shared__ double sx[kGbdtWaves][kGbdtMaxFeatures];
+  __shared__ double sleaf[kGbdtWaves][64];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = block_id() * kGbdtWaves + wid;
+  if (row >= p.n_rows) return;  // whole waves: no block barrier below
+  const double* xg = p.X + row * p.n_features;
+  const bool staged = p.n_features <= kGbdtMaxFeatures;
+  if (staged)
+    for (int i = lane; i < p.n_features; i += 64) sx[wid][i] = xg[i];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const double* x = staged ? sx[wid] : xg;
+  const int T = p.tree_off[p.n_boosters];
+  // lane b < n_boosters: booster b's trees [tb, te) and its running sum
+  const int b = lane < p.n_boosters ? lane : 0;
+  const int tb = p.tree_off[b], te = p.tree_off[b + 1];
+  double s = 0.0;
+  for (int c0 = 0; c0 < T; c0 += 64) {
+    const int t = c0 + lane;
+    if (t < T) sleaf[wid][lane] = gbdt_walk(p, x, t);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane < p.n_boosters) {
+      const int lo = tb > c0 ? tb : c0, hi = te < c0 + 64 ? te : c0 + 64;
+      for (int i = lo; i < hi; ++i) s += sleaf[wid][i - c0];
+    }
+    __builtin_amdgcn_wave_barrier();  // every sum read before the next chunk's writes
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (lane < p.n_boosters) p.out[row * p.n_boosters + lane] = s;
 }
 
 // numpy's pairwise_sum for n < 128 (numpy/_core/src/umath/loops_utils.h.src)
@@ -183,9 +216,9 @@ hipError_t mlp_weights_launch(const MlpParams& p, hipStream_t st) {
 }
 
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st) {
-  const int64_t n = p.n_rows * p.n_boosters;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(gbdt_predict_kernel, grid_for((n + 255) / 256), dim3(256), 0, st, p);
+  if (p.n_rows * p.n_boosters == 0) return hipSuccess;
+  hipLaunchKernelGGL(gbdt_predict_kernel, grid_for((p.n_rows + kGbdtWaves - 1) / kGbdtWaves),
+                     dim3(64 * kGbdtWaves), 0, st, p);
   return hipGetLastError();
 }
 

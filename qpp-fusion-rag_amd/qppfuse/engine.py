@@ -172,15 +172,24 @@ def qpp_raw(score: torch.Tensor, list_off: torch.Tensor, n_retrievers: int, top_
     return out
 
 
-def fused_topk(out: FuseOut, list_off: torch.Tensor, n_retrievers: int, k: int):
+def fused_topk(out: FuseOut, list_off: torch.Tensor, n_retrievers: int, k: int, dest=None):
     """qf_fused_topk: (docid int32 view of uint32 [Q, M, k], score float64 [Q, M, k]);
-    rows shorter than k padded with docid 0xFFFFFFFF (-1) and NaN."""
+    rows shorter than k padded with docid 0xFFFFFFFF (-1) and NaN.  `dest`: a
+    preallocated contiguous (docid, score) pair of that shape (dist.TopkGather's
+    send buffers) to write into instead of new tensors."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
     M = out.fused.shape[0]
-    docid = torch.empty((Q, M, k), dtype=torch.int32, device=dev)
-    score = torch.empty((Q, M, k), dtype=torch.float64, device=dev)
+    if dest is not None:
+        docid, score = dest
+        if (tuple(docid.shape) != (Q, M, k) or tuple(score.shape) != (Q, M, k)
+                or docid.dtype != torch.int32 or score.dtype != torch.float64
+                or not (docid.is_contiguous() and score.is_contiguous())):
+            raise ValueError(f"dest must be contiguous int32 / float64 [{Q}, {M}, {k}]")
+    else:
+        docid = torch.empty((Q, M, k), dtype=torch.int32, device=dev)
+        score = torch.empty((Q, M, k), dtype=torch.float64, device=dev)
     _lib.call("qf_fused_topk", Q, R, _ptr(list_off), _ptr(out.union_count), _ptr(out.union_docid),
               _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], M, int(k), _ptr(docid),
               _ptr(score), _stream())

@@ -42,6 +42,53 @@ class QPPResult:
     error: Optional[str] = None
 
 
+def _round_f32_exact(q) -> float:
+    """The float32 nearest the rational q (ties to even), as a Python float."""
+    from fractions import Fraction
+    if q == 0:
+        return 0.0
+    neg = q < 0
+    a = -q if neg else q
+    # a = m * 2^e with m in [2^23, 2^24): e from the bit lengths, then round m
+    e = a.numerator.bit_length() - a.denominator.bit_length()
+    if Fraction(2) ** e > a:
+        e -= 1
+    e = max(e - 23, -149)  # float32 subnormals: a fixed exponent of 2^-149
+    m = a / Fraction(2) ** e
+    fl = m.numerator // m.denominator
+    rem = m - fl
+    if rem > Fraction(1, 2) or (rem == Fraction(1, 2) and fl % 2 == 1):
+        fl += 1
+    v = float(fl) * 2.0 ** e
+    if v > float(np.finfo(np.float32).max):
+        v = float("inf")
+    return -v if neg else v
+
+
+def java_floats(x: np.ndarray) -> np.ndarray:
+    """What QPPBridge.java holds for each double the reference sends it: Python's
+    json.dumps writes repr(v) (the shortest decimal that round-trips), Gson's
+    getAsFloat is Float.parseFloat of that text (QPPBridge.java:67-70, src/qpp.py:
+    130-147) — one correct rounding of the DECIMAL.  The kernel rounds the double
+    (RN-even); the two differ only when the double lies exactly halfway between two
+    floats and its shortest decimal is not that midpoint, so those values (and any
+    outside the float normal range) are replaced here by the float Java reads, held
+    as a double (which the kernel then converts exactly)."""
+    from fractions import Fraction
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    bits = x.view(np.uint64)
+    exp = (bits >> np.uint64(52)) & np.uint64(0x7FF)
+    normal32 = (exp >= np.uint64(1023 - 126)) & (exp <= np.uint64(1023 + 127))
+    midpoint = (bits & np.uint64(0x1FFFFFFF)) == np.uint64(0x10000000)
+    fix = np.nonzero((midpoint | ~normal32) & np.isfinite(x) & (x != 0.0))[0]
+    if fix.size == 0:
+        return x
+    out = x.copy()
+    for i in fix:
+        out[i] = _round_f32_exact(Fraction(repr(float(x[i]))))
+    return out
+
+
 def _device_qpp(lists: List[List[float]], texts: List[str], top_k: int = 0) -> np.ndarray:
     """Raw predictors [L, 13] for L score lists (each used in the given order)."""
     import torch
@@ -50,6 +97,7 @@ def _device_qpp(lists: List[List[float]], texts: List[str], top_k: int = 0) -> n
     off = np.zeros(len(lists) + 1, dtype=np.int64)
     np.cumsum(lens, out=off[1:])
     flat = np.fromiter((float(x) for s in lists for x in s), dtype=np.float64, count=int(off[-1]))
+    flat = java_floats(flat)  # Gson's float of the JSON decimal (QPPBridge.java:67-70)
     nt, tf = textfeat.feature_arrays(texts)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     raw = engine.qpp_raw(t(flat) if flat.size else torch.zeros(1, dtype=torch.float64, device=dev),

@@ -135,3 +135,59 @@ def test_gather_fused_topk_concatenates_shards_in_rank_order(async_op):
                            for r, n in enumerate(sizes)])
     np.testing.assert_array_equal(d, want)
     assert s.tobytes() == (want.astype(np.float64) / 7).tobytes()
+
+
+def _topk_gather_worker(rank, world, port, sizes, M, k, steps, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qppfuse.dist import TopkGather
+    g = TopkGather(sizes, M, k, "cpu", dst=0)
+    n = sizes[rank]
+    ptrs = {(t.data_ptr(), u.data_ptr()) for t, u in (g.buffers(i) for i in range(2))}
+    pending, got = None, []
+    for step in range(steps):  # bench.py's pipelined loop: wait for the previous, then start
+        if pending is not None:
+            got.append(_copy(pending.wait()))
+        d, s = g.buffers(step)
+        assert d.shape == (n, M, k) and (d.data_ptr(), s.data_ptr()) in ptrs  # no new buffers
+        d.copy_(torch.arange(n * M * k, dtype=torch.int32).reshape(n, M, k) + 100000 * rank
+                + 10 * step)
+        s.copy_(d.to(torch.float64) / 3)
+        pending = g.start(step)
+    got.append(_copy(pending.wait()))
+    out[rank] = got
+    dist.destroy_process_group()
+
+
+def _copy(res):
+    if res is None:
+        return None
+    per, flat = res
+    return ([(d.numpy().copy(), s.numpy().copy()) for d, s in per],
+            None if flat is None else flat[0].numpy().copy())
+
+
+@pytest.mark.parametrize("world,total", [(4, 11157), (2, 10)])
+def test_topk_gather_preallocated_unequal_shards(world, total):
+    """dist.TopkGather (bench.py's allocation-free N > 1 gather) with C4's unequal
+    shard_range(11157, 4, r) shards (2790, 2789, 2789, 2789) on gloo, world 4:
+    three pipelined steps through the two buffer sets; rank 0 holds every rank's
+    rows, in rank order, trimmed to each shard (a flat view only when equal)."""
+    from qppfuse.dist import shard_range
+    sizes = [e - b for b, e in (shard_range(total, world, r) for r in range(world))]
+    M, k, steps = 2, 3, 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_topk_gather_worker, args=(world, _free_port(), sizes, M, k, steps, out),
+             nprocs=world, join=True)
+    for r in range(1, world):
+        assert out[r] == [None] * steps
+    for step, (per, flat) in enumerate(out[0]):
+        assert (flat is None) == (len(set(sizes)) > 1)
+        for r, (d, s) in enumerate(per):
+            want = np.arange(sizes[r] * M * k, dtype=np.int32).reshape(sizes[r], M, k) \
+                + 100000 * r + 10 * step
+            np.testing.assert_array_equal(d, want)
+            assert s.tobytes() == (want.astype(np.float64) / 3).tobytes()
+        if flat is not None:
+            np.testing.assert_array_equal(flat, np.concatenate([d for d, _ in per]))
