@@ -77,6 +77,19 @@ struct ScoreIn<1> {
 
 // ---- block-level helpers ------------------------------------------------------
 
+// The value of lane + 1 (DPP wave_shl:1, one VALU per dword; lane 63 gets its own
+// old value — callers treat lane 63 separately).
+__device__ __forceinline__ int32_t shl1_lane(int32_t v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double shl1_lane(double v) {
+  const int64_t b = __double_as_longlong(v);
+  const int32_t lo = __builtin_amdgcn_update_dpp((int32_t)b, (int32_t)b, 0x130, 0xf, 0xf, false);
+  const int32_t hi = __builtin_amdgcn_update_dpp((int32_t)(b >> 32), (int32_t)(b >> 32), 0x130,
+                                                 0xf, 0xf, false);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
 // MIN / MAX of a 64-bit key over the block (s_min / s_max pre-initialised; a
 // barrier must separate this call from reading the result).
 __device__ __forceinline__ void block_min_max(uint64_t kmn, uint64_t kmx,
@@ -523,6 +536,7 @@ struct JoinShared {
   static constexpr int kBytes = L::kBytes > EXTRA ? L::kBytes : EXTRA;
   __attribute__((aligned(16))) unsigned char smem[kBytes];
   int64_t off[kRMax + 1];
+  int offr[kRMax + 1];  // off - off[0]: the join's 32-bit list boundaries
   double w[kRMax], mn[kRMax], den[kRMax], rden[kRMax];
   int cnt[C::kItems * C::kWaves], gof[C::kItems * C::kWaves];
   // lane 0's score of every (row, wave): lane 63's successor for the sort check
@@ -549,7 +563,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   auto mask_of = [&](uint32_t slot) -> uint32_t {
     return (tmask2[slot >> 1] >> ((slot & 1u) * 16u)) & 0xFFFFu;
   };
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63,
+            wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR
   QF_STAMP_INIT();
   const int R = p.R;
   if (tid <= R) sh.off[tid] = p.list_off[q * R + tid];
@@ -565,6 +580,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     return -1;
   }
   const int N = (int)N64;
+  if (tid <= R) sh.offr[tid] = (int)(sh.off[tid] - base);  // read after the next barrier
   uint32_t dk[ITEMS];
   raw_t sc[ITEMS];
 #pragma unroll
@@ -621,13 +637,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
-    const raw_t nxt = __shfl_down(sc[j], 1, 64);  // entry e + 1, but at lane 63
+    // entry e + 1 (lane 63: garbage, checked below from LDS): DPP wave_shl:1
+    const raw_t nxt = shl1_lane(sc[j]);
     rj[j] = 0u;
     if (lane == 0 && e < N) sh.first[j * WAVES + wid] = sc[j];
     if (e < N) {
       const uint32_t d = dk[j];
       if (d == kEmpty) status = QF_QSTATUS_BADDOC;
-      while (base + e >= sh.off[r + 1]) ++r;
+      int end = sh.offr[r + 1];  // 32-bit boundaries relative to the query's base
+      while (e >= end) end = sh.offr[++r + 1];
       rj[j] = (uint32_t)r;
       uint32_t h = (d * 0x9E3779B1u) >> (32 - C::kTB);
       while (true) {
@@ -641,7 +659,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       dk[j] = h;  // keep the slot
       // preconditions of the ranx methods / W-RRF (checked once, here)
       const int64_t g = base + e;
-      if (g + 1 < sh.off[r + 1]) {
+      if (e + 1 < end) {
         if (ranx) {
           // raw compare: m / 1e6 is strictly increasing in the micro-units m.
           // Lane 63's successor is lane 0 of the next wave: compared after the
@@ -798,11 +816,26 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
 constexpr int kFastSumMethods = QF_COMBSUM | QF_COMBMNZ | QF_RRF | QF_WCOMBSUM | QF_WCOMBMNZ |
                                 QF_WRRF;
 
+// 1 / (60 + pos + 1) for every position of a list the LDS join holds: RRF's
+// and W-RRF's reciprocal at the reference's k = 60 (config rrf_k) by one cached
+// load instead of a reciprocal estimate and two Newton steps inside the
+// divergent per-document loop.  Compile-time IEEE divisions (correctly
+// rounded, == recip_small bit for bit); 80 KB, its first 8 KB hot in L1.
+constexpr int kRecipK = 60, kRecipN = 10240;
+struct RecipTable {
+  double v[kRecipN];
+  constexpr RecipTable() : v() {
+    for (int i = 0; i < kRecipN; ++i) v[i] = 1.0 / (double)(kRecipK + i + 1);
+  }
+};
+__device__ constexpr RecipTable kRecip60{};
+
 // The fast path of store_unsorted_sums: MS = the method set when known at compile
-// time (0: read it from p.methods).
-template <int MS, class C, int KIND, int EXTRA>
+// time (0: read it from p.methods); TAB: rrf_k == 60, reciprocals from kRecip60.
+template <int MS, bool TAB, class C, int KIND, int EXTRA>
 __device__ __forceinline__ void fast_sums(const FuseParams& p, JoinShared<C, KIND, EXTRA>& sh,
                                           int N, const int (&slot)[kNMethods]) {
+  static_assert(C::kNMax <= kRecipN, "positions beyond the table");
   constexpr int BLOCK = C::kBlock;
   using L = JoinLds<C, KIND>;
   using raw_t = typename L::raw_t;
@@ -821,7 +854,8 @@ __device__ __forceinline__ void fast_sums(const FuseParams& p, JoinShared<C, KIN
       const uint32_t q2 = gpr[k];
       const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
       const int n = rrf_k + pos + 1;
-      const double y = (methods & (QF_RRF | QF_WRRF)) ? recip_small(n) : 0.0;
+      const double y = (methods & (QF_RRF | QF_WRRF))
+                           ? (TAB ? kRecip60.v[pos] : recip_small(n)) : 0.0;
       const double w = sh.w[r];
       if (methods & (QF_COMBSUM | QF_COMBMNZ)) a0 += s;  // (s - 0.0) / 1.0 == s
       if (methods & QF_RRF) a1 += y;
@@ -875,14 +909,21 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
     // the method set as a compile-time constant for the common sets (C2's six,
     // CombSUM + RRF, W-CombSUM, single methods): a run-time set turns every
     // accumulation into an add plus two selects (34 -> ~24 instructions per entry)
+    const bool tab = rrf_k == kRecipK;
     switch (methods) {
-      case kFastSumMethods: fast_sums<kFastSumMethods>(p, sh, N, slot); return;
-      case QF_COMBSUM | QF_RRF: fast_sums<QF_COMBSUM | QF_RRF>(p, sh, N, slot); return;
-      case QF_WCOMBSUM: fast_sums<QF_WCOMBSUM>(p, sh, N, slot); return;
-      case QF_COMBSUM: fast_sums<QF_COMBSUM>(p, sh, N, slot); return;
-      case QF_RRF: fast_sums<QF_RRF>(p, sh, N, slot); return;
-      case QF_WRRF: fast_sums<QF_WRRF>(p, sh, N, slot); return;
-      default: fast_sums<0>(p, sh, N, slot); return;
+      case kFastSumMethods:
+        if (tab) fast_sums<kFastSumMethods, true>(p, sh, N, slot);
+        else fast_sums<kFastSumMethods, false>(p, sh, N, slot);
+        return;
+      case QF_COMBSUM | QF_RRF:
+        if (tab) fast_sums<QF_COMBSUM | QF_RRF, true>(p, sh, N, slot);
+        else fast_sums<QF_COMBSUM | QF_RRF, false>(p, sh, N, slot);
+        return;
+      case QF_WCOMBSUM: fast_sums<QF_WCOMBSUM, false>(p, sh, N, slot); return;
+      case QF_COMBSUM: fast_sums<QF_COMBSUM, false>(p, sh, N, slot); return;
+      case QF_RRF: fast_sums<QF_RRF, false>(p, sh, N, slot); return;
+      case QF_WRRF: fast_sums<QF_WRRF, false>(p, sh, N, slot); return;
+      default: fast_sums<0, false>(p, sh, N, slot); return;
     }
   }
   for (int u = tid; u < U; u += BLOCK) {
@@ -1901,6 +1942,48 @@ __device__ __forceinline__ uint32_t sel_if_eq_f64(double a, double s, uint32_t i
   return r;
 }
 
+// bsort_kernel's bucket-key constants for delta = range / 2^shift (every value
+// uniform over the workgroup): x = v + c (cform) or (v - smin) + delta, bucket key
+// (hi32(x) - b0) * scale >> 32.  ok = 0: a range the key cannot take.
+__device__ __forceinline__ double rfl_f64(double v) {  // a wave-uniform double in SGPRs
+  const int64_t b = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
+}
+struct BsKey {
+  double c, delta;
+  uint32_t b0, scale;
+  int cform, ok;
+};
+template <int MINBASE, bool BYDOC>
+__device__ __forceinline__ BsKey bs_key_params(double smin, double smax, bool nan, int shift) {
+  BsKey k{};
+  const double rng = smax - smin;
+  // BYDOC with every score equal: every item is a minimum (by docid); any
+  // positive delta gives the (unused) key a valid range
+  k.delta = (BYDOC && rng == 0.0) ? 1.0 : ldexp(rng, -shift);
+  if (!(isfinite(rng) && k.delta > 0.0) || nan) return k;
+  k.c = k.delta - smin;
+  // x = v + c when that keeps x >= delta / 2 > 0 for every v >= smin (monotone
+  // rounding: x(v) >= x(smin)); else the exact-difference form
+  k.cform = isfinite(k.c) && (smin + k.c) >= 0.5 * k.delta;
+  const double xmin = k.cform ? smin + k.c : k.delta;
+  const double xmax = k.cform ? smax + k.c : rng + k.delta;
+  if (!isfinite(xmax)) return k;
+  k.b0 = (uint32_t)((uint64_t)__double_as_longlong(xmin) >> 32);
+  const uint32_t top = (uint32_t)((uint64_t)__double_as_longlong(xmax) >> 32);
+  // key = (hx - b0) * scale >> 32 spreads the span over all MINBASE buckets (a
+  // power-of-two shift would use 1/2-1 of them): scale = floor(MINBASE * 2^32 /
+  // span), one below for rounding, so the largest key is MINBASE - 1 at most
+  const uint32_t span = top - k.b0 + 1u;
+  k.scale = span <= (uint32_t)MINBASE
+                ? 0xFFFFFFFFu
+                : (uint32_t)((double)MINBASE * 4294967296.0 / (double)span) - 1u;
+  k.ok = 1;
+  return k;
+}
+
 // delta = range / 2^8: with the multiply-scaled key, 8 binades above the minimum
 // balance the buckets best on the C2 fusions (tools/bsort_sim.py: the rank loop's
 // largest bucket per 64 positions 4.3 -> 3.5 against the shifted 12-binade key)
@@ -1930,6 +2013,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   __shared__ double s_mn, s_mx;
   __shared__ int s_wnan[WAVES], s_nan;
   __shared__ uint32_t s_dmn, s_dmx;
+  __shared__ BsKey s_key;  // wave 0's key constants for the first count
   // wid is wave-uniform: readfirstlane puts it (and every row base derived from
   // it) in SGPRs, so the per-row address arithmetic is scalar
   const int tid = threadIdx.x, lane = tid & 63,
@@ -2034,19 +2118,21 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) anyn |= s_wnan[w];
     if (lane == 63) {
-      s_mn = mn;
-      s_mx = mx;
+      // the folded extremes (-0.0 == +0.0) and the first count's key constants,
+      // once here instead of in every wave after the barrier
+      const double fmx = f64_from_asc_key(f64_asc_key(mx)), fmn = f64_from_asc_key(f64_asc_key(mn));
+      s_mn = fmn;
+      s_mx = fmx;
       s_nan = anyn;
       s_dmn = dmn;
       s_dmx = dmx;
+      s_key = bs_key_params<MINBASE, BYDOC>(fmn, fmx, anyn != 0, QF_BSORT_DELTA_SHIFT);
     }
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
-  // folded keys: -0.0 == +0.0
-  const uint64_t kmin = ~f64_asc_key(s_mx), kmax = ~f64_asc_key(s_mn);
   const bool nan = s_nan != 0;
-  if (!BYDOC && kmax == kmin && !nan) {  // every score equal: first-seen order
+  if (!BYDOC && s_mn == s_mx && !nan) {  // every score equal: first-seen order
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
       const int u = wbase + j * 64 + lane;
@@ -2054,8 +2140,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     }
     return;
   }
-  const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
-  const double rng = smax - smin;
+  const double smax = s_mx, smin = s_mn;
 #if defined(QF_BS_STOP) && QF_BS_STOP == 1
   if (smin == 12345.0) outp[0] = 0;
   return;
@@ -2106,29 +2191,12 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   };
   // count with delta = range / 2^shift: -1 = a range the key cannot take (the
   // pair is marked), else whether some bucket exceeds kJsBucketMax
-  auto count = [&](const int shift) -> int {
-    // BYDOC with every score equal: every item is a minimum (by docid); any
-    // positive delta gives the (unused) key a valid range
-    const double delta = (BYDOC && rng == 0.0) ? 1.0 : ldexp(rng, -shift);
-    if (!(isfinite(rng) && delta > 0.0) || nan) return -1;  // uniform
-    const double c = delta - smin;
-    // x = v + c when that keeps x >= delta / 2 > 0 for every v >= smin (monotone
-    // rounding: x(v) >= x(smin)); else the exact-difference form
-    const bool cform = isfinite(c) && (smin + c) >= 0.5 * delta;
-    const double xmin = cform ? smin + c : delta;
-    const double xmax = cform ? smax + c : rng + delta;
-    if (!isfinite(xmax)) return -1;
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)((uint64_t)__double_as_longlong(xmin) >> 32));
-    const uint32_t top = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)((uint64_t)__double_as_longlong(xmax) >> 32));
-    // key = (hx - b0) * scale >> 32 spreads the span over all MINBASE buckets (a
-    // power-of-two shift would use 1/2-1 of them): scale = floor(MINBASE * 2^32 / span),
-    // one below for rounding, so the largest key is MINBASE - 1 at most
-    const uint32_t span = top - b0 + 1u;
-    const uint32_t scale =
-        span <= (uint32_t)MINBASE ? 0xFFFFFFFFu
-                                  : (uint32_t)((double)MINBASE * 4294967296.0 / (double)span) - 1u;
+  auto count = [&](const BsKey& kp) -> int {
+    if (!kp.ok) return -1;  // uniform
+    const double c = rfl_f64(kp.c), delta = kp.delta;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(kp.b0);
+    const uint32_t scale = __builtin_amdgcn_readfirstlane(kp.scale);
+    const bool cform = kp.cform != 0;
     const bool bigl = cform ? count_rows(std::true_type{}, c, delta, b0, scale)
                             : count_rows(std::false_type{}, c, delta, b0, scale);
     {
@@ -2141,13 +2209,13 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     for (int w = 0; w < WAVES; ++w) anybig |= s_big[w] != 0u;
     return anybig ? 1 : 0;
   };
-  int cs = count(QF_BSORT_DELTA_SHIFT);
+  int cs = count(s_key);
   if (cs == 1) {  // uniform: every wave has read the flags; zero the counters, recount
     __syncthreads();
     uint4* c4 = (uint4*)cnt;
     for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    cs = count(QF_BS_RETRY_SHIFT);
+    cs = count(bs_key_params<MINBASE, BYDOC>(smin, smax, nan, QF_BS_RETRY_SHIFT));
   }
   if (cs != 0) {  // uniform: a range the key cannot take, or a bucket still too big
     if (tid == 0) outp[0] = kJsUnsorted;
