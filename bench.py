@@ -221,8 +221,8 @@ class Pipeline:
             self.packed = lgbm.pack_model(model)
             names = NAMES[:R]
             # X columns: model.retrievers order, 13 QPP values each (src/fusion.py:421-427)
-            self.xperm = torch.tensor([names.index(r) for r in model.retrievers],
-                                      dtype=torch.int64, device=dev)
+            self.block_runs = [names.index(r) if r in names else -1 for r in model.retrievers]
+            self.X = torch.empty((Q, 13 * len(model.retrievers)), dtype=torch.float64, device=dev)
             self.run_to_booster = [model.retrievers.index(n) if n in model.retrievers else -1
                                    for n in names]
         self.ev = []
@@ -259,8 +259,7 @@ class Pipeline:
                                 want_micro=learned, want_weights=not learned)
             w = o["weights"]
             if learned:  # the .qpp values as features, GBDT, normalised weights
-                X = (o["micro"].view(self.Q, self.R, 13).index_select(1, self.xperm)
-                     .reshape(self.Q, -1).to(torch.float64) / 1e6)
+                X = e.qpp_features(o["micro"], self.Q, self.R, self.block_runs, out=self.X)
                 w = e.learned_weights(e.gbdt_predict(X, self.packed), self.run_to_booster)
         if timed:
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

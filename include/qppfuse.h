@@ -145,6 +145,17 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
                      double* w_out, void* stream);
 
 /*
+ * Learned fusion's feature matrix on device: X[q, j*13 + c] = the "%.6f" value
+ * of normalised predictor c of run run_of_block[j] (micro_out of
+ * qf_qpp_normalize, / 1e6 exactly as the .qpp text reads back), i.e. the
+ * X[Q, 13 * n_model_retrievers] learned_fusion builds from qpp_data
+ * (src/fusion.py:415-427; src/data_utils.py:262-293).  run_of_block: host array
+ * of n_blocks (<= 32) run indices, -1 = a retriever the batch lacks (zeros).
+ */
+int qf_qpp_features(const int64_t* micro, int64_t n_queries, int32_t n_retrievers,
+                    const int32_t* run_of_block, int32_t n_blocks, double* X, void* stream);
+
+/*
  * Multi-method rank fusion of every query: a join kernel (one workgroup per
  * query: LDS hash join over docids, contribution groups in first-seen order,
  * the ordered sums of every requested method) and a sort kernel (one workgroup

@@ -95,6 +95,25 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
                "qf_qpp_normalize");
 }
 
+int qf_qpp_features(const int64_t* micro, int64_t n_queries, int32_t n_retrievers,
+                    const int32_t* run_of_block, int32_t n_blocks, double* X, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || n_blocks <= 0 || n_blocks > qf::kMaxFeatureBlocks ||
+      !run_of_block || (n_queries > 0 && (!micro || !X)))
+    return fail(QF_EINVAL, "qf_qpp_features: bad arguments (n_blocks must be in [1, %d])",
+                qf::kMaxFeatureBlocks);
+  qf::QppBlocks blk{};
+  blk.n = n_blocks;
+  for (int j = 0; j < n_blocks; ++j) {
+    if (run_of_block[j] < -1 || run_of_block[j] >= n_retrievers)
+      return fail(QF_EINVAL, "qf_qpp_features: run_of_block[%d] = %d out of range", j,
+                  run_of_block[j]);
+    blk.run[j] = run_of_block[j];
+  }
+  return check(qf::qpp_features_launch(micro, n_queries, n_retrievers, blk, X,
+                                       (hipStream_t)stream),
+               "qf_qpp_features");
+}
+
 static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
                        const uint32_t* docid, const void* score, int32_t score_kind,
                        const int32_t* rank, const double* weights, int32_t methods,

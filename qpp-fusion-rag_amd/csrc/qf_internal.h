@@ -129,6 +129,13 @@ hipError_t qpp_colminmax_launch(const double* raw, const int64_t* list_off, int6
                                 double* mm, hipStream_t st);
 hipError_t qpp_colmeanstd_launch(const double* raw, const int64_t* list_off, int64_t Q,
                                  int32_t R, double* st, hipStream_t stm);
+constexpr int kMaxFeatureBlocks = 32;  // model retrievers of a learned-fusion feature matrix
+struct QppBlocks {
+  int32_t n;
+  int32_t run[kMaxFeatureBlocks];
+};
+hipError_t qpp_features_launch(const int64_t* micro, int64_t Q, int32_t R, const QppBlocks& blk,
+                               double* X, hipStream_t st);
 hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64_t* list_off,
                                 int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
                                 double* norm_out, int64_t* micro_out, double* w_out,

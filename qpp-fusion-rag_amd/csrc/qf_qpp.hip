@@ -624,6 +624,38 @@ hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64
   return hipGetLastError();
 }
 
+// Learned fusion's feature matrix from the normalised predictors' "%.6f" values:
+// X[q, j*13 + c] = micro[(q*R + run_of_block[j])*13 + c] / 1e6 — the .qpp text
+// read back (src/data_utils.py:262-293) and laid out per model retriever
+// (src/fusion.py:421-427); a block whose run is -1 (a retriever the batch lacks)
+// stays 0.0.  One thread per feature, coalesced writes.
+__global__ __launch_bounds__(256) void qpp_features_kernel(const int64_t* __restrict__ micro,
+                                                           int64_t Q, int32_t R, QppBlocks blk,
+                                                           double* __restrict__ X) {
+  const int64_t i = block_id() * blockDim.x + threadIdx.x;
+  const int64_t F = (int64_t)blk.n * kQppCols;
+  if (i >= Q * F) return;
+  const int64_t q = i / F;
+  const int f = (int)(i - q * F);
+  const int j = f / kQppCols, c = f - j * kQppCols;
+  const int r = blk.run[j];
+  double v = 0.0;
+  if (r >= 0) {
+    const int64_t m = micro[(q * R + r) * kQppCols + c];
+    v = (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m) : (double)m / 1e6;
+  }
+  X[i] = v;
+}
+
+hipError_t qpp_features_launch(const int64_t* micro, int64_t Q, int32_t R, const QppBlocks& blk,
+                               double* X, hipStream_t st) {
+  const int64_t n = Q * blk.n * kQppCols;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(qpp_features_kernel, grid_for((n + 255) / 256), dim3(256), 0, st, micro, Q,
+                     R, blk, X);
+  return hipGetLastError();
+}
+
 }  // namespace qf
 
 #ifdef QF_STAMPS

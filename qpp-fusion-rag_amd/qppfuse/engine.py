@@ -11,6 +11,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -237,6 +238,22 @@ def qpp_normalize(raw: torch.Tensor, mm: Optional[torch.Tensor], list_off: torch
     _lib.call("qf_qpp_normalize", _ptr(raw), _ptr(mm), _ptr(list_off), Q, R, mode_id,
               int(qpp_index), _ptr(norm), _ptr(micro), _ptr(w), _stream())
     return {"norm": norm, "micro": micro, "weights": w}
+
+
+def qpp_features(micro: torch.Tensor, n_queries: int, n_retrievers: int, run_of_block,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qf_qpp_features: learned fusion's X [Q, 13 * len(run_of_block)] float64 from the
+    normalised predictors' micro-units (qpp_normalize(..., want_micro=True))."""
+    dev = require_device()
+    blocks = np.ascontiguousarray(run_of_block, dtype=np.int32)
+    Q, R = int(n_queries), int(n_retrievers)
+    if micro.dtype != torch.int64 or micro.numel() != Q * R * _lib.QPP_COLS:
+        raise ValueError(f"micro must be int64 [{Q * R}, {_lib.QPP_COLS}]")
+    if out is None:
+        out = torch.empty((Q, len(blocks) * _lib.QPP_COLS), dtype=torch.float64, device=dev)
+    _lib.call("qf_qpp_features", _ptr(micro), Q, R, blocks.ctypes.data, len(blocks), _ptr(out),
+              _stream())
+    return out
 
 
 def synth_runs(q_begin: int, n_queries: int, n_retrievers: int, k: int, seed: int = 20251212,

@@ -18,7 +18,7 @@ def test_header_declares_expected_entry_points():
     for name in ["qf_fuse", "qf_minmax_per_query", "qf_qpp_raw", "qf_qpp_colminmax",
                  "qf_qpp_normalize", "qf_last_error", "qf_version", "qf_max_entries_per_query",
                  "qf_synth_runs", "qf_eval", "qf_gbdt_predict", "qf_learned_weights",
-                 "qf_qpp_colmeanstd", "qf_fuse_probfuse"]:
+                 "qf_qpp_colmeanstd", "qf_fuse_probfuse", "qf_qpp_features"]:
         assert name in fns
 
 

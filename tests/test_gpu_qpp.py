@@ -207,3 +207,27 @@ def test_normalize_qpp_api_zscore(gpu):
         assert np.array(got[q]).tobytes() == np.array(want[q], np.float64).tobytes()
     # the reference takes every method other than "minmax" as zscore (src/qpp.py:357-359)
     assert _normalize_qpp(res, "other") == got
+
+
+def test_qpp_features_equal_the_qpp_text_round_trip(gpu):
+    """qf_qpp_features: learned fusion's X from the normalised predictors' "%.6f"
+    micro-units, per model retriever (src/fusion.py:421-427): float("%.6f" text)
+    of each value, blocks in the model's order, a retriever the batch lacks = 0.0."""
+    import torch
+    from qppfuse import engine
+    rng = np.random.default_rng(4)
+    Q, R = 37, 4
+    micro = torch.from_numpy(rng.integers(-2_000_000, 2_000_000, (Q * R, 13))).to(gpu)
+    micro[5, 3] = 0
+    micro[6, 0] = 1_000_000
+    blocks = [2, -1, 0, 3, 1]
+    X = engine.qpp_features(micro, Q, R, blocks).cpu().numpy()
+    m = micro.cpu().numpy()
+    want = np.zeros((Q, 13 * len(blocks)))
+    for q in range(Q):
+        for j, r in enumerate(blocks):
+            if r >= 0:
+                want[q, j * 13:(j + 1) * 13] = [float(f"{int(v) / 1e6:.6f}") for v in m[q * R + r]]
+    assert X.tobytes() == want.tobytes()
+    with pytest.raises(ValueError):
+        engine.qpp_features(micro, Q, R, [0, 7])

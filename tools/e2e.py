@@ -48,18 +48,28 @@ def ascii_table(prefix: bytes, ids: np.ndarray):
     return off, out.tobytes()
 
 
-def generate(d: Path, Q: int, R: int, K: int):
-    from qppfuse import engine, fastio
-    off, docid, raw = engine.synth_runs(0, Q, R, K)
-    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
-    nt = torch.full((Q,), 4, dtype=torch.int32, device=off.device)
-    tf = torch.rand((Q, 2), dtype=torch.float64, device=off.device)
-    qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
-    mm = engine.qpp_colminmax(qraw, off, R)
-    qmicro = engine.qpp_normalize(qraw, mm, off, R, "minmax", 5)["micro"].cpu().numpy()
-    off_h = off.cpu().numpy()
-    doc_h = docid.cpu().numpy().view(np.uint32)
-    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+def generate(d: Path, Q: int, R: int, K: int, cpu: bool = False):
+    from qppfuse import fastio
+    if cpu:  # no GPU (loader work in the build container): numpy restatement + C oracle
+        sys.path.insert(0, str(ROOT / "tools"))
+        from synth_np import synth
+        from oracle import _loader as coracle
+        off_h, doc_h, raw = synth(0, Q, R, K)
+        norm = coracle.minmax_per_query(raw, off_h)
+        sc_h = np.round(norm * 1e6) / 1e6
+        qmicro = np.random.default_rng(1).integers(0, 10**6, (Q * R, 13))
+    else:
+        from qppfuse import engine
+        off, docid, raw = engine.synth_runs(0, Q, R, K)
+        _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+        nt = torch.full((Q,), 4, dtype=torch.int32, device=off.device)
+        tf = torch.rand((Q, 2), dtype=torch.float64, device=off.device)
+        qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
+        mm = engine.qpp_colminmax(qraw, off, R)
+        qmicro = engine.qpp_normalize(qraw, mm, off, R, "minmax", 5)["micro"].cpu().numpy()
+        off_h = off.cpu().numpy()
+        doc_h = docid.cpu().numpy().view(np.uint32)
+        sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uniq, inv = np.unique(doc_h, return_inverse=True)
     rs = SimpleNamespace(qids=None, docnos=None)
     rs._strtab = {"qid": ascii_table(b"test", np.arange(Q)), "docno": ascii_table(b"doc", uniq)}
@@ -85,11 +95,23 @@ def main():
     ap.add_argument("--queries", type=int, default=3452)
     ap.add_argument("--dir", default=None)
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--load-only", action="store_true",
+                    help="CPU only: generate with numpy, time load_runs (QFIO_TIMING=1 for phases)")
     a = ap.parse_args()
     from qppfuse import fusion
-    torch.cuda.set_device(0)
     d = Path(a.dir or tempfile.mkdtemp(prefix="qf_e2e_"))
     d.mkdir(parents=True, exist_ok=True)
+    if a.load_only:
+        if not any(d.glob("*.norm.res")):
+            generate(d, a.queries, 5, 1000, cpu=True)
+        for _ in range(a.repeat):
+            t0 = time.perf_counter()
+            runs = fusion.load_runs(str(d))
+            print(json.dumps({"load_runs_s": round(time.perf_counter() - t0, 4),
+                              "rows": int(sum(len(df) for df in runs.values()))}), flush=True)
+            del runs
+        return
+    torch.cuda.set_device(0)
     t0 = time.perf_counter()
     E = generate(d, a.queries, 5, 1000)
     gen_s = time.perf_counter() - t0
