@@ -908,6 +908,19 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
   // list already [0, 1] (x = s), every weight in the division-free range, ranks =
   // positions, k + N + 1 <= 2^24 — CombSUM / CombMNZ / RRF / W-* only.  1 / (k +
   // rank) is computed once per entry for RRF and W-RRF (div_small's reciprocal).
+  if (methods == QF_LEARNED) {  // learned fusion alone (C5): its Kahan sums, nothing else
+    for (int u = tid; u < U; u += BLOCK) {
+      const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
+      double a6 = 0.0, c6 = 0.0;
+      for (int k = gs; k < ge; ++k) {
+        const double s = ScoreIn<KIND>::val(gsc[k]);
+        const int r = (int)(gpr[k] >> 16);
+        learned_add(p, s, sh.w[r], r, a6, c6);  // src/fusion.py:436-446
+      }
+      p.fused[base + u] = a6;  // the one method slot
+    }
+    return;
+  }
   const bool fast = KIND == 1 && sh.slow == 0 && !p.rank && (methods & ~kFastSumMethods) == 0 &&
                     rrf_k >= 0 && rrf_k + N + 1 <= (1 << 24);
   if (fast) {
@@ -2009,10 +2022,18 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   static_assert(2 * kJsUMax <= 2 * NB, "(arrival, size) by position overlays the starts");
   // regions A (scores by position) and B (u by position) in one array: the spare
   // counter cnt[NB] lies at the start of B
-  __shared__ __attribute__((aligned(16))) double sval[kJsUMax + kJsUMax / 4];
-  uint16_t* su = (uint16_t*)(sval + kJsUMax);                          // region B
-  __shared__ __attribute__((aligned(16))) uint16_t bk[NB + 8];       // region C
-  uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                       // [NB + 1] u32
+  // One LDS array: region A = the scores by position (f64 [kJsUMax]; until the
+  // scatter: the range partials [0, 8 KB) and the u32 counters [8 KB, 24 KB));
+  // region BC after it = the u | size | arrival words by position (u32 [kJsUMax],
+  // from the scatter on), before that the bucket starts (u16, at BC + 6 KB), the
+  // spare counter cnt[NB] (BC[0]) and BYDOC's docid partials (BC[0, 4 KB)).
+  constexpr int kBcBytes = 6144 + 2 * (NB + 8);
+  static_assert(kBcBytes >= 4 * kJsUMax && 6144 >= 8 * BLOCK, "region BC layout");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[8 * kJsUMax + kBcBytes];
+  double* sval = (double*)lds;                                   // region A
+  uint32_t* sw = (uint32_t*)(lds + 8 * kJsUMax);                 // region BC: u << 20 | size << 8 | at
+  uint16_t* bk = (uint16_t*)(lds + 8 * kJsUMax + 6144);          // bucket starts [NB + 8]
+  uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                 // [NB + 1] u32
   __shared__ uint32_t sd[BYDOC ? kJsUMax : 1];  // docid by position (BYDOC)
   __shared__ uint32_t s_wtot[WAVES], s_big[WAVES];
   __shared__ double s_mn, s_mx;
@@ -2089,8 +2110,8 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
           dmx = max(dmx, d[j]);
         }
       }
-      ((uint32_t*)su)[tid] = dmn;
-      ((uint32_t*)su)[BLOCK + tid] = dmx;
+      sw[tid] = dmn;
+      sw[BLOCK + tid] = dmx;
     }
     const bool anynan = ballot(nan) != 0ull;
     if (lane == 0) s_wnan[wid] = anynan ? 1 : 0;
@@ -2108,7 +2129,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     mx = wave_max_f64_dpp(mx);
     uint32_t dmn = 0u, dmx = 0u;
     if (BYDOC) {
-      const uint32_t* sp = (const uint32_t*)su;
+      const uint32_t* sp = sw;
       dmn = sp[lane];
       dmx = sp[BLOCK + lane];
 #pragma unroll
@@ -2260,8 +2281,8 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   if (bk[tid] == 12345u) outp[0] = 0;
   return;
 #endif
-  // ---- scatter: value and u by position; (arrival, bucket size) kept ---------------
-  uint32_t pa[ROWS];  // position | (arrival | size << 8) << 16
+  // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
+  uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int u = wbase + j * 64 + lane;
@@ -2270,16 +2291,16 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
       const uint32_t st = bk[b], nx = bk[b + 1];
       const uint32_t pos = st + at;
       sval[pos] = v[j];
-      su[pos] = (uint16_t)u;
       if (BYDOC) sd[pos] = d[j];
-      pa[j] = pos | ((at | ((nx - st) << 8)) << 16);
+      pa[j] = pos;
+      pw[j] = ((uint32_t)u << 20) | ((nx - st) << 8) | at;
     }
   }
-  __syncthreads();  // the starts are dead: (arrival, size) by position over them
+  __syncthreads();  // the starts are dead: the u | size | arrival words over them
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int u = wbase + j * 64 + lane;
-    if (j < rows && u < U) bk[pa[j] & 0xFFFFu] = (uint16_t)(pa[j] >> 16);
+    if (j < rows && u < U) sw[pa[j]] = pw[j];
   }
   __syncthreads();
 #if defined(QF_BS_STOP) && QF_BS_STOP == 4
@@ -2295,10 +2316,11 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     uo[j] = 0u;
     if (j < rows && i < U) {
       const double vi = sval[i];
-      const uint32_t ui = su[i], s = bk[i];
-      // the tie-break key: u (first-seen order) or, BYDOC, the docid
-      const uint32_t ti = BYDOC ? sd[i] : ui;
-      const uint32_t lo = (uint32_t)i - (s & 0xFFu), hi = lo + (s >> 8);
+      const uint32_t wi = sw[i];
+      // the tie-break key: the whole word, whose top bits are u — distinct, so the
+      // word order is the first-seen order — or, BYDOC, the docid
+      const uint32_t ti = BYDOC ? sd[i] : wi;
+      const uint32_t lo = (uint32_t)i - (wi & 0xFFu), hi = lo + ((wi >> 8) & 0xFFFu);
       uint32_t before = 0u;
       // the bucket's members by pointer (two per step; a bucket of one: nothing to
       // count): no index arithmetic inside the loop
@@ -2306,9 +2328,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
       const double* pv = sval + k0;
       const double* const pend = sval + hi;
       const double* const plast = pend - 1;  // a pair remains while pv < plast
-      const auto* pt = (BYDOC ? (const void*)(sd + k0) : (const void*)(su + k0));
-      using tkey_t = typename std::conditional<BYDOC, uint32_t, uint16_t>::type;
-      const tkey_t* tp = (const tkey_t*)pt;
+      const uint32_t* tp = BYDOC ? sd + k0 : sw + k0;
       for (; pv < plast; pv += 2, tp += 2) {
         // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the
         // compiler would merge them into (8 cycles: it serves 16 lanes at a time)
@@ -2327,7 +2347,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
         before += (uint32_t)((v0 > vi) | ((v0 == vi) & (t0 < ti)));
       }
       P[j] = lo + before;
-      uo[j] = ui;
+      uo[j] = wi >> 20;
     }
   }
   // ---- outputs (every row's position before any store) ----------------------------------
