@@ -88,6 +88,12 @@ int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const 
                    const double* fused, const int64_t* qid_off, const char* qid_chars,
                    const int64_t* docno_off, const char* docno_chars, const char* tag,
                    int32_t n_threads);
+/* The same for qf_fuse_wide's uint32 perm. */
+int qfio_write_run32(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
+                     const int32_t* counts, const uint32_t* union_docid, const uint32_t* perm,
+                     const double* fused, const int64_t* qid_off, const char* qid_chars,
+                     const int64_t* docno_off, const char* docno_chars, const char* tag,
+                     int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -79,8 +79,10 @@ extern "C" {
 
 const char* qf_version(void);
 const char* qf_last_error(void);
-/* Largest Σ_r |list(q,r)| one query may have for qf_fuse. */
+/* Largest Σ_r |list(q,r)| one query may have for qf_fuse (65,535: perm is
+ * uint16) and for the *_wide entry points (16,777,215: perm is uint32). */
 int qf_max_entries_per_query(void);
+int qf_max_entries_per_query_wide(void);
 
 /*
  * Per-query min-max normalisation of every list (BaseRetriever.normalize_scores,
@@ -162,9 +164,11 @@ int qf_qpp_features(const int64_t* micro, int64_t n_queries, int32_t n_retriever
  * per (query, method): stable LDS bucket sort by fused score, which writes the
  * rank order as perm).
  * Queries of 10,241 .. qf_max_entries_per_query() (65,535) entries take a third
- * kernel (the same join in a global workspace + a bitonic sort), launched only
- * when max_entries > 10,240 (or n_retrievers > 16), with a workspace allocated and freed stream-ordered
- * (hipMallocAsync / hipFreeAsync on `stream`) — the one internal allocation.
+ * kernel (the same join in a global workspace + the bucket sort over the
+ * workspace), launched only when max_entries > 10,240 (or n_retrievers > 16),
+ * with a workspace allocated and freed stream-ordered (hipMallocAsync /
+ * hipFreeAsync on `stream`) — the one internal allocation.  Larger queries (up
+ * to qf_max_entries_per_query_wide()) need qf_fuse_wide: u can exceed 65,535.
  * max_entries must bound every query's entry count (larger queries report
  * QF_QSTATUS_TOOBIG).  n_retrievers <= 32; with more than 16 every query takes
  * the workspace kernel (its retriever masks are 32-bit, the LDS join's 16-bit).
@@ -192,6 +196,36 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
             int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
             uint16_t* perm, double* fused, int64_t out_stride, void* stream);
+
+/*
+ * qf_fuse, qf_fuse_probfuse, qf_fuse_learned_f32 and qf_fused_topk with a uint32
+ * perm [M][E]: every query up to qf_max_entries_per_query_wide() entries (its
+ * union's u may exceed 65,535).  Same outputs, same order, same errors; one call
+ * is all-uint32 (the small queries' perm too).  The reference has no per-query
+ * size limit (src/fusion.py:264-279 builds Python dicts): these lift qf_fuse's.
+ */
+int qf_fuse_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                 const uint32_t* docid, const void* score, int32_t score_kind,
+                 const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
+                 int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
+                 uint32_t* perm, double* fused, int64_t out_stride, void* stream);
+int qf_fuse_probfuse_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                          const uint32_t* docid, const void* score, int32_t score_kind,
+                          const int32_t* rank, const double* weights, int32_t methods,
+                          int32_t rrf_k, const double* seg_prob, int32_t n_segments,
+                          int32_t seg_len, int32_t max_entries, uint32_t* union_docid,
+                          int32_t* union_count, uint32_t* perm, double* fused,
+                          int64_t out_stride, void* stream);
+int qf_fuse_learned_f32_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                             const uint32_t* docid, const void* score, int32_t score_kind,
+                             const double* weights, uint32_t f32_runs, int32_t max_entries,
+                             uint32_t* union_docid, int32_t* union_count, uint32_t* perm,
+                             double* fused, int64_t out_stride, void* stream);
+int qf_fused_topk_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                       const int32_t* union_count, const uint32_t* union_docid,
+                       const uint32_t* perm, const double* fused, int64_t out_stride,
+                       int32_t n_methods, int32_t k, uint32_t* out_docid, double* out_score,
+                       void* stream);
 
 /*
  * qf_fuse with the ProbFuse segment table (ProbFuse.py:136-187): `methods` may

@@ -54,7 +54,7 @@ def fuse(list_off, docid, score, R, method, rrf_k=60, weights=None, rank=None):
     Q = (len(list_off) - 1) // R
     ud = np.zeros(E, np.uint32)
     uc = np.zeros(Q, np.int32)
-    perm = np.zeros(E, np.uint16)
+    perm = np.zeros(E, np.uint32)  # u may exceed 65,535 (qf_fuse_wide)
     fused = np.zeros(E, np.float64)
     m = METHODS.index(method) if isinstance(method, str) else int(method)
     rc = lib().oracle_fuse(Q, R, _p(list_off), _p(docid), _p(score), _p(rank), _p(weights), m,

@@ -85,7 +85,7 @@ static void msort(item_t* a, item_t* tmp, int64_t n) {
  */
 int oracle_fuse(int64_t Q, int32_t R, const int64_t* list_off, const uint32_t* docid,
                 const double* score, const int32_t* rank, const double* weights, int32_t method,
-                int32_t rrf_k, uint32_t* union_docid, int32_t* union_count, uint16_t* perm,
+                int32_t rrf_k, uint32_t* union_docid, int32_t* union_count, uint32_t* perm,
                 double* fused) {
   int64_t maxn = 0;
   for (int64_t q = 0; q < Q; ++q) {
@@ -164,7 +164,7 @@ int oracle_fuse(int64_t Q, int32_t R, const int64_t* list_off, const uint32_t* d
     }
     msort(items, tmp, U);
     for (int32_t i = 0; i < U; ++i) {
-      perm[base + i] = (uint16_t)items[i].i;
+      perm[base + i] = (uint32_t)items[i].i;
       fused[base + i] = items[i].s;
     }
     union_count[q] = U;

@@ -39,7 +39,8 @@ extern "C" {
 
 const char* qf_version(void) { return "qppfuse 0.1.0 gfx950"; }
 const char* qf_last_error(void) { return g_err.c_str(); }
-int qf_max_entries_per_query(void) { return qf::fuse_max_entries(); }
+int qf_max_entries_per_query(void) { return qf::fuse_max_entries(0); }
+int qf_max_entries_per_query_wide(void) { return qf::fuse_max_entries(1); }
 
 int qf_minmax_per_query(const double* score, const int64_t* list_off, int64_t n_lists,
                         double* out_norm, int32_t* out_micro, void* stream) {
@@ -119,8 +120,8 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
                        const int32_t* rank, const double* weights, int32_t methods,
                        int32_t rrf_k, const double* seg_prob, int32_t n_seg, int32_t seg_len,
                        int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
-                       uint16_t* perm, double* fused, int64_t out_stride, void* stream,
-                       const char* fn, uint32_t learned_f32 = 0u) {
+                       void* perm, int perm32, double* fused, int64_t out_stride,
+                       void* stream, const char* fn, uint32_t learned_f32 = 0u) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "%s: n_retrievers must be in [1, %d]", fn, kMaxR);
   if (methods <= 0 ||
@@ -134,9 +135,10 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
     return fail(QF_EINVAL, "%s: QF_PROBFUSE needs the segment table, x > 0 and L > 0", fn);
   if (score_kind != QF_SCORE_F64 && score_kind != QF_SCORE_MICRO)
     return fail(QF_EINVAL, "%s: bad score_kind %d", fn, score_kind);
-  if (max_entries > qf::fuse_max_entries())
-    return fail(QF_ETOOBIG, "%s: %d entries in one query exceed the kernel limit %d", fn,
-                max_entries, qf::fuse_max_entries());
+  if (max_entries > qf::fuse_max_entries(perm32))
+    return fail(QF_ETOOBIG, "%s: %d entries in one query exceed the kernel limit %d%s", fn,
+                max_entries, qf::fuse_max_entries(perm32),
+                perm32 ? "" : " (the _wide entry points take more, with a uint32 perm)");
   if (n_queries == 0) return QF_OK;
   if (!list_off || !docid || !score || !union_docid || !union_count || !perm || !fused ||
       out_stride < 0)
@@ -144,6 +146,7 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
   qf::FuseParams p{n_queries, n_retrievers, list_off,    docid,       score, rank,
                    weights,   methods,      rrf_k,       union_docid, union_count,
                    perm,      fused,        out_stride,  seg_prob,    n_seg, seg_len};
+  p.perm32 = perm32;
   if (learned_f32) {
     const uint32_t all = n_retrievers == 32 ? 0xFFFFFFFFu : (1u << n_retrievers) - 1u;
     p.learned_f32 = learned_f32 & all;
@@ -163,7 +166,19 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
     return fail(QF_EINVAL, "qf_fuse: QF_PROBFUSE needs qf_fuse_probfuse (segment table)");
   return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
                      methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
-                     fused, out_stride, stream, "qf_fuse");
+                     0, fused, out_stride, stream, "qf_fuse");
+}
+
+int qf_fuse_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                 const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
+                 const double* weights, int32_t methods, int32_t rrf_k, int32_t max_entries,
+                 uint32_t* union_docid, int32_t* union_count, uint32_t* perm, double* fused,
+                 int64_t out_stride, void* stream) {
+  if (methods & QF_PROBFUSE)
+    return fail(QF_EINVAL, "qf_fuse_wide: QF_PROBFUSE needs qf_fuse_probfuse_wide (segment table)");
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
+                     methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
+                     1, fused, out_stride, stream, "qf_fuse_wide");
 }
 
 int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
@@ -175,7 +190,19 @@ int qf_fuse_probfuse(int64_t n_queries, int32_t n_retrievers, const int64_t* lis
                      void* stream) {
   return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
                      methods, rrf_k, seg_prob, n_segments, seg_len, max_entries, union_docid,
-                     union_count, perm, fused, out_stride, stream, "qf_fuse_probfuse");
+                     union_count, perm, 0, fused, out_stride, stream, "qf_fuse_probfuse");
+}
+
+int qf_fuse_probfuse_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                          const uint32_t* docid, const void* score, int32_t score_kind,
+                          const int32_t* rank, const double* weights, int32_t methods,
+                          int32_t rrf_k, const double* seg_prob, int32_t n_segments,
+                          int32_t seg_len, int32_t max_entries, uint32_t* union_docid,
+                          int32_t* union_count, uint32_t* perm, double* fused,
+                          int64_t out_stride, void* stream) {
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
+                     methods, rrf_k, seg_prob, n_segments, seg_len, max_entries, union_docid,
+                     union_count, perm, 1, fused, out_stride, stream, "qf_fuse_probfuse_wide");
 }
 
 int qf_fuse_learned_f32(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
@@ -185,23 +212,53 @@ int qf_fuse_learned_f32(int64_t n_queries, int32_t n_retrievers, const int64_t* 
                         double* fused, int64_t out_stride, void* stream) {
   return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, nullptr,
                      weights, QF_LEARNED, 60, nullptr, 0, 0, max_entries, union_docid,
-                     union_count, perm, fused, out_stride, stream, "qf_fuse_learned_f32",
+                     union_count, perm, 0, fused, out_stride, stream, "qf_fuse_learned_f32",
                      f32_runs);
+}
+
+int qf_fuse_learned_f32_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                             const uint32_t* docid, const void* score, int32_t score_kind,
+                             const double* weights, uint32_t f32_runs, int32_t max_entries,
+                             uint32_t* union_docid, int32_t* union_count, uint32_t* perm,
+                             double* fused, int64_t out_stride, void* stream) {
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, nullptr,
+                     weights, QF_LEARNED, 60, nullptr, 0, 0, max_entries, union_docid,
+                     union_count, perm, 1, fused, out_stride, stream,
+                     "qf_fuse_learned_f32_wide", f32_runs);
+}
+
+static int topk_common(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                       const int32_t* union_count, const uint32_t* union_docid, const void* perm,
+                       int perm32, const double* fused, int64_t out_stride, int32_t n_methods,
+                       int32_t k, uint32_t* out_docid, double* out_score, void* stream,
+                       const char* fn) {
+  if (n_queries < 0 || n_retrievers <= 0 || n_methods <= 0 || k < 0 || out_stride < 0)
+    return fail(QF_EINVAL, "%s: bad sizes", fn);
+  if (n_queries > 0 && k > 0 &&
+      (!list_off || !union_count || !union_docid || !perm || !fused || !out_docid || !out_score))
+    return fail(QF_EINVAL, "%s: null buffer", fn);
+  return check(qf::topk_launch(n_queries, n_retrievers, list_off, union_count, union_docid, perm,
+                               perm32, fused, out_stride, n_methods, k, out_docid, out_score,
+                               (hipStream_t)stream),
+               fn);
 }
 
 int qf_fused_topk(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
                   const int32_t* union_count, const uint32_t* union_docid, const uint16_t* perm,
                   const double* fused, int64_t out_stride, int32_t n_methods, int32_t k,
                   uint32_t* out_docid, double* out_score, void* stream) {
-  if (n_queries < 0 || n_retrievers <= 0 || n_methods <= 0 || k < 0 || out_stride < 0)
-    return fail(QF_EINVAL, "qf_fused_topk: bad sizes");
-  if (n_queries > 0 && k > 0 &&
-      (!list_off || !union_count || !union_docid || !perm || !fused || !out_docid || !out_score))
-    return fail(QF_EINVAL, "qf_fused_topk: null buffer");
-  return check(qf::topk_launch(n_queries, n_retrievers, list_off, union_count, union_docid, perm,
-                               fused, out_stride, n_methods, k, out_docid, out_score,
-                               (hipStream_t)stream),
-               "qf_fused_topk");
+  return topk_common(n_queries, n_retrievers, list_off, union_count, union_docid, perm, 0, fused,
+                     out_stride, n_methods, k, out_docid, out_score, stream, "qf_fused_topk");
+}
+
+int qf_fused_topk_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                       const int32_t* union_count, const uint32_t* union_docid,
+                       const uint32_t* perm, const double* fused, int64_t out_stride,
+                       int32_t n_methods, int32_t k, uint32_t* out_docid, double* out_score,
+                       void* stream) {
+  return topk_common(n_queries, n_retrievers, list_off, union_count, union_docid, perm, 1, fused,
+                     out_stride, n_methods, k, out_docid, out_score, stream,
+                     "qf_fused_topk_wide");
 }
 
 int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,

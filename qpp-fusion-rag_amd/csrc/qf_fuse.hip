@@ -383,7 +383,8 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
 // by u: the ranked list is fused[perm[i]] (include/qppfuse.h).
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
-                                          const uint32_t (&item)[ITEMS], uint16_t* operm) {
+                                          const uint32_t (&item)[ITEMS], const FuseParams& p,
+                                          int64_t po) {
   int ro = sx.rows;
   asm volatile("" : "+s"(ro));
 #pragma unroll
@@ -391,7 +392,7 @@ __device__ __forceinline__ void write_out(const SortCtx<ITEMS, WAVES>& sx,
     const int i = (sx.wid * ro + j) * 64 + sx.lane;
     // final outputs, not re-read by the device: non-temporal, so they do not evict
     // the unsorted scores other workgroups are about to gather
-    if (j < ro && i < sx.U) __builtin_nontemporal_store((uint16_t)(item[j] & kUMask), &operm[i]);
+    if (j < ro && i < sx.U) perm_put(p, po + i, item[j] & kUMask);
   }
 }
 
@@ -1167,7 +1168,7 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
   QF_STAMP(0);
   if (hb_full > 0) sort_desc(sx, item, hb - lo, exact, hb_full);  // else all keys equal
   QF_STAMP(1);
-  write_out(sx, item, p.perm + (int64_t)ms * p.out_stride + base);
+  write_out(sx, item, p, (int64_t)ms * p.out_stride + base);
   QF_STAMP(2);
 }
 // Method bit of output slot ms.
@@ -1224,7 +1225,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
       const int U = p.union_count[q];
       bool take = U >= umin && U <= C::kUMax;
       if (FB && U > 1 && U <= kJsUMax)
-        take = p.perm[(idx % M) * p.out_stride + p.list_off[q * p.R]] == kJsUnsorted;
+        take = perm_get(p, (idx % M) * p.out_stride + p.list_off[q * p.R]) == kJsUnsorted;
       if (take) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
     }
     __syncthreads();
@@ -1242,696 +1243,51 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
 
 
 // ============================================================================
-// join_sort_kernel — the common case in ONE kernel: the join above, the sums in
-// registers, and every requested method's stable descending sort in LDS, so the
-// unsorted fused scores never travel through HBM (one workgroup per query;
-// micro-unit scores, <= 16 runs, N <= 5,120 entries, U <= kJsUMax documents,
-// methods among CombSUM / CombMNZ / RRF / W-CombSUM / W-CombMNZ / W-RRF).
-//
-// Per method, a bucket sort on a monotone key:
-//   w(v) = (bits(float((v - smin) + delta)) - bits(float(delta))) >> sh
-//   (delta = (smax - smin) / 4096): every rounding in it is monotone and the
-//   bits of a non-negative float are ordered, so w is non-decreasing in v and
-//   equal scores (-0.0 and +0.0 included) share a bucket.  In float bits it
-//   resolves scores relative to their distance from smin — ~3,840 buckets over
-//   ~12 binades above delta — which suits the skewed fused distributions (most
-//   documents sit in one list near the bottom; a run with a tiny weight packs
-//   its documents just above smin).  The minimum itself (shared by hundreds of
-//   documents when a run has weight 0) gets 256 buckets split by u.
-//   1. count: one returning LDS atomic per item on its bucket (order inside a
-//      bucket is arbitrary);
-//   2. exclusive scan of the bucket counters (and the largest bucket);
-//   3. scatter value + u to start[w] + slot;
-//   4. the final position of an item is its bucket's start + the number of
-//      items of its bucket that precede it in (score descending, u ascending)
-//      order — the stable sort's order, counted exactly with f64 compares.
+// The bucket sort of the default path (bsort_kernel below; join_sort_xl_kernel's
+// workspace bucket sort is the same algorithm over a global workspace).
+// Per (query, method) slot, over the join's unsorted fused[slot][0..U):
+//   1. count: one returning LDS atomic per item on its bucket, a monotone key of
+//      the score (order inside a bucket is arbitrary; the return value is the
+//      item's arrival index);
+//   2. exclusive scan of the bucket counters;
+//   3. scatter the score (and what the rank needs) to start[bucket] + arrival;
+//   4. the final position of an item is its bucket's start + the number of items
+//      of its bucket that precede it in (score descending, u ascending) order —
+//      the stable sort's order, counted exactly with f64 compares.
 // Its cost per item is the size of its bucket (C2 with QPP or random weights:
-// 2-2.5 on average, largest buckets ~10-60; tools/bucket_stats.py).  A bucket
-// above kJsBucketMax or a non-finite / NaN score range leaves the (query,
-// method) to the LSD window sort of fuse_large_kernel's fallback pass (the same
-// order).
-// Unions above kJsUMax are stored unsorted for fuse_large_kernel.
+// 2-2.5 on average; tools/bucket_stats.py).  A bucket above kJsBucketMax is
+// counted once more with a finer key (QF_BS_RETRY_SHIFT); a bucket still above
+// it or a non-finite / NaN score range leaves the (query, method) to the LSD
+// window sort of fuse_large_kernel's fallback pass (the same order).
+// (Rounds 1-2 also kept a one-kernel join + sort and a float-bit-key bucket sort
+// for A/B; both measured slower and were removed in round 3.)
 // ============================================================================
-constexpr int kJsBits = 12;
-constexpr int kJsBuckets = 1 << kJsBits;
 constexpr int kJsBucketMax = 128;
-constexpr int kJsMethods = QF_COMBSUM | QF_COMBMNZ | QF_RRF | QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF;
-
-template <int BLOCK>
-struct JsCfg {
-  using J = JoinCfg<BLOCK, 5120 / BLOCK, 13>;  // N <= 5,120
-  static constexpr int kWaves = BLOCK / 64;
-  static constexpr int kRows = (kJsUMax + BLOCK - 1) / BLOCK;
-  // sort-phase LDS, over the join's: scores by position f64 [kJsUMax], u by
-  // position u16 [kJsUMax], and two sets of bucket counters / starts u32
-  // [kJsBuckets + 4] used by alternate methods (each method zeroes the next
-  // one's set while it counts: no zeroing pass, no extra barrier).  Set 0 lies
-  // beyond the join's LDS and is zeroed when the kernel starts.
-  static constexpr int kValOff = 0;
-  static constexpr int kUOff = kValOff + 8 * kJsUMax;
-  static constexpr int kCnt1Off = kUOff + 2 * kJsUMax;
-  static constexpr int kCntBytes = 4 * (kJsBuckets + 4);
-  static constexpr int kCnt0Off = (JoinLds<J, 1>::kBytes > kCnt1Off + kCntBytes
-                                   ? JoinLds<J, 1>::kBytes : kCnt1Off + kCntBytes);
-  static constexpr int kBytes = kCnt0Off + kCntBytes;
-};
-
-// Buckets: descending scores fill ascending buckets.  Scores above smin take
-// [0, kJsMinBase) by the float-bit key; the minimum score — often shared by
-// hundreds of documents (every document of a zero-weight run, the 0.000000
-// bottom of each .norm.res list) — takes [kJsMinBase, kJsBuckets) split by u,
-// so equal scores do not pile into one bucket.
-constexpr int kJsMinSub = 256;
-constexpr int kJsMinBase = kJsBuckets - kJsMinSub;
-
-// The bucket of a score (x >= delta > 0 for every v in [smin, smax]); usub =
-// kJsMinSub / U (rounded), so u * usub is non-decreasing in u and below kJsMinSub.
-__device__ __forceinline__ uint32_t js_bucket(double v, uint32_t u, float usub, double smin,
-                                              double delta, uint32_t b0, int sh) {
-  const float x = (float)((v - smin) + delta);
-  const uint32_t above = (uint32_t)(kJsMinBase - 1) - (((uint32_t)__float_as_uint(x) - b0) >> sh);
-  const uint32_t sub = min((uint32_t)((float)u * usub), (uint32_t)(kJsMinSub - 1));
-  return v == smin ? (uint32_t)kJsMinBase + sub : above;
-}
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, 4) void join_sort_kernel(FuseParams p) {
-  using Cfg = JsCfg<BLOCK>;
-  using C = typename Cfg::J;
-  constexpr int ROWS = Cfg::kRows, WAVES = Cfg::kWaves;
-  __shared__ JoinShared<C, 1, Cfg::kBytes> sh;
-  static_assert(Cfg::kCnt0Off >= JoinLds<C, 1>::kBytes, "counter set 0 outside the join's LDS");
-  __shared__ unsigned long long s_kmin[kNMethods], s_kmax[kNMethods];
-  __shared__ int s_nan[kNMethods];
-  __shared__ uint32_t s_wtot[WAVES];
-  __shared__ int s_bmax;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t q = block_id();
-  if (q >= p.n_queries) return;
-  if (tid < kNMethods) {  // ordered before their atomics by join_groups' barriers
-    s_kmin[tid] = ~0ull;
-    s_kmax[tid] = 0ull;
-    s_nan[tid] = 0;
-  }
-  for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)  // counter set 0 (see JsCfg)
-    *(uint4*)(sh.smem + Cfg::kCnt0Off + 4 * i) = make_uint4(0u, 0u, 0u, 0u);
-  QF_STAMP_INIT();
-  const int N = join_groups<C, 1>(p, sh, q);
-  if (N < 0) return;
-  QF_STAMP(0);  // the whole join
-  const int U = sh.U;
-  const int64_t base = sh.off[0];
-  if (sh.status != 0 || U > kJsUMax) {  // uniform: an error, or a union for fuse_large_kernel
-    if (sh.status == 0) store_unsorted_sums<C, 1>(p, sh, N);
-    if (tid == 0) p.union_count[q] = sh.status ? sh.status : U;
-    return;
-  }
-  // ---- sums, one document per (thread, row): u = (wid * rows + j) * 64 + lane ----
-  const int rows_all = (U + BLOCK - 1) / BLOCK;
-  const int rows = rows_all;
-  const int methods = p.methods, rrf_k = p.rrf_k;
-  const int32_t* gsc = (const int32_t*)(sh.smem + JoinLds<C, 1>::kGscOff);
-  const uint32_t* gpr = (const uint32_t*)(sh.smem + JoinLds<C, 1>::kGprOff);
-  const uint16_t* ugo = (const uint16_t*)(sh.smem + JoinLds<C, 1>::kGoOff);
-  double a0[ROWS], a1[ROWS], a2[ROWS], a5[ROWS];
-  uint32_t cnts = 0u;  // each document's list count, 5 bits per row
-  // The sums of js_sums, with the per-entry range checks of the division-free
-  // quotients dropped when the whole query is in range (FAST: every list already
-  // [0, 1], every weight in range, ranks = positions, k + N + 1 <= 2^24).
-  auto js_sums = [&](auto fast_tag) {
-    constexpr bool FAST = decltype(fast_tag)::value;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      a0[j] = a1[j] = a2[j] = a5[j] = 0.0;
-      const int u = (wid * rows + j) * 64 + lane;
-      if (j < rows && u < U) {
-        const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
-        cnts |= (uint32_t)(ge - gs) << (5 * j);
-        for (int k = gs; k < ge; ++k) {
-          const double s = micro_to_f64(gsc[k]);
-          const uint32_t q2 = gpr[k];
-          const int r = (int)(q2 >> 16), pos = (int)(q2 & 0xFFFFu);
-          if (methods & (QF_COMBSUM | QF_COMBMNZ)) {  // as store_unsorted_sums
-            if (FAST) {
-              a0[j] += s;  // (s - 0.0) / 1.0 == s, -0.0 included
-            } else {
-              const double den = sh.den[r], mn = sh.mn[r];
-              double x = 0.0;
-              if (den > 0.0) {
-                const double d = s - mn;
-                x = (den == 1.0 && mn == 0.0) ? s
-                    : (den >= 0x1p-900 && den <= 0x1p900 && d >= 0x1p-900 && d <= 0x1p900)
-                        ? div_by_recip(d, den, sh.rden[r])
-                        : d / den;
-              }
-              a0[j] += x;
-            }
-          }
-          if (methods & QF_RRF)
-            a1[j] += FAST ? recip_small(rrf_k + pos + 1) : recip_int(rrf_k + pos + 1);
-          if (methods & (QF_WCOMBSUM | QF_WCOMBMNZ)) a2[j] += sh.w[r] * s;
-          if (methods & QF_WRRF) {
-            if (FAST) {
-              a5[j] += div_small(sh.w[r], rrf_k + pos + 1);
-            } else {
-              const int rk = p.rank ? p.rank[sh.off[r] + pos] : pos + 1;
-              a5[j] += div_int(sh.w[r], rrf_k + rk);
-            }
-          }
-        }
-      }
-    }
-  };
-  const bool fast_sums = sh.slow == 0 && !p.rank && rrf_k >= 0 && rrf_k + N + 1 <= (1 << 24);
-  if (fast_sums) js_sums(std::true_type{});
-  else js_sums(std::false_type{});
-  // the score of method bit t for row j (CombMNZ: sum x count, src/fusion.py:327)
-  auto score_of = [&](int t, int j) -> double {
-    const double c = (double)((cnts >> (5 * j)) & 31u);
-    switch (t) {
-      case 0: return a0[j];
-      case 1: return a0[j] * c;
-      case 2: return a1[j];
-      case 3: return a2[j];
-      case 4: return a2[j] * c;
-      default: return a5[j];
-    }
-  };
-  // ---- every method's score range (f64 min / max; NaN flagged) --------------------
-  const int M = __popc(methods);
-#pragma unroll 1
-  for (int ms = 0; ms < M; ++ms) {
-    const int t = slot_method(methods, ms);
-    double vmn = INFINITY, vmx = -INFINITY;
-    bool nan = false;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = (wid * rows + j) * 64 + lane;
-      if (j < rows && u < U) {
-        const double v = score_of(t, j);
-        vmn = fmin(vmn, v);  // IEEE minNum / maxNum: a NaN is skipped (flagged below)
-        vmx = fmax(vmx, v);
-        nan |= v != v;
-      }
-    }
-    vmn = wave_min_f64_dpp(vmn);
-    vmx = wave_max_f64_dpp(vmx);
-    const bool anynan = ballot(nan) != 0ull;
-    if (lane == 63) {
-      atomicMin(&s_kmin[ms], (unsigned long long)~f64_asc_key(vmx));  // kmin <-> smax
-      atomicMax(&s_kmax[ms], (unsigned long long)~f64_asc_key(vmn));
-      if (anynan) s_nan[ms] = 1;
-    }
-  }
-  if (tid == 0) p.union_count[q] = U;
-  QF_STAMP(8);
-  __syncthreads();  // the groups are dead: their LDS becomes the sort's
-  QF_STAMP(14);
-  double* sval = (double*)(sh.smem + Cfg::kValOff);   // scores by position
-  uint16_t* su = (uint16_t*)(sh.smem + Cfg::kUOff);   // u by position
-#pragma unroll 1
-  for (int ms = 0; ms < M; ++ms) {
-    const int t = slot_method(methods, ms);
-    // opaque per iteration: keeps the compiler from hoisting every row's products and
-    // addresses out of this loop (register pressure; they are cheap to recompute)
-    int rows = rows_all;
-    asm volatile("" : "+s"(rows));
-    asm volatile("" : "+v"(cnts));
-    uint32_t* bk = (uint32_t*)(sh.smem + ((ms & 1) ? Cfg::kCnt1Off : Cfg::kCnt0Off));
-    uint32_t* bk_next = (uint32_t*)(sh.smem + ((ms & 1) ? Cfg::kCnt0Off : Cfg::kCnt1Off));
-    const uint64_t kmin = s_kmin[ms], kmax = s_kmax[ms];  // ~orderable: kmin <-> smax
-    double* outv = p.fused + (int64_t)ms * p.out_stride + base;
-    uint16_t* outp = p.perm + (int64_t)ms * p.out_stride + base;
-    QF_STAMP(9);
-    if (kmax == kmin && !s_nan[ms]) {  // every score equal: first-seen order
-      for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)
-        *(uint4*)&bk_next[i] = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int u = (wid * rows + j) * 64 + lane;
-        if (j < rows && u < U) {
-          __builtin_nontemporal_store((uint16_t)u, &outp[u]);
-          __builtin_nontemporal_store(score_of(t, j), &outv[u]);
-        }
-      }
-      __syncthreads();
-      continue;
-    }
-    const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
-    const double rng = smax - smin;
-    const double delta = rng * 0x1p-12;
-    const float ftop = (float)(rng + delta);
-    // a finite range without NaN (a NaN's key lies beyond +-inf's) and a positive
-    // delta: the bucket sort; otherwise the fallback pass's LSD window sort
-    bool fast = isfinite(rng) && isfinite(ftop) && delta > 0.0 && !s_nan[ms];
-    const uint32_t b0 = __float_as_uint((float)delta);
-    const uint32_t span = __float_as_uint(ftop) - b0;
-    int bsh = span >= (uint32_t)kJsBuckets ? (32 - __clz((int)span)) - kJsBits : 0;
-    if ((span >> bsh) >= (uint32_t)kJsMinBase) ++bsh;  // now span >> bsh < kJsMinBase
-    const float usub = (float)kJsMinSub / (float)U;
-    QF_STAMP(10);
-    uint32_t ws[ROWS];
-    if (fast) {
-      // ---- 1. count (and zero the next method's counters) ----------------------------
-      // every row's atomic issued before any result is used: rows past U add 0
-      // to bucket 0
-      uint32_t old[ROWS];
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int u = (wid * rows + j) * 64 + lane;
-        const bool ok = j < rows && u < U;
-        ws[j] = ok ? js_bucket(score_of(t, j), (uint32_t)u, usub, smin, delta, b0, bsh) : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int u = (wid * rows + j) * 64 + lane;
-        old[j] = atomicAdd(&bk[ws[j]], (j < rows && u < U) ? 1u : 0u);
-      }
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) ws[j] |= old[j] << 16;
-      for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)
-        *(uint4*)&bk_next[i] = make_uint4(0u, 0u, 0u, 0u);
-      if (tid == 0) s_bmax = 0;
-      QF_STAMP(11);
-      __syncthreads();
-      QF_STAMP(12);
-      // ---- 2. exclusive scan of the counters, largest bucket ----------------------
-      {
-        constexpr int kPer = kJsBuckets / BLOCK;
-        uint32_t c[kPer], tot = 0u, mx = 0u;
-#pragma unroll
-        for (int i = 0; i < kPer; i += 4) {
-          const uint4 x4 = *(const uint4*)&bk[tid * kPer + i];
-          c[i] = x4.x; c[i + 1] = x4.y; c[i + 2] = x4.z; c[i + 3] = x4.w;
-        }
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-          mx = max(mx, c[i]);
-          const uint32_t x = c[i];
-          c[i] = tot;
-          tot += x;
-        }
-        const uint32_t incl = wave_incl_scan_dpp(tot);
-        if (lane == 63) s_wtot[wid] = incl;
-        mx = (uint32_t)wave_max_u64_dpp(mx);
-        if (lane == 63) atomicMax(&s_bmax, (int)mx);
-        __syncthreads();
-        uint32_t pre = incl - tot;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w)
-          if (w < wid) pre += s_wtot[w];
-#pragma unroll
-        for (int i = 0; i < kPer; i += 4)
-          *(uint4*)&bk[tid * kPer + i] =
-              make_uint4(pre + c[i], pre + c[i + 1], pre + c[i + 2], pre + c[i + 3]);
-        if (tid == 0) bk[kJsBuckets] = (uint32_t)U;
-      }
-      __syncthreads();
-      QF_STAMP(13);
-      fast = s_bmax <= kJsBucketMax;  // uniform
-    } else {
-      for (int i = tid * 4; i < kJsBuckets + 4; i += BLOCK * 4)
-        *(uint4*)&bk_next[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    if (fast) {
-      // ---- 3. scatter ----------------------------------------------------------
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int u = (wid * rows + j) * 64 + lane;
-        if (j < rows && u < U) {
-          const uint32_t pos = bk[ws[j] & 0xFFFFu] + (ws[j] >> 16);
-          sval[pos] = score_of(t, j);
-          su[pos] = (uint16_t)u;
-        }
-      }
-      __syncthreads();
-      QF_STAMP(1);
-      // ---- 4. rank inside the bucket, write the outputs ---------------------------
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int i = (wid * rows + j) * 64 + lane;
-        if (j < rows && i < U) {
-          const double vi = sval[i];
-          const uint32_t ui = su[i];
-          const uint32_t w = js_bucket(vi, ui, usub, smin, delta, b0, bsh);
-          const uint32_t lo = bk[w], hi = bk[w + 1];
-          // items of the bucket before this one: higher scores, or equal scores
-          // with a smaller u (branch-free; two items per step, loads issued together)
-          uint32_t before = 0u;
-          uint32_t k = hi - lo > 1u ? lo : hi;  // a bucket of one: nothing to count
-          for (; k + 1 < hi; k += 2) {
-            const double v0 = sval[k], v1 = sval[k + 1];
-            const uint32_t u0 = su[k], u1 = su[k + 1];
-            before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui))) +
-                      (uint32_t)((v1 > vi) | ((v1 == vi) & (u1 < ui)));
-          }
-          if (k < hi) {
-            const double v0 = sval[k];
-            const uint32_t u0 = su[k];
-            before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui)));
-          }
-          const uint32_t P = lo + before;
-          __builtin_nontemporal_store((uint16_t)ui, &outp[P]);
-          __builtin_nontemporal_store(vi, &outv[ui]);  // scores stay by u (perm ranks them)
-        }
-      }
-      QF_STAMP(2);
-    } else {
-      // ---- fallback: the scores go out unsorted (by u), perm[0] marked; the LSD
-      // window sort of fuse_large_kernel's fallback pass finishes this (query, method) ---------
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int u = (wid * rows + j) * 64 + lane;
-        if (j < rows && u < U) outv[u] = score_of(t, j);
-      }
-      if (tid == 0) outp[0] = kJsUnsorted;
-    }
-    __syncthreads();
-    QF_STAMP(15);
-  }
-  QF_STAMP(14);
-}
-
-// ============================================================================
-// bucket_sort_kernel — the same bucket sort as join_sort_kernel, as a kernel of
-// its own over the join kernel's unsorted fused[slot][u]: one workgroup per
-// (query, method slot), U <= kJsUMax, everything after the load in LDS
-// (scores by position f64, u by position u16, 2^BITS bucket counters).  Small
-// enough to keep 4 workgroups (32 waves) per CU.  A (query, method) it cannot
-// order (a bucket above kJsBucketMax, a non-finite range, a NaN) gets its perm[0]
-// marked for fuse_large_kernel's fallback pass; its scores stay unsorted in place.
-// ============================================================================
-#ifndef QF_BS_REV
-#define QF_BS_REV 1
-#endif
-// delta = range / 2^QF_BS_DELTA_SHIFT: the float-bit key resolves the scores over
-// about QF_BS_DELTA_SHIFT binades above the minimum
-#ifndef QF_BS_DELTA_SHIFT
-#define QF_BS_DELTA_SHIFT 12
-#endif
 #ifndef QF_BS_RETRY_SHIFT  // the recount's finer delta (a bucket overflowed)
 #define QF_BS_RETRY_SHIFT 20
 #endif
-template <int BLOCK, int BITS>
-struct BsCfg {
-  static constexpr int kWaves = BLOCK / 64;
-  static constexpr int kRows = (kJsUMax + BLOCK - 1) / BLOCK;
-  static constexpr int kBuckets = 1 << BITS;
-  static constexpr int kMinSub = kBuckets / 16;
-  static constexpr int kMinBase = kBuckets - kMinSub;
-};
 
-// The bucket of a score: join_sort_kernel's js_bucket, with the minimum's
-// sub-bucket u >> ush (ush chosen so that U - 1 >> ush < MINSUB).
-template <int NB, int MINBASE, int MINSUB>
-__device__ __forceinline__ uint32_t bs_bucket(double v, uint32_t u, int ush, double smin,
-                                              double delta, uint32_t b0, int sh) {
-  const float x = (float)((v - smin) + delta);
-  const uint32_t above = (uint32_t)(MINBASE - 1) - (((uint32_t)__float_as_uint(x) - b0) >> sh);
-  return v == smin ? (uint32_t)MINBASE + (u >> ush) : above;
-}
-
-template <int BLOCK, int BITS>
-__global__ __launch_bounds__(BLOCK, 8) void bucket_sort_kernel(FuseParams p) {
-  using Cfg = BsCfg<BLOCK, BITS>;
-  constexpr int ROWS = Cfg::kRows, WAVES = Cfg::kWaves, NB = Cfg::kBuckets;
-  constexpr int MINBASE = Cfg::kMinBase, MINSUB = Cfg::kMinSub;
-  __shared__ double sval[kJsUMax];
-  __shared__ uint16_t su[kJsUMax];
-  // bucket counters, then starts: u16 (U <= kJsUMax), two per word
-  __shared__ __attribute__((aligned(16))) uint32_t bkw[NB / 2 + 8];
-  const uint16_t* bk = (const uint16_t*)bkw;
-  __shared__ uint32_t s_wtot[WAVES], s_wmax[WAVES];
-  __shared__ double s_wmin_v[WAVES], s_wmax_v[WAVES];
-  __shared__ int s_wnan[WAVES], s_gnan;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // block -> (query, method slot): slot-major groups of 8 queries (fuse_kernel's
-  // map: query q on XCD q % 8, where the join wrote it), the groups in reverse:
-  // the join's last-written scores are the likeliest still in the L2 /
-  // Infinity Cache
-  const int M = __popc(p.methods);
-  const int64_t bid = block_id();
-  const int64_t grp8 = bid >> 3, ngroups = (p.n_queries + 7) / 8;
-  if (grp8 >= ngroups * M) return;  // a 2-D grid's padding workgroups (grid_for)
-#if QF_BS_REV
-  const int64_t q = (ngroups - 1 - grp8 / M) * 8 + (bid & 7);
-#else
-  const int64_t q = (grp8 / M) * 8 + (bid & 7);
-#endif
-  const int ms = (int)(grp8 % M);
-  if (q >= p.n_queries) return;
-  const int U = p.union_count[q];
-  const int64_t base = p.list_off[q * p.R];
-  if (U < 1 || U > kJsUMax) return;  // error / fuse_large_kernel's
-  QF_STAMP_INIT();
-  double* io = p.fused + (int64_t)ms * p.out_stride + base;
-  uint16_t* outp = p.perm + (int64_t)ms * p.out_stride + base;
-  const int rows = (U + BLOCK - 1) / BLOCK;
-  double v[ROWS];
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {  // every row's load in flight before the first use
-    const int u = (wid * rows + j) * 64 + lane;
-    v[j] = (j < rows && u < U) ? io[u] : 0.0;
-  }
-  for (int i = tid * 4; i < NB / 2 + 8; i += BLOCK * 4)
-    *(uint4*)&bkw[i] = make_uint4(0u, 0u, 0u, 0u);
-  QF_STAMP(8);
-  {  // score range: f64 min / max (a NaN flagged).  Every thread's partials go
-     // through sval (unused until the scatter) and wave 0 alone reduces the
-     // 2 x BLOCK of them: one wave's DPP reductions instead of every wave's
-    double vmn = INFINITY, vmx = -INFINITY;
-    bool nan = false;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = (wid * rows + j) * 64 + lane;
-      if (j < rows && u < U) {
-        vmn = fmin(vmn, v[j]);
-        vmx = fmax(vmx, v[j]);
-        nan |= v[j] != v[j];
-      }
-    }
-    sval[tid] = vmn;
-    sval[BLOCK + tid] = vmx;
-    const bool anynan = ballot(nan) != 0ull;
-    if (lane == 0) s_wnan[wid] = anynan ? 1 : 0;
-  }
-  __syncthreads();  // also orders the counters' zeroing before the count
-  if (wid == 0) {
-    __builtin_amdgcn_s_setprio(3);  // the block waits on this wave (see the join's scans)
-    // lane-contiguous reads (i * 64 + lane): a lane stride of PER doubles hit 4 of
-    // the 64 banks, a 16-way conflict on every read of the block's critical path.
-    // min / max do not depend on the order (the folded keys below equate -0.0, +0.0)
-    constexpr int PER = BLOCK / 64;
-    double mn = sval[lane], mx = sval[BLOCK + lane];
-#pragma unroll
-    for (int i = 1; i < PER; ++i) {
-      mn = fmin(mn, sval[i * 64 + lane]);
-      mx = fmax(mx, sval[BLOCK + i * 64 + lane]);
-    }
-    mn = wave_min_f64_dpp(mn);
-    mx = wave_max_f64_dpp(mx);
-    int anyn = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) anyn |= s_wnan[w];
-    if (lane == 63) {
-      s_wmin_v[0] = mn;
-      s_wmax_v[0] = mx;
-      s_gnan = anyn;
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-  __syncthreads();
-  QF_STAMP(9);
-  const double gmn = s_wmin_v[0], gmx = s_wmax_v[0];
-  const int gnan = s_gnan;
-  // folded keys as join_sort_kernel: kmin <-> the largest score, -0.0 == +0.0
-  const uint64_t kmin = ~f64_asc_key(gmx), kmax = ~f64_asc_key(gmn);
-  const bool nan = gnan != 0;
-  if (kmax == kmin && !nan) {  // every score equal: first-seen order, scores in place
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = (wid * rows + j) * 64 + lane;
-      if (j < rows && u < U) __builtin_nontemporal_store((uint16_t)u, &outp[u]);
-    }
-    return;
-  }
-  const double smax = f64_from_asc_key(~kmin), smin = f64_from_asc_key(~kmax);
-  const double rng = smax - smin;
-  int ush = 0;  // U - 1 >> ush < MINSUB
-  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
-  // A bucket above kJsBucketMax items (documents packed just above the minimum by a
-  // run with a tiny weight) is counted again once with delta 2^8 times finer (~20
-  // binades above the minimum) before the pair is left to the fallback pass: the
-  // finer key alone costs ~7 % on the usual fused distributions, the fallback
-  // pass's LSD sort much more on the few it catches
-  double delta;
-  uint32_t b0;
-  int bsh;
-  uint32_t ws[ROWS], old[ROWS];
-  // count with delta = range / 2^shift; returns -1 for a range the key cannot take
-  // (the pair is marked), else whether some bucket is above kJsBucketMax.  A lambda
-  // called twice, not a loop: the loop kept values live across it (VGPR spills)
-  auto count = [&](const int shift) -> int {
-    delta = ldexp(rng, -shift);
-    const float ftop = (float)(rng + delta);
-    if (!(isfinite(rng) && isfinite(ftop) && delta > 0.0) || nan) return -1;  // uniform
-    b0 = __float_as_uint((float)delta);
-    const uint32_t span = __float_as_uint(ftop) - b0;
-    bsh = span >= (uint32_t)NB ? (32 - __clz((int)span)) - BITS : 0;
-    if ((span >> bsh) >= (uint32_t)MINBASE) ++bsh;
-    // ---- 1. count ------------------------------------------------------------------
-    // every row's atomic issued before any result is used; rows past U add 0 to
-    // bucket 0 (no branches around the atomics, one wait)
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = (wid * rows + j) * 64 + lane;
-      const bool ok = j < rows && u < U;
-      ws[j] = ok ? bs_bucket<NB, MINBASE, MINSUB>(v[j], (uint32_t)u, ush, smin, delta, b0, bsh)
-                 : 0u;
-      old[j] = atomicAdd(&bkw[ws[j] >> 1], ok ? 1u << ((ws[j] & 1u) * 16u) : 0u);
-    }
-    // a bucket above kJsBucketMax items <=> some item arrived at index >= kJsBucketMax
-    bool bigl = false;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const uint32_t at = (old[j] >> ((ws[j] & 1u) * 16u)) & 0xFFFFu;
-      bigl |= at >= (uint32_t)kJsBucketMax;
-      ws[j] |= at << 16;
-    }
-    {
-      const bool wbig = ballot(bigl) != 0ull;
-      if (lane == 0) s_wmax[wid] = wbig ? 1u : 0u;
-    }
-    QF_STAMP(10);
-    __syncthreads();
-    QF_STAMP(11);
-    bool anybig = false;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) anybig |= s_wmax[w] != 0u;
-    return anybig ? 1 : 0;
-  };
-  int cs = count(QF_BS_DELTA_SHIFT);
-  if (cs == 1) {  // uniform: every wave has read the flags; zero the counters, recount
-    __syncthreads();
-    for (int i = tid * 4; i < NB / 2 + 8; i += BLOCK * 4)
-      *(uint4*)&bkw[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    cs = count(QF_BS_RETRY_SHIFT);
-  }
-  if (cs < 0) {  // uniform
-    if (tid == 0) outp[0] = kJsUnsorted;
-    return;
-  }
-  const bool big = cs != 0;
-  // ---- 2. exclusive scan of the counters ---------------------------------------------
-  {
-    constexpr int kPer = NB / BLOCK;  // u16 counters per thread
-    static_assert(kPer % 8 == 0 || kPer == 4, "uint4 / uint2 counter loads");
-    uint32_t c[kPer], tot = 0u;
-#pragma unroll
-    for (int i = 0; i < kPer; i += 2) {
-      const uint32_t x = bkw[(tid * kPer + i) / 2];
-      c[i] = x & 0xFFFFu;
-      c[i + 1] = x >> 16;
-    }
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const uint32_t x = c[i];
-      c[i] = tot;
-      tot += x;
-    }
-    const uint32_t incl = wave_incl_scan_dpp(tot);
-    if (lane == 63) s_wtot[wid] = incl;
-    __syncthreads();
-    uint32_t pre = incl - tot;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w)
-      if (w < wid) pre += s_wtot[w];
-#pragma unroll
-    for (int i = 0; i < kPer; i += 2)
-      bkw[(tid * kPer + i) / 2] = (pre + c[i]) | ((pre + c[i + 1]) << 16);
-    if (tid == 0) bkw[NB / 2] = (uint32_t)U;
-  }
-  __syncthreads();
-  QF_STAMP(12);
-  if (big) {  // uniform
-    if (tid == 0) outp[0] = kJsUnsorted;
-    return;
-  }
-  // ---- 3. scatter --------------------------------------------------------------------
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int u = (wid * rows + j) * 64 + lane;
-    if (j < rows && u < U) {
-      const uint32_t pos = bk[ws[j] & 0xFFFFu] + (ws[j] >> 16);
-      sval[pos] = v[j];
-      su[pos] = (uint16_t)u;
-    }
-  }
-  __syncthreads();
-  QF_STAMP(13);
-  // ---- 4. rank inside the bucket, in position order --------------------------------------
-  // (positions follow the bucket order, so the outputs below land nearly in
-  // place: a wave's stores cover a few lines instead of 64 scattered ones.
-  // Every row's position before any global store: a store in flight would make
-  // the next row's loop wait for it.)
-  uint32_t P[ROWS], uo[ROWS];
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int i = (wid * rows + j) * 64 + lane;
-    P[j] = 0u;
-    uo[j] = 0u;
-    if (j < rows && i < U) {
-      const double vi = sval[i];
-      const uint32_t ui = su[i];
-      const uint32_t w = bs_bucket<NB, MINBASE, MINSUB>(vi, ui, ush, smin, delta, b0, bsh);
-      const uint32_t lo = bk[w], hi = bk[w + 1];
-      uint32_t before = 0u;
-      uint32_t k = hi - lo > 1u ? lo : hi;  // a bucket of one: nothing to count
-      for (; k + 1 < hi; k += 2) {
-        const double v0 = sval[k], v1 = sval[k + 1];
-        const uint32_t u0 = su[k], u1 = su[k + 1];
-        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui))) +
-                  (uint32_t)((v1 > vi) | ((v1 == vi) & (u1 < ui)));
-      }
-      if (k < hi) {
-        const double v0 = sval[k];
-        const uint32_t u0 = su[k];
-        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (u0 < ui)));
-      }
-      P[j] = lo + before;
-      uo[j] = ui;
-    }
-  }
-  QF_STAMP(2);
-  // ---- 5. outputs ------------------------------------------------------------------------
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int i = (wid * rows + j) * 64 + lane;
-    if (j < rows && i < U) {
-      __builtin_nontemporal_store((uint16_t)uo[j], &outp[P[j]]);
-    }
-  }
-  QF_STAMP(15);
-}
 
 // ============================================================================
-// bsort_kernel — the bucket sort of bucket_sort_kernel with its instruction count
-// cut (it is VALU-issue-bound: ~128 wave-instructions per 64 items there):
-//  * the key is one f64 add and an integer shift: x = v + c (c = delta - smin,
-//    when smin + c >= delta / 2; else (v - smin) + delta), and the high word of x's
-//    bits (x > 0: its bits ascend with x) shifted right — no f64 -> f32 convert;
-//    every step is monotone, so the bucket is non-increasing in v;
-//  * u32 bucket counters (one atomic add, its return value the arrival index),
-//    overlaid on the scores' LDS, which is free until the scatter;
-//  * the scatter keeps each item's (arrival index, bucket size) and stores them by
-//    position, so the rank phase reads lo / hi instead of recomputing the key and
-//    reading the starts.
-// Same order (score descending, ties in first-seen u order), same protocol
-// (perm[0] = kJsUnsorted for the fallback pass).
-// LDS: region A 24 KB (range partials [0, 8 KB) + counters [8 KB, 24 KB); then the
-// scores by position), region B 6 KB (u by position), region C 8 KB (bucket
-// starts; then (arrival, size) by position).  38.9 KB: 4 workgroups per CU.
+// bsort_kernel — the default path's sort: the bucket sort above, one workgroup
+// (512 threads) per (query, method slot) with U <= kJsUMax, at a low VALU count
+// (the kernel is VALU-issue-bound):
+//  * the key is one f64 add and a multiply-high: x = v + c (c = delta - smin,
+//    when smin + c >= delta / 2; else (v - smin) + delta), the high word of x's
+//    bits (x > 0: its bits ascend with x) scaled over the MINBASE buckets — every
+//    step monotone, so the bucket is non-increasing in v; the minimum score
+//    (shared by hundreds of documents when a run has weight 0) takes MINSUB
+//    sub-buckets split by u;
+//  * u32 bucket counters overlaid on the scores' LDS, which is free until the
+//    scatter;
+//  * the scatter keeps each item's (u, bucket size, arrival index) and stores
+//    them as one u32 word by position, so the rank phase reads lo / hi and the
+//    tie key with one read.
+// Same order (score descending, ties in first-seen u order); a pair it cannot
+// order gets perm[0] = kJsUnsorted for the fallback pass.
+// LDS: the scores by position (24 KB; before the scatter the range partials and
+// the counters), then 14 KB for the bucket starts and, from the scatter on, the
+// words by position.  38.2 KB: 4 workgroups per CU.
 // ============================================================================
 // Raw v_min_f64 / v_max_f64, without fmin / fmax's NaN canonicalisation (three
 // more instructions per call): the callers flag NaNs themselves and discard the
@@ -2019,9 +1375,6 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   constexpr int WAVES = BLOCK / 64, ROWS = (kJsUMax + BLOCK - 1) / BLOCK, NB = 1 << BITS;
   constexpr int MINSUB = NB / 16, MINBASE = NB - MINSUB;
   static_assert(2 * BLOCK * 8 + 4 * NB <= 8 * kJsUMax, "partials + counters overlay the scores");
-  static_assert(2 * kJsUMax <= 2 * NB, "(arrival, size) by position overlays the starts");
-  // regions A (scores by position) and B (u by position) in one array: the spare
-  // counter cnt[NB] lies at the start of B
   // One LDS array: region A = the scores by position (f64 [kJsUMax]; until the
   // scatter: the range partials [0, 8 KB) and the u32 counters [8 KB, 24 KB));
   // region BC after it = the u | size | arrival words by position (u32 [kJsUMax],
@@ -2070,7 +1423,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   const int64_t base = p.list_off[q * p.R];
   if (U < 1 || U > kJsUMax) return;  // error / fuse_large_kernel's
   double* io = p.fused + (int64_t)ms * p.out_stride + base;
-  uint16_t* outp = p.perm + (int64_t)ms * p.out_stride + base;
+  const int64_t po = (int64_t)ms * p.out_stride + base;  // perm of this pair
   const int rows = (U + BLOCK - 1) / BLOCK;
   const int wbase = wid * rows * 64;  // this wave's items: [wbase, wbase + rows * 64)
   double v[ROWS];
@@ -2162,15 +1515,11 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
       const int u = wbase + j * 64 + lane;
-      if (j < rows && u < U) __builtin_nontemporal_store((uint16_t)u, &outp[u]);
+      if (j < rows && u < U) perm_put(p, po + u, (uint32_t)u);
     }
     return;
   }
   const double smax = s_mx, smin = s_mn;
-#if defined(QF_BS_STOP) && QF_BS_STOP == 1
-  if (smin == 12345.0) outp[0] = 0;
-  return;
-#endif
   int ush = 0;  // U - 1 >> ush < MINSUB
   while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
   const uint32_t dmin = BYDOC ? s_dmn : 0u;
@@ -2244,13 +1593,9 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     cs = count(bs_key_params<MINBASE, BYDOC>(smin, smax, nan, QF_BS_RETRY_SHIFT));
   }
   if (cs != 0) {  // uniform: a range the key cannot take, or a bucket still too big
-    if (tid == 0) outp[0] = kJsUnsorted;
+    if (tid == 0) perm_put(p, po, kJsUnsorted);
     return;
   }
-#if defined(QF_BS_STOP) && QF_BS_STOP == 2
-  if (ws[0] == 12345u) outp[0] = 0;
-  return;
-#endif
   // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
   {
     constexpr int kPer = NB / BLOCK;  // counters per thread
@@ -2277,10 +1622,6 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     if (tid == 0) bk[NB] = (uint16_t)U;
   }
   __syncthreads();
-#if defined(QF_BS_STOP) && QF_BS_STOP == 3
-  if (bk[tid] == 12345u) outp[0] = 0;
-  return;
-#endif
   // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
   uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
 #pragma unroll
@@ -2303,10 +1644,6 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     if (j < rows && u < U) sw[pa[j]] = pw[j];
   }
   __syncthreads();
-#if defined(QF_BS_STOP) && QF_BS_STOP == 4
-  if (bk[tid] == 12345u) outp[0] = 0;
-  return;
-#endif
   // ---- rank inside the bucket, in position order --------------------------------------
   uint32_t P[ROWS], uo[ROWS];
 #pragma unroll
@@ -2333,9 +1670,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
         // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the
         // compiler would merge them into (8 cycles: it serves 16 lanes at a time)
         const double v0 = pv[0];
-#ifndef QF_BS_READ2
         asm volatile("" ::: "memory");
-#endif
         const double v1 = pv[1];
         const uint32_t t0 = tp[0], t1 = tp[1];
         before += (uint32_t)((v0 > vi) | ((v0 == vi) & (t0 < ti))) +
@@ -2351,17 +1686,10 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     }
   }
   // ---- outputs (every row's position before any store) ----------------------------------
-#if defined(QF_BS_STOP) && QF_BS_STOP == 5
-  uint32_t acc = 0u;
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) acc += P[j] ^ uo[j];
-  if (acc == 12345u) outp[0] = 0;
-  return;
-#endif
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int i = wbase + j * 64 + lane;
-    if (j < rows && i < U) __builtin_nontemporal_store((uint16_t)uo[j], &outp[P[j]]);
+    if (j < rows && i < U) perm_put(p, po + P[j], uo[j]);
   }
 }
 
@@ -2379,10 +1707,16 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 //      as the LDS join, bit for bit;
 //   4. unions of up to 10,240 documents are left unsorted, with their U, to the
 //      LDS sort kernels launched after this one; larger ones get, per method
-//      slot, a bitonic sort of (key = ~orderable(score), tie = u — or docid for
-//      learned fusion) — unique pairs, so the order equals the stable sort of
-//      the LDS path: passes with stride >= kXlTile run in the workspace, the rest
-//      on kXlTile-item tiles in LDS.
+//      slot, the bucket sort of bsort_kernel over the workspace (xl_bsort:
+//      16,384 buckets counted in LDS, scores and tie words scattered to the
+//      workspace by bucket, each item ranked inside its bucket).  A slot it
+//      cannot order (a bucket above kXlBucketMax after the finer recount, a
+//      non-finite range, a NaN) takes a bitonic sort of (key = ~orderable(score),
+//      tie = u — or docid for learned fusion) — unique pairs, so the order equals
+//      the stable sort of the LDS path: passes with stride >= kXlTile run in the
+//      workspace, the rest on kXlTile-item tiles in LDS.
+// u and every entry index are 32-bit: up to kXlNMaxWide entries per query with
+// qf_fuse_wide's uint32 perm (kXlNMax with qf_fuse's uint16 perm).
 // A persistent grid of G <= 512 workgroups (two per CU) lists the large queries of each strided
 // chunk (one parallel load of their sizes) and runs them in turn, so batches
 // without large queries cost one short launch — and fuse_launch only makes it
@@ -2390,16 +1724,21 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 // ============================================================================
 constexpr int kXlBlock = 1024;
 constexpr int kXlTile = 4096;  // bitonic items per LDS tile (64 KB of keys + ties)
-constexpr int kXlNMax = 65535; // perm entries and u are uint16
-constexpr int kXlGrid = 512;   // workgroups: two per CU (74 KB of LDS each) while the
-                               // workspace stays within 1 GB, else one per CU
+constexpr int kXlNMax = 65535;  // entries per query with a uint16 perm
+constexpr int kXlNMaxWide = (1 << 24) - 1;  // with a uint32 perm (grouped entries: e | r << 27)
+constexpr int kXlGrid = 512;   // workgroups: two per CU (75 KB of LDS each)
 
 struct XlWs {
   uint32_t *tkey, *tmask, *tu;           // [TS] hash table
   uint32_t *eslot, *umask, *ugo, *gent;  // [NMAX] entry slot, document masks / group
-                                         // starts, grouped entries (e | r << 16)
-  uint64_t *skey, *stie;                 // [P] sort keys and ties
-  double* sval;                          // [P] unsorted scores (their sign kept)
+                                         // starts, grouped entries (e | r << 27)
+  uint64_t *skey, *stie;                 // [P] sort keys and ties (bitonic)
+  double* sval;                          // [P] unsorted scores (bitonic); scores by
+                                         // position (bucket sort)
+  // the bucket sort's views of skey / stie: tie | size | arrival by position,
+  // bucket | arrival by u, u by position (learned fusion)
+  uint64_t* sw;
+  uint32_t *sarr, *su;
 };
 static __host__ __device__ inline int64_t xl_ws_bytes(int ts, int nmax, int np) {
   const int64_t a = 12 * (int64_t)ts + 16 * (int64_t)nmax + 24 * (int64_t)np;
@@ -2413,6 +1752,9 @@ __device__ __forceinline__ XlWs xl_ws(unsigned char* b, int ts, int nmax, int np
   w.eslot = e; w.umask = e + nmax; w.ugo = e + 2 * nmax; w.gent = e + 3 * nmax;
   uint64_t* k = (uint64_t*)(((uintptr_t)(e + 4 * nmax) + 7) & ~(uintptr_t)7);
   w.skey = k; w.stie = k + np; w.sval = (double*)(k + 2 * np);
+  w.sw = w.skey;
+  w.sarr = (uint32_t*)w.stie;
+  w.su = w.sarr + np;
   return w;
 }
 
@@ -2489,11 +1831,169 @@ __device__ __forceinline__ void xl_tile_pass(uint64_t* __restrict__ gkey,
   }
 }
 
+// ---- the workspace bucket sort of one (query, method slot) --------------------------
+// bsort_kernel's algorithm with its per-item arrays in the workspace: 16,384
+// u32 bucket counters in LDS (over the bitonic tiles), minimum's sub-buckets by u
+// (BYDOC: by docid), a bucket above kXlBucketMax recounted once at the finer
+// delta.  Returns false, perm untouched, for the bitonic fallback.
+constexpr int kXlBits = 14, kXlNB = 1 << kXlBits;
+constexpr int kXlMinSub = kXlNB / 16, kXlMinBase = kXlNB - kXlMinSub;
+constexpr int kXlBucketMax = 256;
+// delta = range / 2^10: four times bsort_kernel's buckets, two more binades
+constexpr int kXlDeltaShift = 10;
+struct XlScratch {  // the bucket sort's block reductions
+  double mn[kXlBlock / 64], mx[kXlBlock / 64];
+  uint32_t dmn[kXlBlock / 64], dmx[kXlBlock / 64];
+  int flag[kXlBlock / 64];
+};
+
+template <bool BYDOC>
+__device__ bool xl_bsort(const FuseParams& p, const double* __restrict__ io, int64_t base, int U,
+                         int64_t po, const XlWs& w, uint32_t* cnt, uint32_t* s_wsum,
+                         XlScratch* xs) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int WAVES = kXlBlock / 64;
+  // ---- score (and docid) range ---------------------------------------------------------
+  double mn = INFINITY, mx = -INFINITY;
+  uint32_t dmn = ~0u, dmx = 0u;
+  int nan = 0;
+  for (int u = tid; u < U; u += kXlBlock) {
+    const double v = io[u];
+    mn = raw_min_f64(mn, v);
+    mx = raw_max_f64(mx, v);
+    nan |= v != v;
+    if (BYDOC) {
+      const uint32_t d = p.union_docid[base + u];
+      dmn = min(dmn, d);
+      dmx = max(dmx, d);
+    }
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  nan = ballot(nan != 0) != 0ull;
+  if (BYDOC) {
+    dmn = (uint32_t)wave_min_u64_dpp(dmn);
+    dmx = (uint32_t)wave_max_u64_dpp(dmx);
+  }
+  if (lane == 63) {
+    xs->mn[wid] = mn;
+    xs->mx[wid] = mx;
+    xs->dmn[wid] = dmn;
+    xs->dmx[wid] = dmx;
+    xs->flag[wid] = nan;
+  }
+  __syncthreads();
+  for (int i = 0; i < WAVES; ++i) {
+    mn = fmin(mn, xs->mn[i]);
+    mx = fmax(mx, xs->mx[i]);
+    dmn = min(dmn, xs->dmn[i]);
+    dmx = max(dmx, xs->dmx[i]);
+    nan |= xs->flag[i];
+  }
+  __syncthreads();  // xs is reused below
+  // the folded extremes (-0.0 == +0.0)
+  const double smin = f64_from_asc_key(f64_asc_key(mn)), smax = f64_from_asc_key(f64_asc_key(mx));
+  if (!BYDOC && !nan && smin == smax) {  // every score equal: first-seen order
+    for (int u = tid; u < U; u += kXlBlock) perm_put(p, po + u, (uint32_t)u);
+    return true;
+  }
+  int ush = 0, dsh = 0;  // minimum's sub-bucket: u >> ush (BYDOC: d - dmin >> dsh)
+  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)kXlMinSub) ++ush;
+  if (BYDOC)
+    while (((dmx - dmn) >> dsh) >= (uint32_t)kXlMinSub) ++dsh;
+  // ---- count: one LDS atomic per item; bucket | arrival << 16 by u ------------------------
+  auto count = [&](const BsKey& kp) -> int {
+    for (int i = tid; i <= kXlNB; i += kXlBlock) cnt[i] = 0u;
+    __syncthreads();
+    if (!kp.ok) return -1;  // uniform
+    int big = 0;
+    for (int u = tid; u < U; u += kXlBlock) {
+      const double v = io[u];
+      const double x = kp.cform ? v + kp.c : (v - smin) + kp.delta;
+      const uint32_t hx = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
+      const uint32_t key = __umulhi(hx - kp.b0, kp.scale);  // < kXlMinBase
+      uint32_t b;
+      if (v == smin)
+        b = (uint32_t)kXlMinBase +
+            (BYDOC ? (p.union_docid[base + u] - dmn) >> dsh : (uint32_t)u >> ush);
+      else
+        b = (uint32_t)(kXlMinBase - 1) - key;
+      const uint32_t at = atomicAdd(&cnt[b], 1u);
+      big |= at >= (uint32_t)kXlBucketMax;
+      w.sarr[u] = b | (min(at, 0xFFFFu) << 16);
+    }
+    const bool wbig = ballot(big != 0) != 0ull;
+    if (lane == 0) xs->flag[wid] = wbig ? 1 : 0;
+    __syncthreads();
+    int any = 0;
+    for (int i = 0; i < WAVES; ++i) any |= xs->flag[i];
+    __syncthreads();  // the flags are read before the next count writes them
+    return any;
+  };
+  int cs = count(bs_key_params<kXlMinBase, BYDOC>(smin, smax, nan, kXlDeltaShift));
+  if (cs == 1) cs = count(bs_key_params<kXlMinBase, BYDOC>(smin, smax, nan, QF_BS_RETRY_SHIFT));
+  if (cs != 0) return false;  // uniform
+  // ---- exclusive scan of the counters, in place; cnt[kXlNB] = U ----------------------------
+  {
+    constexpr int kPer = kXlNB / kXlBlock;
+    static_assert(kPer == 16, "four uint4 counter loads per thread");
+    const uint4* c4 = (const uint4*)cnt + tid * 4;
+    uint32_t c[kPer];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 x = c4[i];
+      c[4 * i] = x.x; c[4 * i + 1] = x.y; c[4 * i + 2] = x.z; c[4 * i + 3] = x.w;
+    }
+    uint32_t tot = 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t x = c[i];
+      c[i] = tot;
+      tot += x;
+    }
+    uint32_t all;
+    const uint32_t pre = xl_scan(tot, s_wsum, &all);  // barriers: every counter read first
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) cnt[tid * kPer + i] = pre + c[i];
+    if (tid == 0) cnt[kXlNB] = (uint32_t)U;
+  }
+  __syncthreads();
+  // ---- scatter: score and tie | size | arrival by position ---------------------------------
+  for (int u = tid; u < U; u += kXlBlock) {
+    const uint32_t a = w.sarr[u], b = a & 0xFFFFu, at = a >> 16;
+    const uint32_t st = cnt[b], nx = cnt[b + 1];
+    const uint32_t pos = st + at;
+    const uint32_t tie = BYDOC ? p.union_docid[base + u] : (uint32_t)u;
+    w.sval[pos] = io[u];
+    w.sw[pos] = ((uint64_t)tie << 32) | ((nx - st) << 16) | at;
+    if (BYDOC) w.su[pos] = (uint32_t)u;
+  }
+  xl_sync();
+  // ---- rank inside the bucket: (score descending, tie ascending) ----------------------------
+  const uint32_t* tw = (const uint32_t*)w.sw;  // the tie: the high word of sw[k]
+  for (int i = tid; i < U; i += kXlBlock) {
+    const double vi = w.sval[i];
+    const uint64_t wi = w.sw[i];
+    const uint32_t at = (uint32_t)wi & 0xFFFFu, sz = ((uint32_t)wi >> 16) & 0xFFFFu;
+    const uint32_t ti = (uint32_t)(wi >> 32);
+    const uint32_t lo = (uint32_t)i - at;
+    uint32_t before = 0u;
+    for (uint32_t k = lo; k < lo + sz; ++k) {
+      const double vk = w.sval[k];
+      const uint32_t tk = tw[2 * k + 1];
+      before += (uint32_t)((vk > vi) | ((vk == vi) & (tk < ti)));
+    }
+    perm_put(p, po + lo + before, BYDOC ? w.su[i] : ti);
+  }
+  xl_sync();  // the workspace is the next slot's
+  return true;
+}
+
 template <int KIND>
 __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlWs& w, int tb, int pb,
                        int sort_min, int64_t* s_off, double* s_w, double* s_min, double* s_den,
                        double* s_rden, uint32_t* s_wsum, int* s_status, uint64_t* t_key,
-                       uint64_t* t_tie) {
+                       uint64_t* t_tie, XlScratch* xs) {
   const int tid = threadIdx.x;
   const int R = p.R, TS = 1 << tb;
   QF_STAMP_INIT();
@@ -2593,7 +2093,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     while (base + e >= s_off[r + 1]) ++r;
     const uint32_t u = w.tu[w.eslot[e]];
     const uint32_t k = w.ugo[u] + (uint32_t)__popc(w.umask[u] & ((1u << r) - 1u));
-    w.gent[k] = (uint32_t)e | ((uint32_t)r << 16);
+    w.gent[k] = (uint32_t)e | ((uint32_t)r << 27);
   }
   xl_sync();
   QF_STAMP(4);
@@ -2604,7 +2104,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     DocSums acc;
     for (int k = gs; k < ge; ++k) {
       const uint32_t v = w.gent[k];
-      const int e = (int)(v & 0xFFFFu), rr = (int)(v >> 16);
+      const int e = (int)(v & 0x7FFFFFFu), rr = (int)(v >> 27);
       acc.add(p, methods, lc, ScoreIn<KIND>::load(p.score, base + e), rr,
               (int)(base + e - s_off[rr]));
     }
@@ -2623,14 +2123,19 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   for (int ms = 0; ms < M; ++ms) {
     const bool by_docid = slot_method(methods, ms) == 6;
     double* io = p.fused + (int64_t)ms * p.out_stride + base;
-    uint16_t* pm = p.perm + (int64_t)ms * p.out_stride + base;
+    const int64_t po = (int64_t)ms * p.out_stride + base;
+    const bool done = by_docid
+                          ? xl_bsort<true>(p, io, base, (int)U, po, w, (uint32_t*)t_key, s_wsum, xs)
+                          : xl_bsort<false>(p, io, base, (int)U, po, w, (uint32_t*)t_key, s_wsum, xs);
+    QF_STAMP(10);
+    if (done) continue;  // uniform
     for (int i = tid; i < NP; i += kXlBlock) {
       uint64_t k = ~0ull, t = ~0ull;  // padding sorts last
       if (i < (int)U) {
         const double v = io[i];
         w.sval[i] = v;
         k = ~f64_asc_key(v);
-        t = by_docid ? ((uint64_t)p.union_docid[base + i] << 16) | (uint64_t)i : (uint64_t)i;
+        t = by_docid ? ((uint64_t)p.union_docid[base + i] << 32) | (uint64_t)i : (uint64_t)i;
       }
       w.skey[i] = k;
       w.stie[i] = t;
@@ -2653,8 +2158,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     }
     QF_STAMP(8);
     for (int i = tid; i < (int)U; i += kXlBlock) {
-      const uint32_t u = (uint32_t)(w.stie[i] & 0xFFFFu);
-      pm[i] = (uint16_t)u;
+      perm_put(p, po + i, (uint32_t)(w.stie[i] & 0xFFFFFFFFu));
     }
     xl_sync();
     QF_STAMP(9);
@@ -2673,7 +2177,12 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
   __shared__ uint32_t s_wsum[kXlBlock / 64];
   __shared__ int s_status, s_n;
   __shared__ int64_t s_list[kXlBlock];
-  __shared__ uint64_t t_key[kXlTile], t_tie[kXlTile];
+  // the bitonic tiles (keys, ties), or the bucket sort's kXlNB + 1 counters
+  __shared__ uint64_t t_buf[2 * kXlTile + 2];
+  static_assert(8 * (2 * kXlTile + 2) >= 4 * (kXlNB + 1), "counters overlay the tiles");
+  uint64_t* t_key = t_buf;
+  uint64_t* t_tie = t_buf + kXlTile;
+  __shared__ XlScratch xs;
   const int tid = threadIdx.x;
   const XlWs w = xl_ws(ws + (int64_t)blockIdx.x * ws_each, 1 << tb, nmax, 1 << pb);
   const int64_t span = (int64_t)gridDim.x * kXlBlock;
@@ -2690,7 +2199,7 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
     const int n = s_n;
     for (int t = 0; t < n; ++t)
       xl_one<KIND>(p, s_list[t], w, tb, pb, sort_min, s_off, s_w, s_min, s_den, s_rden,
-                   s_wsum, &s_status, t_key, t_tie);
+                   s_wsum, &s_status, t_key, t_tie, &xs);
     __syncthreads();
   }
 }
@@ -2705,7 +2214,7 @@ using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
 using SortXL = SortCfg<1024, 10, 2>;  // U <= 10240
 
-int fuse_max_entries() { return kXlNMax; }
+int fuse_max_entries(int wide) { return wide ? kXlNMaxWide : kXlNMax; }
 
 template <class J>
 static void launch_join(const FuseParams& p, int kind, hipStream_t st) {
@@ -2739,10 +2248,13 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
   int tb = 1, pb = 0;
   while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
   while ((1 << pb) < max_entries) ++pb;
-  const int nmax = max_entries < kXlNMax ? max_entries : kXlNMax;
+  const int cap = p.perm32 ? kXlNMaxWide : kXlNMax;
+  const int nmax = max_entries < cap ? max_entries : cap;
   const int64_t each = xl_ws_bytes(1 << tb, nmax, 1 << pb);
-  int64_t g = ((int64_t)1 << 30) / each;
-  g = g < kXlGrid / 2 ? kXlGrid / 2 : (g > kXlGrid ? kXlGrid : g);
+  // workgroups: two per CU while the workspace stays within 4 GB (1.4 % of HBM);
+  // very large queries get fewer (each workgroup runs its queries in turn)
+  int64_t g = ((int64_t)4 << 30) / each;
+  g = g < 1 ? 1 : (g > kXlGrid ? kXlGrid : g);
   if (p.n_queries < g) g = p.n_queries;
   hipError_t e = hipMallocAsync(ws_out, (size_t)(each * g), st);
   if (e != hipSuccess) return e;
@@ -2756,52 +2268,24 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
   return hipGetLastError();
 }
 
-// Blocks per query of the fused join + sort (development switch: QF_JS_BLOCK=0
-// turns it off, 512 / 1024 pick the workgroup size).
-static int js_block() {
-  static const int b = [] {
-    const char* e = std::getenv("QF_JS_BLOCK");
-    return e ? std::atoi(e) : 14;
-  }();
-  return b;
-}
-
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
   void* ws = nullptr;
   hipError_t e = hipSuccess;
-  const int jsb = js_block();
-  if (((jsb == 11 || jsb == 12 || jsb == 13) && !(p.methods & QF_LEARNED) || jsb == 14) &&
-      p.R <= kRMax && max_entries <= JoinXL::kNMax && max_entries > JoinS::kNMax) {
+  if (p.R <= kRMax && max_entries <= JoinXL::kNMax && max_entries > JoinS::kNMax) {
     // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
     if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
     else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
     else launch_join<JoinXL>(p, kind, st);
     const int M = __builtin_popcount((unsigned)p.methods);
-    const dim3 g = grid_for((p.n_queries + 7) / 8 * 8 * M);
-    if (jsb == 14) {
-      if (p.methods & ~QF_LEARNED)
-        hipLaunchKernelGGL((bsort_kernel<512, 12, false>), g, dim3(512), 0, st, p);
-      if (p.methods & QF_LEARNED)
-        hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),
-                           dim3(512), 0, st, p);
-    }
-    else if (jsb == 11) hipLaunchKernelGGL((bucket_sort_kernel<512, 11>), g, dim3(512), 0, st, p);
-    else if (jsb == 12) hipLaunchKernelGGL((bucket_sort_kernel<512, 12>), g, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((bucket_sort_kernel<512, 13>), g, dim3(512), 0, st, p);
+    if (p.methods & ~QF_LEARNED)
+      hipLaunchKernelGGL((bsort_kernel<512, 12, false>), grid_for((p.n_queries + 7) / 8 * 8 * M),
+                         dim3(512), 0, st, p);
+    if (p.methods & QF_LEARNED)
+      hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),
+                         dim3(512), 0, st, p);
     // unions above kJsUMax and the pairs the bucket sort marked: one pass
     launch_sort_large<SortL, true>(p, kJsUMax + 1, st, 1);
     if (max_entries > SortL::kUMax) launch_sort_large<SortXL>(p, SortL::kUMax + 1, st, 1);
-    return hipGetLastError();
-  }
-  if (kind == 1 && p.R <= kRMax && max_entries <= 5120 && max_entries > JoinS::kNMax &&
-      (p.methods & ~kJsMethods) == 0 && (jsb == 512 || jsb == 1024)) {
-    // one kernel: join + sums + sorts in LDS; unions above kJsUMax (stored unsorted)
-    // are sorted by fuse_large_kernel, which costs a few microseconds when none exist
-    if (jsb == 512)
-      hipLaunchKernelGGL((join_sort_kernel<512>), grid_for(p.n_queries), dim3(512), 0, st, p);
-    else
-      hipLaunchKernelGGL((join_sort_kernel<1024>), grid_for(p.n_queries), dim3(1024), 0, st, p);
-    launch_sort_large<SortL, true>(p, kJsUMax + 1, st, 1);
     return hipGetLastError();
   }
   if (p.R > kRMax) {
@@ -2841,7 +2325,7 @@ __global__ __launch_bounds__(256) void topk_kernel(int64_t n_queries, int32_t R,
                                                    const int64_t* __restrict__ list_off,
                                                    const int32_t* __restrict__ union_count,
                                                    const uint32_t* __restrict__ union_docid,
-                                                   const uint16_t* __restrict__ perm,
+                                                   const void* __restrict__ perm, int perm32,
                                                    const double* __restrict__ fused,
                                                    int64_t out_stride, int32_t M, int32_t k,
                                                    uint32_t* __restrict__ out_docid,
@@ -2854,14 +2338,15 @@ __global__ __launch_bounds__(256) void topk_kernel(int64_t n_queries, int32_t R,
   const int64_t base = list_off[q * R];
   const int uc = union_count[q];
   const int n = uc < 0 ? 0 : (uc < k ? uc : k);
-  const uint16_t* pm = perm + (int64_t)m * out_stride + base;
-  const double* fz = fused + (int64_t)m * out_stride + base;
+  const int64_t po = (int64_t)m * out_stride + base;
+  const double* fz = fused + po;
   for (int i = lane; i < k; i += 64) {
     uint32_t d = 0xFFFFFFFFu;
     double sc = __longlong_as_double(0x7FF8000000000000ll);
     if (i < n) {
-      d = union_docid[base + pm[i]];
-      sc = fz[pm[i]];  // scores by u, ranked through perm
+      const uint32_t u = perm32 ? ((const uint32_t*)perm)[po + i] : ((const uint16_t*)perm)[po + i];
+      d = union_docid[base + u];
+      sc = fz[u];  // scores by u, ranked through perm
     }
     out_docid[row * k + i] = d;
     out_score[row * k + i] = sc;
@@ -2870,12 +2355,13 @@ __global__ __launch_bounds__(256) void topk_kernel(int64_t n_queries, int32_t R,
 
 hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
                        const int32_t* union_count, const uint32_t* union_docid,
-                       const uint16_t* perm, const double* fused, int64_t out_stride, int32_t M,
-                       int32_t k, uint32_t* out_docid, double* out_score, hipStream_t st) {
+                       const void* perm, int perm32, const double* fused, int64_t out_stride,
+                       int32_t M, int32_t k, uint32_t* out_docid, double* out_score,
+                       hipStream_t st) {
   const int64_t rows = n_queries * M;
   if (rows == 0 || k == 0) return hipSuccess;
   hipLaunchKernelGGL(topk_kernel, grid_for((rows + 3) / 4), dim3(256), 0, st, n_queries,
-                     R, list_off, union_count, union_docid, perm, fused, out_stride, M, k,
+                     R, list_off, union_count, union_docid, perm, perm32, fused, out_stride, M, k,
                      out_docid, out_score);
   return hipGetLastError();
 }

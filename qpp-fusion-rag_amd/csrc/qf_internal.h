@@ -28,7 +28,7 @@ struct FuseParams {
   int32_t rrf_k;
   uint32_t* union_docid;
   int32_t* union_count;
-  uint16_t* perm;
+  void* perm;      // uint16 [M][E], or uint32 when perm32 (qf_fuse_wide)
   double* fused;
   int64_t out_stride;
   const double* seg_prob;  // QF_PROBFUSE: [R][n_seg] segment probabilities
@@ -37,7 +37,17 @@ struct FuseParams {
   // run r's products are float32; learned_sum_f32 = the groupby sum is float32 Kahan
   uint32_t learned_f32;
   int32_t learned_sum_f32;
+  int32_t perm32;  // perm holds uint32 entries (unions above 65,535 documents)
 };
+// perm element i (m * out_stride + base + rank): every kernel writes perm through
+// these, so one flag switches a call between the uint16 and uint32 layouts
+__device__ __forceinline__ void perm_put(const FuseParams& p, int64_t i, uint32_t u) {
+  if (p.perm32) __builtin_nontemporal_store(u, (uint32_t*)p.perm + i);
+  else __builtin_nontemporal_store((uint16_t)u, (uint16_t*)p.perm + i);
+}
+__device__ __forceinline__ uint32_t perm_get(const FuseParams& p, int64_t i) {
+  return p.perm32 ? ((const uint32_t*)p.perm)[i] : ((const uint16_t*)p.perm)[i];
+}
 
 // IR evaluation (qf_eval): run m, query q reads its ranked list at
 // [q_base[q*base_stride], + q_count[q] (or up to the next base)) of score /
@@ -115,13 +125,14 @@ struct MlpParams {
 };
 hipError_t mlp_weights_launch(const MlpParams& p, hipStream_t st);
 
-int fuse_max_entries();
+int fuse_max_entries(int wide);
 hipError_t eval_launch(const EvalParams& p, hipStream_t st);
 hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);
 hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
                        const int32_t* union_count, const uint32_t* union_docid,
-                       const uint16_t* perm, const double* fused, int64_t out_stride, int32_t M,
-                       int32_t k, uint32_t* out_docid, double* out_score, hipStream_t st);
+                       const void* perm, int perm32, const double* fused, int64_t out_stride,
+                       int32_t M, int32_t k, uint32_t* out_docid, double* out_score,
+                       hipStream_t st);
 hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t Q, int32_t R,
                           int32_t top_k, const int32_t* nt, const double* tf, double* out,
                           hipStream_t st);

@@ -757,11 +757,15 @@ static inline size_t fmt6(double x, char* out) {
 
 size_t qfio_format_score(double x, char* out) { return fmt6(x, out); }
 
-int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
-                   const int32_t* counts, const uint32_t* union_docid, const uint16_t* perm,
-                   const double* fused, const int64_t* qid_off, const char* qid_chars,
-                   const int64_t* docno_off, const char* docno_chars, const char* tag,
-                   int32_t n_threads) {
+}  // extern "C"
+
+// write_runfile for one fused run (include/qfio.h), either perm width
+template <class Perm>
+static int write_run(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
+                     const int32_t* counts, const uint32_t* union_docid, const Perm* perm,
+                     const double* fused, const int64_t* qid_off, const char* qid_chars,
+                     const int64_t* docno_off, const char* docno_chars, const char* tag,
+                     int32_t n_threads) {
   if (!path || (n_out > 0 && (!order || !qbase || !counts || !union_docid || !perm || !fused ||
                               !qid_off || !qid_chars || !docno_off || !docno_chars || !tag)))
     return fail(QFIO_EINVAL, "qfio_write_run: bad arguments");
@@ -857,6 +861,26 @@ int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const 
   }
   if (close(fd) != 0 || werr) return fail(QFIO_EIO, std::string("short write to ") + path);
   return QFIO_OK;
+}
+
+extern "C" {
+
+int qfio_write_run(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
+                   const int32_t* counts, const uint32_t* union_docid, const uint16_t* perm,
+                   const double* fused, const int64_t* qid_off, const char* qid_chars,
+                   const int64_t* docno_off, const char* docno_chars, const char* tag,
+                   int32_t n_threads) {
+  return write_run(path, n_out, order, qbase, counts, union_docid, perm, fused, qid_off, qid_chars,
+                   docno_off, docno_chars, tag, n_threads);
+}
+
+int qfio_write_run32(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
+                     const int32_t* counts, const uint32_t* union_docid, const uint32_t* perm,
+                     const double* fused, const int64_t* qid_off, const char* qid_chars,
+                     const int64_t* docno_off, const char* docno_chars, const char* tag,
+                     int32_t n_threads) {
+  return write_run(path, n_out, order, qbase, counts, union_docid, perm, fused, qid_off, qid_chars,
+                   docno_off, docno_chars, tag, n_threads);
 }
 
 }  // extern "C"

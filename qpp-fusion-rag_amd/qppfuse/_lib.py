@@ -31,12 +31,14 @@ MAX_RUNS = 32  # qf_fuse: retriever masks are 32-bit (include/qppfuse.h)
 EVAL_NDCG, EVAL_RR, EVAL_R, EVAL_P, EVAL_AP = range(5)
 EVAL_MAX_METRICS, EVAL_MAX_QRELS = 16, 256
 
-# name -> (restype, argtypes); must match include/qppfuse.h
+# name -> (restype, argtypes); must match include/qppfuse.h (the *_wide entry points
+# take the same arguments as their narrow forms: perm is a pointer either way)
 _vp, _i32, _i64, _u64, _f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
 SIGNATURES = {
     "qf_version": (C.c_char_p, []),
     "qf_last_error": (C.c_char_p, []),
     "qf_max_entries_per_query": (C.c_int, []),
+    "qf_max_entries_per_query_wide": (C.c_int, []),
     "qf_minmax_per_query": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "qf_qpp_raw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
@@ -59,6 +61,8 @@ SIGNATURES = {
                                       _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
 }
+for _n in ("qf_fuse", "qf_fuse_probfuse", "qf_fuse_learned_f32", "qf_fused_topk"):
+    SIGNATURES[_n + "_wide"] = SIGNATURES[_n]
 
 
 class QPPFuseError(RuntimeError):
@@ -105,3 +109,7 @@ def version() -> str:
 
 def max_entries_per_query() -> int:
     return int(lib().qf_max_entries_per_query())
+
+
+def max_entries_per_query_wide() -> int:
+    return int(lib().qf_max_entries_per_query_wide())

@@ -60,11 +60,16 @@ class FuseOut:
     fused[m, b + perm[m, b + i]] (include/qppfuse.h)."""
     union_docid: torch.Tensor  # int32 view of uint32 [E]
     union_count: torch.Tensor  # int32 [Q]
-    perm: torch.Tensor         # int16 view of uint16 [M, E]
+    perm: torch.Tensor         # int16 view of uint16 [M, E] (int32 view of uint32: wide)
     fused: torch.Tensor        # float64 [M, E]
     methods: list
     list_off: Optional[torch.Tensor] = None  # the last launch's run set (ranked_fused)
     n_retrievers: int = 0
+
+    @property
+    def wide(self) -> bool:
+        """uint32 perm (qf_fuse_wide: unions above 65,535 documents)."""
+        return self.perm.dtype == torch.int32
 
     def ranked_fused(self) -> torch.Tensor:
         """[M, E] scores in rank order (rank i of a query at b + i; entries past its
@@ -81,19 +86,24 @@ class FuseOut:
         out = torch.zeros_like(self.fused)
         n = int(qoff[-1])
         for m in range(self.fused.shape[0]):
-            u = self.perm[m, :n].to(torch.int64) & 0xFFFF
+            u = self.perm[m, :n].to(torch.int64) & (0xFFFFFFFF if self.wide else 0xFFFF)
             idx = torch.where(ok, base + u, torch.zeros_like(u))
             out[m, :n] = torch.where(ok, self.fused[m].gather(0, idx),
                                      torch.zeros((), dtype=torch.float64, device=off.device))
         return out[:, :E]
 
 
-def alloc_fuse_out(n_queries: int, n_entries: int, mask: int, device) -> FuseOut:
+def needs_wide(max_entries: int) -> bool:
+    """Whether a query of max_entries entries needs the uint32 perm (qf_fuse_wide)."""
+    return int(max_entries) > _lib.max_entries_per_query()
+
+
+def alloc_fuse_out(n_queries: int, n_entries: int, mask: int, device, wide: bool = False) -> FuseOut:
     M = bin(mask).count("1")
     E = max(int(n_entries), 1)
     return FuseOut(torch.empty(E, dtype=torch.int32, device=device),
                    torch.empty(max(n_queries, 1), dtype=torch.int32, device=device),
-                   torch.empty((M, E), dtype=torch.int16, device=device),
+                   torch.empty((M, E), dtype=torch.int32 if wide else torch.int16, device=device),
                    torch.empty((M, E), dtype=torch.float64, device=device),
                    method_names(mask))
 
@@ -107,7 +117,9 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
     """qf_fuse over every query of a packed run set (see include/qppfuse.h); with
     "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table;
     methods == ["learned"] with learned_f32 (run bitmask: float32 model weights,
-    FusionMLP), qf_fuse_learned_f32."""
+    FusionMLP), qf_fuse_learned_f32.  A query above qf_max_entries_per_query()
+    (65,535) entries takes the _wide entry points (uint32 perm): `out` is then
+    allocated wide (alloc_fuse_out(..., wide=True))."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
@@ -121,13 +133,19 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
         raise TypeError("score must be float64 or int32 micro-units")
     if max_entries is None:
         raise ValueError("max_entries (largest per-query entry count) is required")
+    wide = needs_wide(max_entries)
     if out is None:
-        out = alloc_fuse_out(Q, E, mask, dev)
+        out = alloc_fuse_out(Q, E, mask, dev, wide=wide)
+    elif wide and not out.wide:
+        raise ValueError(f"max_entries {max_entries} needs a uint32 perm: "
+                         "alloc_fuse_out(..., wide=True)")
+    wide = out.wide
+    sfx = "_wide" if wide else ""
     out.list_off, out.n_retrievers = list_off, R
     if mask & _lib.PROBFUSE:
         if seg_prob is None or seg_prob.dtype != torch.float64 or seg_prob.numel() != R * n_segments:
             raise ValueError("probfuse needs seg_prob: float64 [n_retrievers * n_segments]")
-        _lib.call("qf_fuse_probfuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
+        _lib.call("qf_fuse_probfuse" + sfx, Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
                   _ptr(rank), _ptr(weights), mask, int(rrf_k), _ptr(seg_prob), int(n_segments),
                   int(seg_len), int(max_entries), _ptr(out.union_docid), _ptr(out.union_count),
                   _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], _stream())
@@ -137,12 +155,12 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
             raise ValueError("learned_f32 applies to methods == ['learned'] only")
         if int(learned_f32) >> R:
             raise ValueError(f"learned_f32 names runs beyond the {R} of the run set")
-        _lib.call("qf_fuse_learned_f32", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
+        _lib.call("qf_fuse_learned_f32" + sfx, Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
                   _ptr(weights), int(learned_f32) & 0xFFFFFFFF, int(max_entries),
                   _ptr(out.union_docid), _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused),
                   out.fused.shape[1], _stream())
         return out
-    _lib.call("qf_fuse", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
+    _lib.call("qf_fuse" + sfx, Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
               _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
               _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused), out.fused.shape[1],
               _stream())
@@ -191,7 +209,7 @@ def fused_topk(out: FuseOut, list_off: torch.Tensor, n_retrievers: int, k: int, 
     else:
         docid = torch.empty((Q, M, k), dtype=torch.int32, device=dev)
         score = torch.empty((Q, M, k), dtype=torch.float64, device=dev)
-    _lib.call("qf_fused_topk", Q, R, _ptr(list_off), _ptr(out.union_count), _ptr(out.union_docid),
+    _lib.call("qf_fused_topk_wide" if out.wide else "qf_fused_topk", Q, R, _ptr(list_off), _ptr(out.union_count), _ptr(out.union_docid),
               _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], M, int(k), _ptr(docid),
               _ptr(score), _stream())
     return docid, score

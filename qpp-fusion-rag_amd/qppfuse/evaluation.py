@@ -90,6 +90,16 @@ def pack_qrels(qrels: Dict[str, Dict[str, int]], qids: Sequence[str],
     return QrelSet(off, docid, rel)
 
 
+def _ranked_index(qbase, counts, perm):
+    """(source, destination) indices that put every query's list in rank order at
+    its own slots: destination qbase[q] + i takes source qbase[q] + perm[qbase[q] + i]."""
+    counts = np.maximum(np.asarray(counts, np.int64), 0)
+    qb = np.asarray(qbase, np.int64)
+    dst = np.repeat(qb, counts) + (np.arange(int(counts.sum()), dtype=np.int64)
+                                   - np.repeat(np.cumsum(counts) - counts, counts))
+    return np.repeat(qb, counts) + perm[dst].astype(np.int64), dst
+
+
 def evaluate_device(q_base, base_stride: int, q_count, docid, perm, score, out_stride: int,
                     n_runs: int, n_queries: int, qrels_dev, max_qrels: int,
                     measures: Sequence[str], text_scores: bool = True):
@@ -175,9 +185,16 @@ class IREvaluator:
             t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
             q_base = t(run._qbase.astype(np.int64))
             q_count = t(run._counts.astype(np.int32))
-            docid = t(run._udoc.view(np.int32))
-            perm = t(run._perm.view(np.int16))
-            score = t(run._fused)
+            if run._perm.dtype == np.uint32:  # wide (qf_fuse_wide): qf_eval's perm is
+                # uint16, so the lists go over in rank order instead (perm NULL)
+                g = _ranked_index(run._qbase, run._counts, run._perm)
+                udoc, fz = np.zeros_like(run._udoc), np.zeros_like(run._fused)
+                udoc[g[1]], fz[g[1]] = run._udoc[g[0]], run._fused[g[0]]
+                docid, perm, score = t(udoc.view(np.int32)), None, t(fz)
+            else:
+                docid = t(run._udoc.view(np.int32))
+                perm = t(run._perm.view(np.int16))
+                score = t(run._fused)
             qs = pack_qrels(qrels, qids, docnos)
             vals = []
             for a in range(0, len(self.metric_names), _lib.EVAL_MAX_METRICS):

@@ -55,8 +55,9 @@ def lib() -> C.CDLL:
         L.qfio_runset_free.argtypes = [_vp]
         L.qfio_format_score.restype = C.c_size_t
         L.qfio_format_score.argtypes = [C.c_double, C.c_char_p]
-        L.qfio_write_run.restype = C.c_int
-        L.qfio_write_run.argtypes = [C.c_char_p, _i64] + [_vp] * 10 + [C.c_char_p, _i32]
+        for fn in (L.qfio_write_run, L.qfio_write_run32):
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_char_p, _i64] + [_vp] * 10 + [C.c_char_p, _i32]
         _LIB = L
     return _LIB
 
@@ -250,10 +251,12 @@ def write_run(path: str, order: np.ndarray, qbase: np.ndarray, counts: np.ndarra
     qbase = np.ascontiguousarray(qbase, np.int64)
     counts = np.ascontiguousarray(counts, np.int32)
     ud = np.ascontiguousarray(union_docid, np.uint32)
-    pm = np.ascontiguousarray(perm, np.uint16)
+    wide = np.asarray(perm).dtype == np.uint32  # qf_fuse_wide's perm
+    pm = np.ascontiguousarray(perm, np.uint32 if wide else np.uint16)
     fz = np.ascontiguousarray(fused, np.float64)
     qcb = np.frombuffer(qc, np.uint8) if qc else np.zeros(1, np.uint8)
     dcb = np.frombuffer(dc, np.uint8) if dc else np.zeros(1, np.uint8)
-    _check(lib().qfio_write_run(os.fsencode(path), len(order), _p(order), _p(qbase), _p(counts),
+    fn = lib().qfio_write_run32 if wide else lib().qfio_write_run
+    _check(fn(os.fsencode(path), len(order), _p(order), _p(qbase), _p(counts),
                                 _p(ud), _p(pm), _p(fz), _p(qo), _p(qcb), _p(do), _p(dcb),
                                 tag.encode(), int(n_threads)), "write_runfile")

@@ -292,7 +292,7 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
         raise ValueError(f"query '{rs.qids[bad[0]]}': {QF_QSTATUS.get(code, code)}")
     E = rs.n_entries
     udoc = out.union_docid.cpu().numpy()[:E].view(np.uint32)
-    perm = out.perm.cpu().numpy()[:, :E].view(np.uint16)
+    perm = out.perm.cpu().numpy()[:, :E].view(np.uint32 if out.wide else np.uint16)
     fused = out.fused.cpu().numpy()[:, :E]
     res = {}
     for m, name in enumerate(out.methods):

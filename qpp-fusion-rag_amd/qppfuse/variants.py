@@ -129,7 +129,8 @@ def _device_fuse(rs, method: str, weights=None, k: int = 60, seg=None):
         raise ValueError(f"query '{rs.qids[bad[0]]}': {QF_QSTATUS.get(code, code)}")
     E = rs.n_entries
     return (counts, out.union_docid.cpu().numpy()[:E].view(np.uint32),
-            out.perm.cpu().numpy()[0, :E].view(np.uint16), out.fused.cpu().numpy()[0, :E])
+            out.perm.cpu().numpy()[0, :E].view(np.uint32 if out.wide else np.uint16),
+            out.fused.cpu().numpy()[0, :E])
 
 
 def _ranked(rs, counts, udoc, perm, fused, qi):

@@ -7,6 +7,8 @@ produce, and the writer exactly the bytes of write_runfile's f-strings
 import math
 import os
 
+from pathlib import Path
+
 import numpy as np
 import pandas as pd
 import pytest
@@ -143,6 +145,34 @@ def test_write_run_matches_python_writer(tmp_path):
             u = qbase[q] + perm[qbase[q] + k]  # qf_fuse's layout: scores by u, perm ranks
             want.append(f"{qids[q]} Q0 {docnos[ud[u]]} {k + 1} {fused[u]:.6f} tag-1\n")
     assert out.read_text() == "".join(want)
+    # qf_fuse_wide's uint32 perm (qfio_write_run32): the same bytes
+    out32 = tmp_path / "x32.res"
+    fastio.write_run(str(out32), order, qbase, counts, ud, perm.astype(np.uint32), fused, rs,
+                     "tag-1")
+    assert out32.read_bytes() == out.read_bytes()
+
+
+def test_write_run_uint32_perm_beyond_65535():
+    """A union of 70,000 documents: ranks past u = 65,535 through the uint32 perm."""
+    import tempfile
+    from qppfuse.runset import RunSet
+    rng = np.random.default_rng(6)
+    n = 70_000
+    docnos = np.array([f"d{i:06d}" for i in range(n)], dtype=object)
+    ud = rng.permutation(n).astype(np.uint32)
+    fused = rng.standard_normal(n)
+    perm = np.argsort(-fused, kind="stable").astype(np.uint32)
+    rs = RunSet(qids=["q1"], rankers=["a"], docnos=docnos, list_off=np.zeros(2, np.int64),
+                docid=np.zeros(0, np.uint32), score=np.zeros(0), rank=np.zeros(0, np.int64))
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "w.res"
+        fastio.write_run(str(out), np.zeros(1, np.int64), np.zeros(1, np.int64),
+                         np.array([n], np.int32), ud, perm, fused, rs, "t")
+        lines = out.read_text().splitlines()
+    assert len(lines) == n
+    for k in (0, 65535, 65536, n - 1):
+        u = perm[k]
+        assert lines[k] == f"q1 Q0 {docnos[ud[u]]} {k + 1} {fused[u]:.6f} t"
 
 
 def test_load_runs_returns_frames_and_caches_the_pack(tmp_path):

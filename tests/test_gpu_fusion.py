@@ -84,7 +84,7 @@ def test_fuse_all_methods_bit_exact_vs_c_oracle(gpu, shape):
     w_h = w.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
     uc = out.union_count.cpu().numpy()
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fused = out.ranked_fused().cpu().numpy()
     assert (uc > 0).all()
     for m, name in enumerate(ALL):
@@ -107,7 +107,7 @@ def test_fuse_f64_scores_bit_exact(gpu):
     for m, name in enumerate(["combsum", "combmnz", "rrf"]):
         _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, raw_h, R, name)
         f = out.ranked_fused().cpu().numpy()[m]
-        p = out.perm.cpu().numpy().view(np.uint16)[m]
+        p = _perm_np(out)[m]
         for q in range(Q):
             b, n = off_h[q * R], uc[q]
             assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
@@ -136,7 +136,7 @@ def test_bucket_sort_weight_extremes(gpu):
     doc_h = docid.cpu().numpy().view(np.uint32)
     sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uc = out.union_count.cpu().numpy()
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fused = out.ranked_fused().cpu().numpy()
     assert (uc > 0).all()
     for m, name in enumerate(ALL):
@@ -170,7 +170,7 @@ def test_ranx_minmax_denominator_floor(gpu, max_entries):
                       max_entries=max_entries)
     uc = int(out.union_count[0])
     f = out.ranked_fused().cpu().numpy()
-    p = out.perm.cpu().numpy().view(np.uint16)
+    p = _perm_np(out)
     for m, name in enumerate(["combsum", "combmnz", "rrf"]):
         _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name)
         assert uc == o_uc[0] == 5
@@ -204,7 +204,7 @@ def test_edge_cases_empty_lists_ties_single(gpu):
     for m, name in enumerate(ALL):
         o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, weights=w.cpu().numpy())
         np.testing.assert_array_equal(uc, o_uc)
-        np.testing.assert_array_equal(out.perm.cpu().numpy().view(np.uint16)[m][:off[-1]][
+        np.testing.assert_array_equal(_perm_np(out)[m][:off[-1]][
             np.concatenate([np.arange(off[q * R], off[q * R] + uc[q]) for q in range(3)])],
             o_perm[np.concatenate([np.arange(off[q * R], off[q * R] + uc[q]) for q in range(3)])])
         f = out.ranked_fused().cpu().numpy()[m]
@@ -213,7 +213,8 @@ def test_edge_cases_empty_lists_ties_single(gpu):
             assert f[b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
-@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680, 7681, 10240, 10241, 65535])
+@pytest.mark.parametrize("n_entries", [1024, 1025, 5120, 5121, 7680, 7681, 10240, 10241, 65535,
+                                       65536, 100_000])
 def test_kernel_capacity_boundaries(gpu, n_entries):
     """Queries exactly at / just past each kernel configuration's capacity."""
     from qppfuse import engine
@@ -233,7 +234,7 @@ def test_kernel_capacity_boundaries(gpu, n_entries):
         assert uc[0] == o_uc[0]
         n = uc[0]
         assert out.ranked_fused().cpu().numpy()[m][:n].tobytes() == o_fused[:n].tobytes()
-        np.testing.assert_array_equal(out.perm.cpu().numpy().view(np.uint16)[m][:n], o_perm[:n])
+        np.testing.assert_array_equal(_perm_np(out)[m][:n], o_perm[:n])
 
 
 def test_too_big_and_unsorted_are_reported(gpu):
@@ -246,12 +247,22 @@ def test_too_big_and_unsorted_are_reported(gpu):
                       weights=torch.ones(1, dtype=torch.float64, device=gpu))
     assert out.union_count.cpu().numpy()[0] == 3  # weighted methods need no order
     with pytest.raises(_lib.QPPFuseError):
-        engine.fuse(doff, ddoc, dsc, R, ["rrf"], max_entries=_lib.max_entries_per_query() + 1)
+        engine.fuse(doff, ddoc, dsc, R, ["rrf"],
+                    max_entries=_lib.max_entries_per_query_wide() + 1)
+    small = engine.alloc_fuse_out(1, 3, _lib.RRF, gpu)  # uint16 perm: too narrow
+    with pytest.raises(ValueError, match="uint32 perm"):
+        engine.fuse(doff, ddoc, dsc, R, ["rrf"], max_entries=_lib.max_entries_per_query() + 1,
+                    out=small)
     with pytest.raises(ValueError):
         engine.fuse(doff, ddoc, dsc, R, ["wrrf"], max_entries=3)  # no weights
     off, doc, sc, doff, ddoc, dsc = _csr([([1, 2, 1], [0.9, 0.5, 0.1]), ([4], [1.0])], gpu)
     out = engine.fuse(doff, ddoc, dsc, 2, ["combsum"], max_entries=4)
     assert out.union_count.cpu().numpy()[0] == -5  # duplicate docid inside one list
+
+
+def _perm_np(out):
+    """perm as numpy: uint16, or uint32 when the call took the wide entry points."""
+    return out.perm.cpu().numpy().view(np.uint32 if out.wide else np.uint16)
 
 
 def _sort_case(kind, n, rng):
@@ -274,13 +285,15 @@ def _sort_case(kind, n, rng):
 
 
 @pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000, 7681, 10240, 10241,
-                               40000])
+                               40000, 70000])
 @pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform",
                                   "huge_and_inf"])
 def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
     """One retriever, W-CombSUM with weight 1: the fused scores are the inputs, so the
-    kernel's sort (LSD window + run fix-up + full-LSD fallback) is checked against a
-    stable descending sort with -0.0 == +0.0 (Python's sorted(), src/fusion.py:488)."""
+    kernel's sort (LSD window + run fix-up + full-LSD fallback; above 10,240 the
+    workspace bucket sort and its bitonic fallback, above 65,535 with the uint32 perm)
+    is checked against a stable descending sort with -0.0 == +0.0 (Python's sorted(),
+    src/fusion.py:488)."""
     from qppfuse import engine
     rng = np.random.default_rng(hash((kind, n)) & 0xFFFF)
     s = _sort_case(kind, n, rng)
@@ -291,7 +304,7 @@ def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
     out = engine.fuse(t(off), t(doc.view(np.int32)), t(s), 1, ["wcombsum"], weights=w,
                       max_entries=n)
     assert int(out.union_count[0]) == n
-    perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
+    perm = _perm_np(out)[0][:n].astype(np.int64)
     fused = out.ranked_fused().cpu().numpy()[0][:n]
     want = np.argsort(-s, kind="stable")
     np.testing.assert_array_equal(perm, want)
@@ -312,7 +325,7 @@ def test_fused_topk_compaction(gpu, k):
     d, s = d.cpu().numpy().view(np.uint32), s.cpu().numpy()
     off_h, uc = off.cpu().numpy(), out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fz = out.ranked_fused().cpu().numpy()
     for q in range(Q):
         b, n = off_h[q * R], min(k, uc[q])
@@ -346,7 +359,7 @@ def test_grids_beyond_65536_workgroups(gpu):
     sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fused = out.ranked_fused().cpu().numpy()
     E = Q * R * K
     qb = np.repeat(off_h[0:-1:R][:Q], R * K)
@@ -377,7 +390,7 @@ def test_bucket_sort_grid_beyond_65536_workgroups(gpu):
     sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fused = out.ranked_fused().cpu().numpy()
     qs = np.sort(np.random.default_rng(4).choice(Q, 300, replace=False))
     qs = np.concatenate([[0], qs, [Q - 1]])
@@ -425,7 +438,7 @@ def test_workspace_path_for_very_large_queries(gpu, kind):
                       rank=torch.from_numpy(rank).to(gpu), max_entries=n_max)
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fz = out.ranked_fused().cpu().numpy()
     for m, name in enumerate(ALL):
         o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
@@ -438,13 +451,14 @@ def test_workspace_path_for_very_large_queries(gpu, kind):
             assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
-@pytest.mark.parametrize("K", [6000, 12000])
+@pytest.mark.parametrize("K", [6000, 12000, 50000])
 def test_workspace_path_learned_ties_by_docid(gpu, K):
     """Learned fusion on a very large query: ties in docid order (the groupby's
     output order, src/fusion.py:443-446).  With two lists the Kahan sum equals
     the plain left-to-right sum, so the scores are W-CombSUM's.  K = 6000: a union
     of ~9,000 (the workspace join, then the LDS sort); K = 12000: ~18,000 (the
-    workspace bitonic sort)."""
+    workspace bucket sort, minimum's sub-buckets by docid); K = 50000: ~75,000 (the
+    same with the uint32 perm)."""
     from qppfuse import engine
     R = 2
     rng = np.random.default_rng(5)
@@ -465,7 +479,7 @@ def test_workspace_path_learned_ties_by_docid(gpu, K):
     unsorted = np.empty(n)
     unsorted[o_perm[:n].astype(np.int64)] = o_fused[:n]
     want = np.lexsort((ud, -unsorted))
-    perm = out.perm.cpu().numpy().view(np.uint16)[0][:n].astype(np.int64)
+    perm = _perm_np(out)[0][:n].astype(np.int64)
     np.testing.assert_array_equal(perm, want)
     assert out.ranked_fused().cpu().numpy()[0][:n].tobytes() == unsorted[want].tobytes()
 
@@ -493,7 +507,7 @@ def test_more_than_16_runs_take_the_workspace_join(gpu, R, K):
                       rank=torch.from_numpy(rank).to(gpu), max_entries=n_max)
     uc = out.union_count.cpu().numpy()
     ud = out.union_docid.cpu().numpy().view(np.uint32)
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fz = out.ranked_fused().cpu().numpy()
     for m, name in enumerate(ALL):
         o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
@@ -593,7 +607,7 @@ def test_method_subsets_bit_exact(gpu, methods):
     doc_h = docid.cpu().numpy().view(np.uint32)
     sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
     uc = out.union_count.cpu().numpy()
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fused = out.ranked_fused().cpu().numpy()
     slot = {m: i for i, m in enumerate(sorted(methods, key=ALL.index))}
     for name in methods:
@@ -634,7 +648,7 @@ def test_two_runs_on_adversarial_keys(gpu, kind, overlap, n):
     out = engine.fuse(t(off), t(doc.view(np.int32)), t(sc), 2, ms, weights=t(w_h),
                       max_entries=2 * n)
     uc = int(out.union_count[0])
-    perm = out.perm.cpu().numpy().view(np.uint16)
+    perm = _perm_np(out)
     fused = out.ranked_fused().cpu().numpy()
     for m, name in enumerate(ms):
         _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, 2, name, 60, weights=w_h)
@@ -643,39 +657,82 @@ def test_two_runs_on_adversarial_keys(gpu, kind, overlap, n):
         assert fused[m][:uc].tobytes() == o_fused[:uc].tobytes(), name
 
 
-@pytest.mark.gpu
-def test_one_kernel_join_sort_path(gpu):
-    """join_sort_kernel (QF_JS_BLOCK=512: join, sums and every method's sort in one
-    workgroup per query — the measured-slower alternative kept for A/B) bit-exact vs
-    the oracle; the switch is read once per process, so it runs in a child."""
-    import subprocess
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parents[1]
-    code = (
-        "import sys; sys.path[:0] = [%r, %r]\n" % (str(root), str(root / "qpp-fusion-rag_amd")) +
-        "import numpy as np, torch\n"
-        "from qppfuse import engine\n"
-        "from oracle import _loader as coracle\n"
-        "Q, R, K = 48, 5, 1000\n"
-        "off, docid, raw = engine.synth_runs(0, Q, R, K, seed=5)\n"
-        "_, micro = engine.minmax_per_query(raw, off, want_norm=False)\n"
-        "w = torch.rand(Q * R, dtype=torch.float64, device=off.device)\n"
-        "ms = ['combsum', 'combmnz', 'rrf', 'wcombsum', 'wcombmnz', 'wrrf']\n"
-        "out = engine.fuse(off, docid, micro, R, ms, weights=w, max_entries=R * K)\n"
-        "f = out.ranked_fused().cpu().numpy(); p = out.perm.cpu().numpy().view(np.uint16)\n"
-        "uc = out.union_count.cpu().numpy(); o = off.cpu().numpy()\n"
-        "d = docid.cpu().numpy().view(np.uint32); s = micro.cpu().numpy() / 1e6\n"
-        "for m, name in enumerate(ms):\n"
-        "    _, ouc, op, of = coracle.fuse(o, d, s, R, name, 60, weights=w.cpu().numpy())\n"
-        "    assert np.array_equal(uc, ouc)\n"
-        "    for q in range(Q):\n"
-        "        b, n = o[q * R], uc[q]\n"
-        "        assert f[m, b:b + n].tobytes() == of[b:b + n].tobytes(), (name, q)\n"
-        "        assert np.array_equal(p[m, b:b + n], op[b:b + n]), (name, q)\n"
-        "print('js-ok')\n")
-    env = dict(__import__("os").environ, QF_JS_BLOCK="512")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                       timeout=110)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    assert "js-ok" in r.stdout
+def _wide_case(rng, sizes, R, pool_factor=2):
+    lists, ranks = [], []
+    for K in sizes:
+        pool = rng.choice(1 << 30, size=max(1, pool_factor * K), replace=False).astype(np.uint32)
+        for r in range(R):
+            k = K if r != 2 else K // 2  # ragged lists
+            docs = rng.choice(pool, size=k, replace=False)
+            lists.append((docs, np.sort(rng.integers(0, 400_000 + r * 7919, k))[::-1] / 1e6))
+            ranks.append(np.arange(1, k + 1, dtype=np.int32))
+    return lists, np.concatenate(ranks)
+
+
+@pytest.mark.parametrize("kind", ["f64", "micro"])
+def test_wide_perm_queries_beyond_65535_entries(gpu, kind):
+    """qf_fuse_wide: a query of 100,000+ entries whose union exceeds 65,535 documents
+    (u needs 32 bits) next to small, mid-size and 40,000-entry queries in the same
+    call — every path writes the uint32 perm — bit-exact vs the oracle for every
+    method; qf_fused_topk_wide packs the same ranks."""
+    from qppfuse import engine, _lib
+    R = 4
+    rng = np.random.default_rng(21 if kind == "f64" else 22)
+    sizes = [300, 29_000, 0, 2600, 11_000, 1]  # per-list K: 101,500 entries in query 1
+    lists, rank = _wide_case(rng, sizes, R, pool_factor=5)
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    n_max = int(np.max(off[R::R] - off[0:-1:R]))
+    assert n_max > _lib.max_entries_per_query()
+    if kind == "micro":
+        dsc = torch.from_numpy(np.rint(sc * 1e6).astype(np.int32)).to(gpu)
+    w = rng.uniform(0.05, 1.0, len(sizes) * R)
+    out = engine.fuse(doff, ddoc, dsc, R, ALL, rrf_k=60, weights=torch.from_numpy(w).to(gpu),
+                      rank=torch.from_numpy(rank).to(gpu), max_entries=n_max)
+    assert out.wide
+    uc = out.union_count.cpu().numpy()
+    assert uc[1] > 65535
+    ud = out.union_docid.cpu().numpy().view(np.uint32)
+    perm = _perm_np(out)
+    fz = out.ranked_fused().cpu().numpy()
+    for m, name in enumerate(ALL):
+        o_ud, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w,
+                                                   rank=rank)
+        np.testing.assert_array_equal(uc, o_uc)
+        for q in range(len(sizes)):
+            b, n = off[q * R], uc[q]
+            np.testing.assert_array_equal(ud[b:b + n], o_ud[b:b + n])
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=f"{name} q{q}")
+            assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+    k = 70_000
+    d, s = engine.fused_topk(out, doff, R, k)
+    d, s = d.cpu().numpy().view(np.uint32), s.cpu().numpy()
+    for q in range(len(sizes)):
+        b, n = off[q * R], min(k, uc[q])
+        for m in range(len(ALL)):
+            np.testing.assert_array_equal(d[q, m, :n], ud[b + perm[m, b:b + n].astype(np.int64)])
+            assert s[q, m, :n].tobytes() == fz[m, b:b + n].tobytes()
+
+
+def test_wide_api_fuse_and_write_runfile(gpu, tmp_path):
+    """The reference's API over a query of 3 x 40,000 entries (union ~84,000):
+    fuse_many takes the wide path; the FusedRun's ranked lists and write_runfile's
+    bytes equal the restated reference's (oracle/ref_port.py) on the same runs."""
+    import pandas as pd
+    rng = np.random.default_rng(31)
+    K = 40_000
+    pool = np.array([f"d{i:07d}" for i in rng.choice(10**7, size=3 * K, replace=False)])
+    frames = {}
+    for name in ("bm25", "splade", "tct"):
+        docs = rng.choice(pool, size=K, replace=False)
+        sc = np.sort(rng.integers(0, 10**6, K))[::-1] / 1e6
+        frames[name] = pd.DataFrame({"qid": "q1", "iter": "Q0", "docno": docs,
+                                     "rank": np.arange(1, K + 1), "score": sc, "runid": name})
+    fusion = _api()
+    got = fusion.fuse_many(frames, ["combsum", "rrf"])
+    for m in ("combsum", "rrf"):
+        want = ref_port.fuse(frames, m)
+        assert len(want["q1"]) > 65535
+        assert got[m]["q1"] == want["q1"], m
+        path = tmp_path / f"{m}.res"
+        fusion.write_runfile(got[m], str(path), m)
+        assert path.read_text() == ref_port.runfile_text(want, m), m

@@ -27,8 +27,9 @@ lib.qf_debug_stamps.restype = C.c_int
 lib.qf_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int]
 NB, NS = 32768, 16
 names = ["init", "insert", "numbering", "group offsets", "placement", "sums",
-         "sort:fill", "sort:tiles k<=T", "sort:global+tiles", "sort:output"]
-Q, R, K = 3452, 16, 1000
+         "sort:fill", "sort:tiles k<=T", "sort:global+tiles", "sort:output", "sort:bucket"]
+args = [a for a in sys.argv[1:] if not a.startswith("-")]
+Q, R, K = (int(a) for a in args) if len(args) == 3 else (3452, 16, 1000)
 dev = torch.device("cuda", 0)
 off, docid, raw = engine.synth_runs(0, Q, R, K)
 _, micro = engine.minmax_per_query(raw, off, want_norm=False)
@@ -44,6 +45,6 @@ for ms in (["rrf"], ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"
     lib.qf_debug_stamps(buf.ctypes.data_as(C.c_void_p), NB * NS, 1)
     # XL blocks 0..511; the LDS kernels return before their first stamp for
     # queries above their capacity, so these slots are the XL kernel's alone.
-    st = buf.reshape(NB, NS)[:512, :10].astype(np.float64)
+    st = buf.reshape(NB, NS)[:512, :11].astype(np.float64)
     out["+".join(ms)] = {n: round(float(st[:, i].sum() / Q)) for i, n in enumerate(names)}
 print(json.dumps(out, indent=1))
