@@ -736,3 +736,10 @@ def test_wide_api_fuse_and_write_runfile(gpu, tmp_path):
         path = tmp_path / f"{m}.res"
         fusion.write_runfile(got[m], str(path), m)
         assert path.read_text() == ref_port.runfile_text(want, m), m
+    # the IR evaluation of the wide FusedRun (its lists go over in rank order)
+    from qppfuse.evaluation import IREvaluator
+    ev = IREvaluator(["nDCG@10", "RR@10", "R@100", "P@10"])
+    ranked = [d for d, _ in got["rrf"]["q1"]]
+    qrels = {"q1": {ranked[i]: 1 + i % 2 for i in (0, 7, 500, 70_000)} | {"dx": 1}}
+    assert ev.evaluate(got["rrf"], qrels, per_query=True) == \
+        ev.evaluate({"q1": got["rrf"]["q1"]}, qrels, per_query=True)
