@@ -497,7 +497,10 @@ def cpu_baseline_native(p: Pipeline, nq: int):
     sc = h["micro"].astype(np.float64) / 1e6
     t0 = time.perf_counter()
     for m in p.methods:
-        coracle.fuse(h["off"], h["docid"], sc, p.R, m, 60, weights=h["w"])
+        # learned fusion's native cost: the same weighted per-document sum (the C
+        # oracle has no Kahan / docid-tie variant; the loop shape is W-CombSUM's)
+        coracle.fuse(h["off"], h["docid"], sc, p.R, "wcombsum" if m == "learned" else m, 60,
+                     weights=h["w"])
     coracle.qpp_raw(h["raw"], h["off"], np.repeat(h["nt"], p.R), np.repeat(h["tf"][:, 0], p.R),
                     np.repeat(h["tf"][:, 1], p.R))
     dt = time.perf_counter() - t0

@@ -185,15 +185,29 @@ size_t count_rows(const char* p, const char* end) {
   return n;
 }
 
-// Row columns, structure of arrays over all files in file order.
+inline uint64_t hash_sv(std::string_view v) {  // FNV-1a + avalanche
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : v) h = (h ^ c) * 1099511628211ull;
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  return h;
+}
+
+// Row columns, structure of arrays over all files in file order.  The parse also
+// hashes each docno (its bytes are in cache then) and marks the rows whose qid /
+// iter / tag differs from the row before (run heads: those columns are long runs).
 struct Cols {
   RawArray<SV> q, d, it, tag;
   RawArray<int64_t> rank;
   RawArray<double> score;
   RawArray<int32_t> micro;
+  RawArray<uint64_t> dh;                 // docno hashes
+  RawArray<uint8_t> qh, ith, tagh;       // run heads
   void resize(size_t n) {
     q.resize(n); d.resize(n); it.resize(n); tag.resize(n);
     rank.resize(n); score.resize(n); micro.resize(n);
+    dh.resize(n); qh.resize(n); ith.resize(n); tagh.resize(n);
   }
 };
 
@@ -201,6 +215,8 @@ struct Cols {
 // returns the number of rows whose score is not an exact 6-decimal number.
 bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micro_bad,
                  std::string& err) {
+  std::string_view pq, pit, ptag;  // the previous row's (a chunk's first row is a head)
+  bool first = true;
   while (p < end) {
     std::string_view f[7];
     int nf = 0;
@@ -224,6 +240,12 @@ bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micr
     c.it[o] = SV{f[1].data(), f[1].size()};
     c.d[o] = SV{f[2].data(), f[2].size()};
     c.tag[o] = SV{f[5].data(), f[5].size()};
+    c.dh[o] = hash_sv(f[2]);
+    c.qh[o] = first || f[0] != pq;
+    c.ith[o] = first || f[1] != pit;
+    c.tagh[o] = first || f[5] != ptag;
+    pq = f[0]; pit = f[1]; ptag = f[5];
+    first = false;
     // rank: [+-]digits (strtoll's accepted form for plain integer text)
     {
       const std::string_view t = f[3];
@@ -249,25 +271,42 @@ bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micr
   return true;
 }
 
-inline uint64_t hash_sv(std::string_view v) {  // FNV-1a + avalanche
-  uint64_t h = 1469598103934665603ull;
-  for (unsigned char c : v) h = (h ^ c) * 1099511628211ull;
-  h ^= h >> 33;
-  h *= 0xff51afd7ed558ccdull;
-  h ^= h >> 33;
-  return h;
-}
-
 // Sorted unique strings of `views`, and each view's index among them: hash
 // partitions deduplicated in parallel, then only the distinct strings sorted.
+// The sort key of a distinct string: its first 16 bytes big-endian, zero-padded
+// (no NUL in the text, so a proper prefix sorts first); only equal keys compare
+// the strings.  Sorting 24-byte records keeps the sort in cache instead of
+// chasing string pointers.
+struct Key {
+  uint64_t k1, k2;
+  uint32_t u;
+};
+inline Key make_key(std::string_view v, uint32_t u) {
+  unsigned char b[16] = {0};
+  memcpy(b, v.data(), std::min<size_t>(16, v.size()));
+  uint64_t k1 = 0, k2 = 0;
+  for (int i = 0; i < 8; ++i) {
+    k1 = (k1 << 8) | b[i];
+    k2 = (k2 << 8) | b[8 + i];
+  }
+  return Key{k1, k2, u};
+}
+
+// hs_in: the strings' hash_sv values when the caller has them (the parse's)
 template <class Views>
-void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<uint32_t>& id) {
+void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<uint32_t>& id,
+            const uint64_t* hs_in = nullptr) {
   PhaseTimer tm;
   const size_t n = views.size();
   constexpr int P = 256;
-  std::vector<uint64_t> hs(n);
+  RawArray<uint64_t> hs_own;
+  const uint64_t* hs = hs_in;
+  if (!hs) {
+    hs_own.resize(n);
 #pragma omp parallel for schedule(static)
-  for (size_t i = 0; i < n; ++i) hs[i] = hash_sv(sv(views[i]));
+    for (size_t i = 0; i < n; ++i) hs_own[i] = hash_sv(sv(views[i]));
+    hs = hs_own.data();
+  }
   // rows of each partition (top 8 bits), in row order
   const int T = std::max(1, omp_get_max_threads());
   std::vector<std::vector<uint32_t>> cnt(T, std::vector<uint32_t>(P, 0));
@@ -290,8 +329,10 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   for (int t = 0; t < T; ++t)
     for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) rows[at[t][hs[i] >> 56]++] = (uint32_t)i;
   tm.mark("  hash+partition");
-  // per partition: open-addressing table of first rows -> local unique index
+  // per partition: open-addressing table of first rows -> local unique index; each
+  // new distinct string's sort key is made while its bytes are in cache
   std::vector<std::vector<uint32_t>> ufirst(P);  // first row of each distinct string
+  std::vector<std::vector<Key>> ukey(P);
   std::vector<uint32_t> local(n);
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < P; ++b) {
@@ -301,6 +342,7 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     while (cap < 2 * m) cap <<= 1;
     std::vector<uint32_t> tab(cap, 0xFFFFFFFFu);
     auto& uf = ufirst[b];
+    auto& uk = ukey[b];
     for (size_t k = a0; k < a1; ++k) {
       const uint32_t i = rows[k];
       size_t h = (size_t)hs[i] & (cap - 1);
@@ -309,6 +351,7 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
         if (u == 0xFFFFFFFFu) {
           tab[h] = (uint32_t)uf.size();
           local[i] = (uint32_t)uf.size();
+          uk.push_back(make_key(sv(views[i]), (uint32_t)uf.size()));  // u: local for now
           uf.push_back(i);
           break;
         }
@@ -323,28 +366,16 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   for (int b = 0; b < P; ++b) ubase[b + 1] = ubase[b] + ufirst[b].size();
   const size_t U = ubase[P];
   std::vector<uint32_t> reps(U);  // row of each distinct string
-  for (int b = 0; b < P; ++b)
-    std::copy(ufirst[b].begin(), ufirst[b].end(), reps.begin() + (long)ubase[b]);
-  // Sort the distinct strings by byte order (== Python's str order for UTF-8).
-  // Keys are the first 16 bytes big-endian, zero-padded (no NUL in the text, so
-  // a proper prefix sorts first); only equal keys compare the strings.  Sorting
-  // 24-byte records keeps the sort in cache instead of chasing string pointers.
-  struct Key {
-    uint64_t k1, k2;
-    uint32_t u;
-  };
   std::vector<Key> keys(U);
-#pragma omp parallel for schedule(static)
-  for (size_t k = 0; k < U; ++k) {
-    const std::string_view v = sv(views[reps[k]]);
-    unsigned char b[16] = {0};
-    memcpy(b, v.data(), std::min<size_t>(16, v.size()));
-    uint64_t k1 = 0, k2 = 0;
-    for (int i = 0; i < 8; ++i) {
-      k1 = (k1 << 8) | b[i];
-      k2 = (k2 << 8) | b[8 + i];
+  // Sort the distinct strings by byte order (== Python's str order for UTF-8).
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int b = 0; b < P; ++b) {
+    std::copy(ufirst[b].begin(), ufirst[b].end(), reps.begin() + (long)ubase[b]);
+    Key* kd = keys.data() + ubase[b];
+    for (size_t j = 0; j < ukey[b].size(); ++j) {
+      kd[j] = ukey[b][j];
+      kd[j].u += (uint32_t)ubase[b];
     }
-    keys[k] = Key{k1, k2, (uint32_t)k};
   }
   auto less = [&](const Key& a, const Key& b) {
     if (a.k1 != b.k1) return a.k1 < b.k1;
@@ -372,18 +403,31 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
 
 // intern() for columns made of long runs of one value (qid, Q0, tag): only the
 // run heads are interned.
+// head[i]: row i differs from row i - 1 (or starts a parse chunk: a head too many
+// costs nothing but one more string to intern).
 template <class Views>
-void intern_runs(const Views& views, std::vector<std::string_view>& uniq, RawArray<uint32_t>& id) {
+void intern_runs(const Views& views, const uint8_t* head, std::vector<std::string_view>& uniq,
+                 RawArray<uint32_t>& id) {
   const size_t n = views.size();
-  std::vector<uint8_t> head(n);
+  const int T = std::max(1, omp_get_max_threads());
+  std::vector<size_t> nh(T + 1, 0);
 #pragma omp parallel for schedule(static)
-  for (size_t i = 0; i < n; ++i) head[i] = i == 0 || sv(views[i]) != sv(views[i - 1]);
-  std::vector<size_t> hix;
-  for (size_t i = 0; i < n; ++i)
-    if (head[i]) hix.push_back(i);
-  if (hix.size() * 4 > n) {  // not run-structured
+  for (int t = 0; t < T; ++t) {
+    size_t c = 0;
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) c += head[i] | (i == 0);
+    nh[t + 1] = c;
+  }
+  for (int t = 0; t < T; ++t) nh[t + 1] += nh[t];
+  if (nh[T] * 4 > n) {  // not run-structured
     intern(views, uniq, id);
     return;
+  }
+  std::vector<size_t> hix(nh[T]);
+#pragma omp parallel for schedule(static)
+  for (int t = 0; t < T; ++t) {
+    size_t o = nh[t];
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i)
+      if (head[i] | (i == 0)) hix[o++] = i;
   }
   std::vector<std::string_view> hv(hix.size());
   for (size_t k = 0; k < hix.size(); ++k) hv[k] = sv(views[hix[k]]);
@@ -514,12 +558,12 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->row_score = std::move(cols.score);
   RawArray<int32_t> row_micro = std::move(cols.micro);
   // ---- intern qids / docnos / iter / tag ---------------------------------------
-  intern_runs(cols.q, rs->qids, rs->row_qid);
+  intern_runs(cols.q, cols.qh.data(), rs->qids, rs->row_qid);
   tm.mark("intern qid");
-  intern(cols.d, rs->docnos, rs->row_docid);
+  intern(cols.d, rs->docnos, rs->row_docid, cols.dh.data());
   tm.mark("intern docno");
-  intern_runs(cols.it, rs->iters, rs->row_iter);
-  intern_runs(cols.tag, rs->tags, rs->row_tag);
+  intern_runs(cols.it, cols.ith.data(), rs->iters, rs->row_iter);
+  intern_runs(cols.tag, cols.tagh.data(), rs->tags, rs->row_tag);
   tm.mark("intern iter/tag");
   if (rs->docnos.size() >= 0xFFFFFFFFull) { delete rs; return fail(QFIO_EINVAL, "too many docnos"); }
   // ---- CSR by (query, file), stable in file order -------------------------------

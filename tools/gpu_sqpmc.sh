@@ -4,7 +4,7 @@
 # Usage: tools/gpu_sqpmc.sh [lib]   (one rocprofv3 --pmc pass; <= 8 SQ counters)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-O=gpurun_out/sqpmc
+O=${SQPMC_OUT:-gpurun_out/sqpmc}
 mkdir -p $O
 L=${1:-qpp-fusion-rag_amd/qppfuse/libqppfuse.so}
 QF_LIB=$L timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/p1 -o run -- python3 tools/fusebench.py > $O/p1.log 2>&1
