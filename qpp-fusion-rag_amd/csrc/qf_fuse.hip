@@ -1724,6 +1724,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 // ============================================================================
 constexpr int kXlBlock = 1024;
 constexpr int kXlTile = 4096;  // bitonic items per LDS tile (64 KB of keys + ties)
+constexpr int kXlUnroll = 4;   // entries per thread per step of the join's phases
 constexpr int kXlNMax = 65535;  // entries per query with a uint16 perm
 constexpr int kXlNMaxWide = (1 << 24) - 1;  // with a uint32 perm (grouped entries: e | r << 27)
 constexpr int kXlGrid = 512;   // workgroups: two per CU (75 KB of LDS each)
@@ -2021,27 +2022,58 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   xl_sync();
   QF_STAMP(0);
   // ---- 1. insert --------------------------------------------------------------
+  // kXlUnroll entries per thread per step, each phase's loads / atomics for all of
+  // them issued before any result is used: the L2 atomic round trips overlap
+  // (one entry per step left every thread waiting on one chain at a time)
   int status = 0, r = 0;
-  for (int e = tid; e < N; e += kXlBlock) {
-    const int64_t g = base + e;
-    while (g >= s_off[r + 1]) ++r;
-    const uint32_t d = p.docid[g];
-    if (d == kEmpty) status = QF_QSTATUS_BADDOC;
-    uint32_t h = (d * 0x9E3779B1u) >> (32 - tb);
-    while (true) {
-      const uint32_t prev = atomicCAS(&w.tkey[h], kEmpty, d);
-      if (prev == kEmpty || prev == d) break;
-      h = (h + 1) & (TS - 1);
+  for (int e0 = tid; e0 < N; e0 += kXlUnroll * kXlBlock) {
+    uint32_t d[kXlUnroll], h[kXlUnroll], prev[kXlUnroll], old[kXlUnroll];
+    int rr[kXlUnroll];
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      d[j] = 0u;
+      if (e < N) {
+        while (base + e >= s_off[r + 1]) ++r;
+        d[j] = p.docid[base + e];
+      }
+      rr[j] = r;
     }
-    const uint32_t old = atomicOr(&w.tmask[h], 1u << r);
-    if ((old >> r) & 1u) status = QF_QSTATUS_DUPDOC;
-    w.eslot[e] = h;
-    if (g + 1 < s_off[r + 1]) {
-      if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
-          ScoreIn<KIND>::raw(p.score, g + 1) > ScoreIn<KIND>::raw(p.score, g))
-        status = QF_QSTATUS_UNSORTED;
-      if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
-        status = QF_QSTATUS_RANKORDER;
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      h[j] = (d[j] * 0x9E3779B1u) >> (32 - tb);
+      if (e0 + j * kXlBlock < N) {
+        if (d[j] == kEmpty) status = QF_QSTATUS_BADDOC;
+        prev[j] = atomicCAS(&w.tkey[h[j]], kEmpty, d[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      if (e0 + j * kXlBlock < N) {
+        while (prev[j] != kEmpty && prev[j] != d[j]) {  // probe on
+          h[j] = (h[j] + 1) & (TS - 1);
+          prev[j] = atomicCAS(&w.tkey[h[j]], kEmpty, d[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j)
+      old[j] = e0 + j * kXlBlock < N ? atomicOr(&w.tmask[h[j]], 1u << rr[j]) : 0u;
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      if (e < N) {
+        const int64_t g = base + e;
+        if ((old[j] >> rr[j]) & 1u) status = QF_QSTATUS_DUPDOC;
+        w.eslot[e] = h[j];
+        if (g + 1 < s_off[rr[j] + 1]) {
+          if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
+              ScoreIn<KIND>::raw(p.score, g + 1) > ScoreIn<KIND>::raw(p.score, g))
+            status = QF_QSTATUS_UNSORTED;
+          if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
+            status = QF_QSTATUS_RANKORDER;
+        }
+      }
     }
   }
   if (status) atomicMin(s_status, status);
@@ -2053,24 +2085,43 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     return;
   }
   // ---- 2. first-seen numbering ---------------------------------------------------
+  // chunks of kXlUnroll * kXlBlock entries, kXlUnroll consecutive ones per thread (in
+  // entry order: thread t's precede thread t + 1's), one block scan per chunk
   uint32_t U = 0;
   r = 0;
-  for (int c0 = 0; c0 < N; c0 += kXlBlock) {
-    const int e = c0 + tid;
-    uint32_t h = 0, msk = 0;
-    bool rep = false;
-    if (e < N) {
-      while (base + e >= s_off[r + 1]) ++r;
-      h = w.eslot[e];
-      msk = xl_ld(&w.tmask[h]);
-      rep = __ffs(msk) - 1 == r;
+  for (int c0 = 0; c0 < N; c0 += kXlUnroll * kXlBlock) {
+    const int eb = c0 + tid * kXlUnroll;
+    uint32_t h[kXlUnroll], msk[kXlUnroll], d[kXlUnroll];
+    int rr[kXlUnroll];
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      h[j] = 0u;
+      d[j] = 0u;
+      if (eb + j < N) {
+        while (base + eb + j >= s_off[r + 1]) ++r;
+        h[j] = w.eslot[eb + j];
+        d[j] = p.docid[base + eb + j];
+      }
+      rr[j] = r;
+    }
+    uint32_t n_rep = 0u, is_rep = 0u;
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      msk[j] = eb + j < N ? xl_ld(&w.tmask[h[j]]) : 0u;
+      const bool rp = eb + j < N && __ffs(msk[j]) - 1 == rr[j];
+      is_rep |= (uint32_t)rp << j;
+      n_rep += rp;
     }
     uint32_t tot;
-    const uint32_t u = U + xl_scan(rep ? 1u : 0u, s_wsum, &tot);
-    if (rep) {
-      w.tu[h] = u;
-      w.umask[u] = msk;
-      p.union_docid[base + u] = xl_ld(&w.tkey[h]);
+    uint32_t u = U + xl_scan(n_rep, s_wsum, &tot);
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      if ((is_rep >> j) & 1u) {
+        w.tu[h[j]] = u;
+        w.umask[u] = msk[j];
+        p.union_docid[base + u] = d[j];  // the entry's own docid (= the table's key)
+        ++u;
+      }
     }
     U += tot;
   }
@@ -2089,11 +2140,30 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   xl_sync();
   QF_STAMP(3);
   r = 0;
-  for (int e = tid; e < N; e += kXlBlock) {
-    while (base + e >= s_off[r + 1]) ++r;
-    const uint32_t u = w.tu[w.eslot[e]];
-    const uint32_t k = w.ugo[u] + (uint32_t)__popc(w.umask[u] & ((1u << r) - 1u));
-    w.gent[k] = (uint32_t)e | ((uint32_t)r << 27);
+  for (int e0 = tid; e0 < N; e0 += kXlUnroll * kXlBlock) {
+    uint32_t hs[kXlUnroll], u[kXlUnroll];
+    int rr[kXlUnroll];
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      hs[j] = 0u;
+      if (e < N) {
+        while (base + e >= s_off[r + 1]) ++r;
+        hs[j] = w.eslot[e];
+      }
+      rr[j] = r;
+    }
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) u[j] = e0 + j * kXlBlock < N ? w.tu[hs[j]] : 0u;
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      if (e < N) {
+        const uint32_t k =
+            w.ugo[u[j]] + (uint32_t)__popc(w.umask[u[j]] & ((1u << rr[j]) - 1u));
+        w.gent[k] = (uint32_t)e | ((uint32_t)rr[j] << 27);
+      }
+    }
   }
   xl_sync();
   QF_STAMP(4);
