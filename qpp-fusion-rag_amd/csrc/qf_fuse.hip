@@ -1986,7 +1986,200 @@ __device__ bool xl_bsort(const FuseParams& p, const double* __restrict__ io, int
     }
     perm_put(p, po + lo + before, BYDOC ? w.su[i] : ti);
   }
+  // (Measured, not kept: these loops four items per thread with their loads first,
+  // as the join's phases — the kernel's spills grow 42 -> 72 VGPRs and the six sorts
+  // of 500 x 16 x top-4000 take 5.08-5.46 ms against 4.74-5.10.)
   xl_sync();  // the workspace is the next slot's
+  return true;
+}
+
+// ---- the workspace join's insert, partitioned ------------------------------------
+// A query's hash table in the workspace is far larger than the caches once 500
+// workgroups run (one ~1 MB table each), so every atomicCAS / atomicOr of the
+// global insert was a random HBM read-modify-write.  Instead: count the entries
+// per hash partition (LDS counters), scatter them by partition (entry | retriever
+// << 27, docid), then join each partition in an LDS table of kXlPartSlots slots
+// and number its distinct documents compactly (c = running count over the
+// partitions).  Outputs as the global insert's: eslot[e] = the document's index c
+// and tmask[c] = its retriever mask, both < U — so the numbering and placement
+// that follow read small arrays.  A partition above kXlPartMax entries returns
+// false (nothing the global insert needs was written) and the global insert runs.
+constexpr int kXlPartBits = 13, kXlPartSlots = 1 << kXlPartBits;  // 64 KB of LDS
+constexpr int kXlPartAvg = 2048;  // entries per partition on average
+constexpr int kXlPartMax = 6144;  // at most 3/4 of the slots
+constexpr int kXlPartRows = kXlPartMax / kXlBlock;
+
+template <int KIND>
+__device__ bool xl_partition_insert(const FuseParams& p, const XlWs& w, int64_t base, int N,
+                                    const int64_t* s_off, uint32_t* lds, uint32_t* s_wsum,
+                                    XlScratch* xs, int* s_status) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int WAVES = kXlBlock / 64;
+  int pbits = 0;
+  while (((int64_t)kXlPartAvg << pbits) < (int64_t)N) ++pbits;
+  const int P = 1 << pbits;  // <= 8,192 counters (N <= 2^24): 32 KB of the 64 KB
+  auto part_of = [&](uint32_t d) -> uint32_t {
+    return pbits ? (d * 0x9E3779B1u) >> (32 - pbits) : 0u;
+  };
+  uint32_t* pcnt = lds;        // [P]: counts, then fill cursors
+  uint32_t* pe = w.tkey;       // [N] entry | retriever << 27, by partition
+  uint32_t* pd = w.tkey + N;   // [N] docid, by partition (the table holds >= 2 N)
+  uint32_t* pstart = w.ugo;    // [P + 1] (free until the group offsets)
+  for (int i = tid; i < P; i += kXlBlock) pcnt[i] = 0u;
+  __syncthreads();
+  // ---- A. count per partition; the list checks of the global insert ----------------
+  int status = 0, r = 0;
+  for (int e0 = tid; e0 < N; e0 += kXlUnroll * kXlBlock) {
+    uint32_t d[kXlUnroll];
+    int rr[kXlUnroll];
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      d[j] = 0u;
+      if (e < N) {
+        while (base + e >= s_off[r + 1]) ++r;
+        d[j] = p.docid[base + e];
+      }
+      rr[j] = r;
+    }
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      if (e < N) {
+        const int64_t g = base + e;
+        if (d[j] == kEmpty) status = QF_QSTATUS_BADDOC;
+        atomicAdd(&pcnt[part_of(d[j])], 1u);
+        if (g + 1 < s_off[rr[j] + 1]) {
+          if ((p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF)) &&
+              ScoreIn<KIND>::raw(p.score, g + 1) > ScoreIn<KIND>::raw(p.score, g))
+            status = QF_QSTATUS_UNSORTED;
+          if ((p.methods & QF_WRRF) && p.rank && p.rank[g + 1] < p.rank[g])
+            status = QF_QSTATUS_RANKORDER;
+        }
+      }
+    }
+  }
+  if (status) atomicMin(s_status, status);
+  __syncthreads();
+  if (*s_status) return true;  // uniform: the caller reports it
+  // ---- B. partition starts (exclusive scan), the largest partition ------------------
+  {
+    const int per = (P + kXlBlock - 1) / kXlBlock;  // counters per thread (<= 8)
+    const int c0 = tid * per;
+    uint32_t tot = 0u, mx = 0u;
+    for (int i = 0; i < per; ++i)
+      if (c0 + i < P) {
+        tot += pcnt[c0 + i];
+        mx = max(mx, pcnt[c0 + i]);
+      }
+    uint32_t all;
+    uint32_t o = xl_scan(tot, s_wsum, &all);  // barriers: every count read first
+    for (int i = 0; i < per; ++i)
+      if (c0 + i < P) {
+        const uint32_t c = pcnt[c0 + i];
+        pstart[c0 + i] = o;
+        pcnt[c0 + i] = o;
+        o += c;
+      }
+    if (tid == 0) pstart[P] = (uint32_t)N;
+    const bool big = ballot(mx > (uint32_t)kXlPartMax) != 0ull;
+    if (lane == 0) xs->flag[wid] = big ? 1 : 0;
+    __syncthreads();
+    int any = 0;
+    for (int i = 0; i < WAVES; ++i) any |= xs->flag[i];
+    if (any) return false;  // uniform
+  }
+  // ---- C. scatter the entries by partition --------------------------------------------
+  r = 0;
+  for (int e0 = tid; e0 < N; e0 += kXlUnroll * kXlBlock) {
+    uint32_t d[kXlUnroll], pos[kXlUnroll];
+    int rr[kXlUnroll];
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      d[j] = 0u;
+      if (e < N) {
+        while (base + e >= s_off[r + 1]) ++r;
+        d[j] = p.docid[base + e];
+      }
+      rr[j] = r;
+    }
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j)
+      pos[j] = e0 + j * kXlBlock < N ? atomicAdd(&pcnt[part_of(d[j])], 1u) : 0u;
+#pragma unroll
+    for (int j = 0; j < kXlUnroll; ++j) {
+      const int e = e0 + j * kXlBlock;
+      if (e < N) {
+        pe[pos[j]] = (uint32_t)e | ((uint32_t)rr[j] << 27);
+        pd[pos[j]] = d[j];
+      }
+    }
+  }
+  xl_sync();
+  // ---- D. each partition: LDS hash join, compact document numbering ------------------------
+  uint32_t* key = lds;                 // [kXlPartSlots]: docid, then the compact index
+  uint32_t* msk = lds + kXlPartSlots;  // [kXlPartSlots]: retriever mask
+  const int hshift = 32 - pbits - kXlPartBits;  // the hash bits below the partition's
+  uint32_t cbase = 0u;
+  int dup = 0;
+  for (int pp = 0; pp < P; ++pp) {
+    const uint32_t a = pstart[pp], b = pstart[pp + 1];
+    for (int i = tid; i < kXlPartSlots / 4; i += kXlBlock) {
+      ((uint4*)key)[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+      ((uint4*)msk)[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+    uint32_t hh[kXlPartRows], ev[kXlPartRows], dv[kXlPartRows];
+#pragma unroll
+    for (int j = 0; j < kXlPartRows; ++j) {
+      const uint32_t k = a + (uint32_t)(tid + j * kXlBlock);
+      ev[j] = k < b ? pe[k] : 0xFFFFFFFFu;
+      dv[j] = k < b ? pd[k] : kEmpty;
+    }
+#pragma unroll
+    for (int j = 0; j < kXlPartRows; ++j) {
+      if (ev[j] != 0xFFFFFFFFu) {
+        uint32_t h = ((dv[j] * 0x9E3779B1u) >> hshift) & (kXlPartSlots - 1);
+        while (true) {
+          const uint32_t prev = atomicCAS(&key[h], kEmpty, dv[j]);
+          if (prev == kEmpty || prev == dv[j]) break;
+          h = (h + 1) & (kXlPartSlots - 1);
+        }
+        const uint32_t rj = ev[j] >> 27;
+        const uint32_t old = atomicOr(&msk[h], 1u << rj);
+        dup |= (old >> rj) & 1u;
+        hh[j] = h;
+      }
+    }
+    __syncthreads();
+    // compact index of each occupied slot, in slot order
+    constexpr int kPer = kXlPartSlots / kXlBlock;  // 8
+    const int s0 = tid * kPer;
+    uint32_t occ = 0u, n_occ = 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const bool o = key[s0 + i] != kEmpty;
+      occ |= (uint32_t)o << i;
+      n_occ += o;
+    }
+    uint32_t all;
+    uint32_t c = cbase + xl_scan(n_occ, s_wsum, &all);  // barriers: every key read first
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      if ((occ >> i) & 1u) {
+        w.tmask[c] = msk[s0 + i];
+        key[s0 + i] = c++;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kXlPartRows; ++j)
+      if (ev[j] != 0xFFFFFFFFu) w.eslot[ev[j] & 0x7FFFFFFu] = key[hh[j]];
+    cbase += all;
+    __syncthreads();  // the table is the next partition's
+  }
+  if (dup) atomicMin(s_status, QF_QSTATUS_DUPDOC);
+  xl_sync();
   return true;
 }
 
@@ -2015,13 +2208,15 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     s_den[tid] = ranx_den(mx, mn);
     s_rden[tid] = 1.0 / s_den[tid];
   }
+  __syncthreads();  // s_status
+  QF_STAMP(0);
+  // ---- 1. insert: partitioned, else (a partition too large) the global table --------
+  if (!xl_partition_insert<KIND>(p, w, base, N, s_off, (uint32_t*)t_key, s_wsum, xs, s_status)) {
   for (int i = tid; i < TS; i += kXlBlock) {
     w.tkey[i] = kEmpty;
     w.tmask[i] = 0u;
   }
   xl_sync();
-  QF_STAMP(0);
-  // ---- 1. insert --------------------------------------------------------------
   // kXlUnroll entries per thread per step, each phase's loads / atomics for all of
   // them issued before any result is used: the L2 atomic round trips overlap
   // (one entry per step left every thread waiting on one chain at a time)
@@ -2078,6 +2273,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   }
   if (status) atomicMin(s_status, status);
   xl_sync();
+  }
   QF_STAMP(1);
   if (*s_status) {  // uniform
     if (tid == 0) p.union_count[q] = *s_status;
@@ -2088,7 +2284,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   // chunks of kXlUnroll * kXlBlock entries, kXlUnroll consecutive ones per thread (in
   // entry order: thread t's precede thread t + 1's), one block scan per chunk
   uint32_t U = 0;
-  r = 0;
+  int r = 0;
   for (int c0 = 0; c0 < N; c0 += kXlUnroll * kXlBlock) {
     const int eb = c0 + tid * kXlUnroll;
     uint32_t h[kXlUnroll], msk[kXlUnroll], d[kXlUnroll];

@@ -814,6 +814,7 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
                               !qid_off || !qid_chars || !docno_off || !docno_chars || !tag)))
     return fail(QFIO_EINVAL, "qfio_write_run: bad arguments");
   if (n_threads > 0) omp_set_num_threads(n_threads);
+  PhaseTimer tm;
   const size_t tl = strlen(tag);
   const int T = std::max(1, omp_get_max_threads());
   const int64_t chunks = std::min<int64_t>(std::max<int64_t>(n_out, 1), (int64_t)T * 8);
@@ -883,6 +884,7 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
     for (char* p : buf) free(p);
     return fail(QFIO_EIO, "qfio_write_run: out of memory");
   }
+  tm.mark("write: format");
   std::vector<off_t> at((size_t)chunks + 1, 0);
   for (int64_t c = 0; c < chunks; ++c) at[(size_t)c + 1] = at[(size_t)c] + (off_t)len[(size_t)c];
   const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
@@ -891,6 +893,9 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
     return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(errno));
   }
   int werr = 0;
+  // (Measured, not kept: the file sized once, mapped, and every chunk copied in by
+  // its own thread — 0.145-0.185 s per 390 MB run on the GPU box's host, the same as
+  // these pwrites' 0.144-0.173 s: the page-cache copy is the bound either way.)
 #pragma omp parallel for schedule(dynamic, 1) reduction(| : werr)
   for (int64_t c = 0; c < chunks; ++c) {
     size_t done = 0;
@@ -903,7 +908,9 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
     free(buf[(size_t)c]);
     buf[(size_t)c] = nullptr;
   }
+  tm.mark("write: pwrite");
   if (close(fd) != 0 || werr) return fail(QFIO_EIO, std::string("short write to ") + path);
+  tm.mark("write: close");
   return QFIO_OK;
 }
 
