@@ -324,7 +324,8 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     size_t o = start[b];
     for (int t = 0; t < T; ++t) { at[t][b] = o; o += cnt[t][b]; }
   }
-  std::vector<uint32_t> rows(n);
+  RawArray<uint32_t> rows;  // uninitialised: the scatter writes every element
+  rows.resize(n);
 #pragma omp parallel for schedule(static)
   for (int t = 0; t < T; ++t)
     for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) rows[at[t][hs[i] >> 56]++] = (uint32_t)i;
@@ -333,7 +334,8 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   // new distinct string's sort key is made while its bytes are in cache
   std::vector<std::vector<uint32_t>> ufirst(P);  // first row of each distinct string
   std::vector<std::vector<Key>> ukey(P);
-  std::vector<uint32_t> local(n);
+  RawArray<uint32_t> local;
+  local.resize(n);
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < P; ++b) {
     const size_t a0 = start[b], a1 = start[b + 1], m = a1 - a0;
@@ -343,6 +345,8 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     std::vector<uint32_t> tab(cap, 0xFFFFFFFFu);
     auto& uf = ufirst[b];
     auto& uk = ukey[b];
+    uf.reserve(m);  // at most m distinct: no regrowth copies
+    uk.reserve(m);
     for (size_t k = a0; k < a1; ++k) {
       const uint32_t i = rows[k];
       size_t h = (size_t)hs[i] & (cap - 1);
@@ -365,12 +369,14 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   std::vector<size_t> ubase(P + 1, 0);
   for (int b = 0; b < P; ++b) ubase[b + 1] = ubase[b] + ufirst[b].size();
   const size_t U = ubase[P];
-  std::vector<uint32_t> reps(U);  // row of each distinct string
-  std::vector<Key> keys(U);
+  RawArray<uint32_t> reps;  // row of each distinct string
+  RawArray<Key> keys;
+  reps.resize(U);
+  keys.resize(U);
   // Sort the distinct strings by byte order (== Python's str order for UTF-8).
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < P; ++b) {
-    std::copy(ufirst[b].begin(), ufirst[b].end(), reps.begin() + (long)ubase[b]);
+    std::copy(ufirst[b].begin(), ufirst[b].end(), reps.data() + ubase[b]);
     Key* kd = keys.data() + ubase[b];
     for (size_t j = 0; j < ukey[b].size(); ++j) {
       kd[j] = ukey[b][j];
@@ -386,9 +392,10 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   // (Measured, not kept: sampled range buckets — 4,096 splitters, a binary search
   // per key, a counting scatter, per-bucket sorts — 115 ms on the GPU box's host
   // against the parallel sort's ~65 ms for C2's 8.6 M distinct docnos.)
-  __gnu_parallel::sort(keys.begin(), keys.end(), less);
+  __gnu_parallel::sort(keys.data(), keys.data() + U, less);
   tm.mark("  sort distinct");
-  std::vector<uint32_t> rank(U);
+  RawArray<uint32_t> rank;
+  rank.resize(U);
   uniq.resize(U);
 #pragma omp parallel for schedule(static)
   for (size_t k = 0; k < U; ++k) {
