@@ -129,6 +129,16 @@ inline std::string_view sv(const SV& v) { return std::string_view(v.p, v.n); }
 inline std::string_view sv(std::string_view v) { return v; }
 
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+// is_space as a table (the parse's per-byte test)
+struct SpaceTable {
+  bool t[256];
+  constexpr SpaceTable() : t{} {
+    t[(unsigned char)' '] = t[(unsigned char)'\t'] = t[(unsigned char)'\r'] = true;
+    t[(unsigned char)'\v'] = t[(unsigned char)'\f'] = true;
+  }
+  constexpr bool operator[](unsigned char c) const { return t[c]; }
+};
+constexpr SpaceTable kSpace{};
 
 // [-]digits[.digits<=6] that fits int32 micro-units; "-0.000000" (which parses
 // to -0.0) is excluded.
@@ -221,15 +231,18 @@ bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micr
     std::string_view f[7];
     int nf = 0;
     const char* line = p;
-    while (p < end && *p != '\n') {
-      while (p < end && is_space(*p)) ++p;
-      if (p >= end || *p == '\n') break;
+    // the line's end first (memchr), then the fields inside it by a table lookup
+    const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+    const char* e = nl ? nl : end;
+    while (true) {
+      while (p < e && kSpace[(unsigned char)*p]) ++p;
+      if (p >= e) break;
       const char* s = p;
-      while (p < end && *p != '\n' && !is_space(*p)) ++p;
+      while (p < e && !kSpace[(unsigned char)*p]) ++p;
       if (nf < 7) f[nf] = std::string_view(s, (size_t)(p - s));
       ++nf;
     }
-    if (p < end) ++p;  // '\n'
+    p = nl ? nl + 1 : end;
     if (nf == 0) continue;  // blank line (pandas skips it)
     if (nf != 6) {
       err = "expected 6 fields (qid Q0 docno rank score tag), got " + std::to_string(nf) +
