@@ -13,7 +13,7 @@ for i in $(seq ${REPS:-3}); do
 import csv, glob, sys
 O, n = sys.argv[1], sys.argv[2]
 f = glob.glob(f'{O}/{n}/**/run_kernel_stats.csv', recursive=True)[0]
-print(n, {r['Name'].split('(')[0].split('::')[-1][:22]: round(float(r['AverageNs'])/1e3, 1)
+import re; dg = re.findall(r"ok ([0-9a-f]{16})", open(f"{O}/{n}.log").read()); print(n, dg, {r['Name'].split('(')[0].split('::')[-1][:22]: round(float(r['AverageNs'])/1e3, 1)
           for r in csv.DictReader(open(f)) if 'sort' in r['Name'] or 'join' in r['Name']})
 PY
   done

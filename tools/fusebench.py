@@ -19,4 +19,9 @@ out = engine.alloc_fuse_out(Q, Q * R * K, engine.methods_mask(M), dev)
 for _ in range(5):
     engine.fuse(off, docid, micro, R, M, weights=w, max_entries=R * K, out=out)
 torch.cuda.synchronize()
-print("ok")
+# a digest of the outputs (union sizes + every ranked list): equal across libraries
+# means the same results
+import hashlib
+h = hashlib.sha256(out.union_count.cpu().numpy().tobytes())
+h.update(out.ranked_fused().cpu().numpy().tobytes())
+print("ok", h.hexdigest()[:16])
