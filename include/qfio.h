@@ -72,6 +72,14 @@ void qfio_runset_free(qfio_runset* rs);
  * with out_chars = NULL).  Returns the byte count, -1 on bad arguments. */
 int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
                             int64_t n, int64_t* out_off, char* out_chars);
+/* the bytes of a column whose out_off[n+1] a first qfio_gather_strings call
+ * (out_chars = NULL, same codes) has filled: one pass instead of a second
+ * qfio_gather_strings.  Returns 0, -1 on bad arguments. */
+int qfio_gather_chars(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
+                      int64_t n, const int64_t* out_off, char* out_chars);
+/* Arrow offsets of n repeats of one len-byte string: out_off[i] = i * len, i <= n
+ * (a column of one value: iter "Q0", a run's tag). */
+void qfio_repeat_offsets(int64_t len, int64_t n, int64_t* out_off);
 
 /* Python's f"{x:.6f}" of x into out (>= 400 bytes); returns the length. */
 size_t qfio_format_score(double x, char* out);

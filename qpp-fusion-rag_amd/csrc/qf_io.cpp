@@ -15,6 +15,7 @@
 // Python's correctly rounded formatting: the exact binary value decides, ties
 // to even — done in integers (micro-units, fma sign tests as the device's
 // round6) for |x| < 2^33 and by snprintf (glibc, also exact) otherwise.
+#include <emmintrin.h>
 #include <fcntl.h>
 #include <omp.h>
 #include <sys/mman.h>
@@ -205,27 +206,68 @@ inline uint64_t hash_sv(std::string_view v) {  // FNV-1a + avalanche
   return h;
 }
 
+// The parse's docno hash (consistent within one load; intern() partitions and
+// probes by it): 8 bytes per multiply instead of FNV's one.
+inline uint64_t hash_words(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    h = (h ^ w) * 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  if (i < n) {
+    uint64_t w = 0;
+    memcpy(&w, p + i, n - i);
+    h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 29;
+  }
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  return h;
+}
+
+// Whitespace bytes (' ' and \t \n \v \f \r) of 16 bytes at p, as a bit mask.
+inline uint32_t ws_mask16(const char* p) {
+  const __m128i c = _mm_loadu_si128((const __m128i*)p);
+  const __m128i sp = _mm_cmpeq_epi8(c, _mm_set1_epi8(' '));
+  const __m128i x = _mm_sub_epi8(c, _mm_set1_epi8(9));
+  const __m128i ctl = _mm_cmpeq_epi8(_mm_min_epu8(x, _mm_set1_epi8(4)), x);
+  return (uint32_t)_mm_movemask_epi8(_mm_or_si128(sp, ctl));
+}
+
 // Row columns, structure of arrays over all files in file order.  The parse also
-// hashes each docno (its bytes are in cache then) and marks the rows whose qid /
-// iter / tag differs from the row before (run heads: those columns are long runs).
+// hashes each docno (its bytes are in cache then).  qid / iter / tag are long runs
+// of one value: only their run heads (a row whose value differs from the row
+// before, or a chunk's first row) are kept, per parse chunk — 44 bytes per row
+// written instead of 95 (the columns are fresh pages: every byte is a page-fault
+// byte too).
+struct Head {
+  size_t row;
+  SV v;
+};
+struct Heads {
+  std::vector<Head> q, it, tag;
+};
 struct Cols {
-  RawArray<SV> q, d, it, tag;
+  RawArray<SV> d;
   RawArray<int64_t> rank;
   RawArray<double> score;
   RawArray<int32_t> micro;
-  RawArray<uint64_t> dh;                 // docno hashes
-  RawArray<uint8_t> qh, ith, tagh;       // run heads
+  RawArray<uint64_t> dh;  // docno hashes
   void resize(size_t n) {
-    q.resize(n); d.resize(n); it.resize(n); tag.resize(n);
+    d.resize(n);
     rank.resize(n); score.resize(n); micro.resize(n);
-    dh.resize(n); qh.resize(n); ith.resize(n); tagh.resize(n);
+    dh.resize(n);
   }
 };
 
 // Parse [begin, end) of a mapped file (whole lines) into rows o, o+1, ...;
 // returns the number of rows whose score is not an exact 6-decimal number.
-bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micro_bad,
-                 std::string& err) {
+bool parse_chunk(const char* p, const char* end, const char* map_end, Cols& c, Heads& h,
+                 size_t o, size_t& micro_bad, std::string& err) {
   std::string_view pq, pit, ptag;  // the previous row's (a chunk's first row is a head)
   bool first = true;
   while (p < end) {
@@ -235,13 +277,32 @@ bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micr
     // the line's end first (memchr), then the fields inside it by a table lookup
     const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
     const char* e = nl ? nl : end;
-    while (true) {
-      while (p < e && kSpace[(unsigned char)*p]) ++p;
-      if (p >= e) break;
-      const char* s = p;
-      while (p < e && !kSpace[(unsigned char)*p]) ++p;
-      if (nf < 7) f[nf] = std::string_view(s, (size_t)(p - s));
-      ++nf;
+    const size_t len = (size_t)(e - p);
+    if (len < 64 && (size_t)(map_end - p) >= 64) {
+      // the fields from a whitespace bit mask of the line (16-byte loads that stay
+      // inside the mapping; bits past the line count as whitespace)
+      uint64_t ws = 0;
+      for (size_t k = 0; k < len; k += 16) ws |= (uint64_t)ws_mask16(p + k) << k;
+      ws |= ~0ull << len;
+      uint64_t st = ~ws & ((ws << 1) | 1u);  // first byte of a field
+      uint64_t en = ws & (~ws << 1);         // first byte after a field
+      nf = __builtin_popcountll(st);
+      for (int k = 0; k < nf && k < 7; ++k) {
+        const int a = __builtin_ctzll(st), b = __builtin_ctzll(en);
+        f[k] = std::string_view(p + a, (size_t)(b - a));
+        st &= st - 1;
+        en &= en - 1;
+      }
+    } else {
+      const char* q = p;
+      while (true) {
+        while (q < e && kSpace[(unsigned char)*q]) ++q;
+        if (q >= e) break;
+        const char* s = q;
+        while (q < e && !kSpace[(unsigned char)*q]) ++q;
+        if (nf < 7) f[nf] = std::string_view(s, (size_t)(q - s));
+        ++nf;
+      }
     }
     p = nl ? nl + 1 : end;
     if (nf == 0) continue;  // blank line (pandas skips it)
@@ -250,14 +311,11 @@ bool parse_chunk(const char* p, const char* end, Cols& c, size_t o, size_t& micr
             " in line: " + std::string(line, std::min<size_t>(120, (size_t)(p - line)));
       return false;
     }
-    c.q[o] = SV{f[0].data(), f[0].size()};
-    c.it[o] = SV{f[1].data(), f[1].size()};
     c.d[o] = SV{f[2].data(), f[2].size()};
-    c.tag[o] = SV{f[5].data(), f[5].size()};
-    c.dh[o] = hash_sv(f[2]);
-    c.qh[o] = first || f[0] != pq;
-    c.ith[o] = first || f[1] != pit;
-    c.tagh[o] = first || f[5] != ptag;
+    c.dh[o] = hash_words(f[2].data(), f[2].size());
+    if (first || f[0] != pq) h.q.push_back(Head{o, SV{f[0].data(), f[0].size()}});
+    if (first || f[1] != pit) h.it.push_back(Head{o, SV{f[1].data(), f[1].size()}});
+    if (first || f[5] != ptag) h.tag.push_back(Head{o, SV{f[5].data(), f[5].size()}});
     pq = f[0]; pit = f[1]; ptag = f[5];
     first = false;
     // rank: [+-]digits (strtoll's accepted form for plain integer text)
@@ -423,35 +481,21 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
 }
 
 // intern() for columns made of long runs of one value (qid, Q0, tag): only the
-// run heads are interned.
-// head[i]: row i differs from row i - 1 (or starts a parse chunk: a head too many
-// costs nothing but one more string to intern).
-template <class Views>
-void intern_runs(const Views& views, const uint8_t* head, std::vector<std::string_view>& uniq,
-                 RawArray<uint32_t>& id) {
-  const size_t n = views.size();
-  const int T = std::max(1, omp_get_max_threads());
-  std::vector<size_t> nh(T + 1, 0);
-#pragma omp parallel for schedule(static)
-  for (int t = 0; t < T; ++t) {
-    size_t c = 0;
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) c += head[i] | (i == 0);
-    nh[t + 1] = c;
-  }
-  for (int t = 0; t < T; ++t) nh[t + 1] += nh[t];
-  if (nh[T] * 4 > n) {  // not run-structured
-    intern(views, uniq, id);
-    return;
-  }
-  std::vector<size_t> hix(nh[T]);
-#pragma omp parallel for schedule(static)
-  for (int t = 0; t < T; ++t) {
-    size_t o = nh[t];
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i)
-      if (head[i] | (i == 0)) hix[o++] = i;
-  }
-  std::vector<std::string_view> hv(hix.size());
-  for (size_t k = 0; k < hix.size(); ++k) hv[k] = sv(views[hix[k]]);
+// run heads the parse kept are interned (a head too many — a chunk's first row —
+// costs one more string), then every row takes its run's id.
+void intern_runs(const std::vector<Heads>& heads, std::vector<Head> Heads::*which, size_t n,
+                 std::vector<std::string_view>& uniq, RawArray<uint32_t>& id) {
+  std::vector<size_t> hix;
+  std::vector<std::string_view> hv;
+  size_t nh = 0;
+  for (const Heads& h : heads) nh += (h.*which).size();
+  hix.reserve(nh);
+  hv.reserve(nh);
+  for (const Heads& h : heads)  // chunks in row order
+    for (const Head& x : h.*which) {
+      hix.push_back(x.row);
+      hv.push_back(sv(x.v));
+    }
   RawArray<uint32_t> hid;
   intern(hv, uniq, hid);
   id.resize(n);
@@ -560,10 +604,12 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   tm.mark("alloc columns");
   std::vector<std::string> errs(NC);
   std::vector<size_t> mbad(NC, 0);
+  std::vector<Heads> heads(NC);
 #pragma omp parallel for schedule(dynamic, 1)
   for (size_t k = 0; k < NC; ++k) {
     const size_t f = k / T, t = k % T;
-    parse_chunk(cut[f * (T + 1) + t], cut[f * (T + 1) + t + 1], cols, nrow[k], mbad[k], errs[k]);
+    parse_chunk(cut[f * (T + 1) + t], cut[f * (T + 1) + t + 1], cut[f * (T + 1) + T], cols, heads[k],
+                nrow[k], mbad[k], errs[k]);
   }
   tm.mark("parse");
   for (size_t k = 0; k < NC; ++k)
@@ -579,12 +625,12 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->row_score = std::move(cols.score);
   RawArray<int32_t> row_micro = std::move(cols.micro);
   // ---- intern qids / docnos / iter / tag ---------------------------------------
-  intern_runs(cols.q, cols.qh.data(), rs->qids, rs->row_qid);
+  intern_runs(heads, &Heads::q, E, rs->qids, rs->row_qid);
   tm.mark("intern qid");
   intern(cols.d, rs->docnos, rs->row_docid, cols.dh.data());
   tm.mark("intern docno");
-  intern_runs(cols.it, cols.ith.data(), rs->iters, rs->row_iter);
-  intern_runs(cols.tag, cols.tagh.data(), rs->tags, rs->row_tag);
+  intern_runs(heads, &Heads::it, E, rs->iters, rs->row_iter);
+  intern_runs(heads, &Heads::tag, E, rs->tags, rs->row_tag);
   tm.mark("intern iter/tag");
   if (rs->docnos.size() >= 0xFFFFFFFFull) { delete rs; return fail(QFIO_EINVAL, "too many docnos"); }
   // ---- CSR by (query, file), stable in file order -------------------------------
@@ -781,6 +827,21 @@ extern "C" {
 int64_t qfio_gather_strings(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
                             int64_t n, int64_t* out_off, char* out_chars) {
   return gather_strings(tab_off, tab_chars, codes, n, out_off, out_chars);
+}
+
+int qfio_gather_chars(const int64_t* tab_off, const char* tab_chars, const uint32_t* codes,
+                      int64_t n, const int64_t* out_off, char* out_chars) {
+  if (n < 0 || (n && (!tab_off || !tab_chars || !codes || !out_off || !out_chars))) return -1;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i)
+    memcpy(out_chars + out_off[i], tab_chars + tab_off[codes[i]], (size_t)(out_off[i + 1] - out_off[i]));
+  return 0;
+}
+
+void qfio_repeat_offsets(int64_t len, int64_t n, int64_t* out_off) {
+  if (n < 0 || !out_off) return;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i <= n; ++i) out_off[i] = i * len;
 }
 
 void qfio_runset_free(qfio_runset* rs) { delete rs; }

@@ -47,6 +47,10 @@ def lib() -> C.CDLL:
         L.qfio_join_lines.argtypes = [_vp, _vp, _i64, _vp]
         L.qfio_gather_strings.restype = _i64
         L.qfio_gather_strings.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp]
+        L.qfio_gather_chars.restype = C.c_int
+        L.qfio_gather_chars.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp]
+        L.qfio_repeat_offsets.restype = None
+        L.qfio_repeat_offsets.argtypes = [_i64, _i64, _vp]
         L.qfio_runset_drop_text.restype = None
         L.qfio_runset_drop_text.argtypes = [_vp]
         L.qfio_runset_views.restype = None
@@ -119,19 +123,20 @@ def arrow_strings(off: np.ndarray, chars: np.ndarray, codes: np.ndarray):
     import pyarrow as pa
     codes = np.ascontiguousarray(codes, np.uint32)
     n = len(codes)
-    if n and codes[0] == codes[-1] and (codes == codes[0]).all():
-        v = bytes(chars[off[codes[0]]:off[codes[0] + 1]])
-        o = np.arange(n + 1, dtype=np.int64) * len(v)
-        arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(o), pa.py_buffer(v * n))
-        return pd.arrays.ArrowStringArray(pa.chunked_array([arr]))
-    # large_string (int64 offsets): what pandas' ArrowStringArray holds, so no cast
     L = lib()
     out_off = np.empty(n + 1, np.int64)
+    if n and codes[0] == codes[-1] and (codes == codes[0]).all():
+        v = bytes(chars[off[codes[0]]:off[codes[0] + 1]])
+        L.qfio_repeat_offsets(len(v), n, _p(out_off))
+        arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(out_off), pa.py_buffer(v * n))
+        return pd.arrays.ArrowStringArray(pa.chunked_array([arr]))
+    # large_string (int64 offsets): what pandas' ArrowStringArray holds, so no cast
     nb = L.qfio_gather_strings(_p(off), _p(chars), _p(codes), n, _p(out_off), None)
     if nb < 0:
         raise ValueError("gather_strings: bad arguments")
     buf = np.empty(max(int(nb), 1), np.uint8)
-    L.qfio_gather_strings(_p(off), _p(chars), _p(codes), n, _p(out_off), _p(buf))
+    if L.qfio_gather_chars(_p(off), _p(chars), _p(codes), n, _p(out_off), _p(buf)) != 0:
+        raise ValueError("gather_chars: bad arguments")
     arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(out_off), pa.py_buffer(buf[:nb]))
     return pd.arrays.ArrowStringArray(pa.chunked_array([arr]))
 

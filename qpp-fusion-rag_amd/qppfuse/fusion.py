@@ -291,14 +291,32 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
         code = int(counts[bad[0]])
         raise ValueError(f"query '{rs.qids[bad[0]]}': {QF_QSTATUS.get(code, code)}")
     E = rs.n_entries
-    udoc = out.union_docid.cpu().numpy()[:E].view(np.uint32)
-    perm = out.perm.cpu().numpy()[:, :E].view(np.uint32 if out.wide else np.uint16)
-    fused = out.fused.cpu().numpy()[:, :E]
+    qbase = rs.query_base()
+    total = int(counts.sum())
+    if 0 < total < E:
+        # only the unions cross PCIe: query q's U_q slots of every output, gathered
+        # on the device into consecutive ranges (C2: 0.55 GB instead of 1.1 GB);
+        # perm holds union positions, so it is unchanged
+        dev = out.union_count.device
+        cnt = torch.from_numpy(counts.astype(np.int64)).to(dev)
+        cb = torch.cumsum(cnt, 0) - cnt  # compact base of each query
+        qb = torch.from_numpy(np.ascontiguousarray(qbase, np.int64)).to(dev)
+        q_of = torch.repeat_interleave(torch.arange(len(counts), device=dev), cnt,
+                                       output_size=total)
+        idx = qb[q_of] + (torch.arange(total, device=dev) - cb[q_of])
+        udoc = out.union_docid[idx].cpu().numpy().view(np.uint32)
+        perm = out.perm[:, idx].cpu().numpy().view(np.uint32 if out.wide else np.uint16)
+        fused = out.fused[:, idx].cpu().numpy()
+        qbase = cb.cpu().numpy()
+    else:
+        udoc = out.union_docid.cpu().numpy()[:E].view(np.uint32)
+        perm = out.perm.cpu().numpy()[:, :E].view(np.uint32 if out.wide else np.uint16)
+        fused = out.fused.cpu().numpy()[:, :E]
     res = {}
     for m, name in enumerate(out.methods):
         order = ("sorted" if name in UNWEIGHTED else "docno" if name == "learned"
                  else "first_seen")
-        res[name] = FusedRun(rs.qids, rs.docnos, rs.query_base(), counts, udoc, perm[m],
+        res[name] = FusedRun(rs.qids, rs.docnos, qbase, counts, udoc, perm[m],
                              fused[m], order, rs)
     return res
 
