@@ -420,6 +420,13 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     uf.reserve(m);  // at most m distinct: no regrowth copies
     uk.reserve(m);
     for (size_t k = a0; k < a1; ++k) {
+      // the partition's rows are scattered over the columns and the text: their
+      // hash and view prefetched 16 rows ahead, the text 8 rows ahead
+      if (k + 16 < a1) {
+        __builtin_prefetch(&hs[rows[k + 16]]);
+        __builtin_prefetch(&views[rows[k + 16]]);
+      }
+      if (k + 8 < a1) __builtin_prefetch(sv(views[rows[k + 8]]).data());
       const uint32_t i = rows[k];
       size_t h = (size_t)hs[i] & (cap - 1);
       while (true) {
@@ -483,8 +490,10 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
 // intern() for columns made of long runs of one value (qid, Q0, tag): only the
 // run heads the parse kept are interned (a head too many — a chunk's first row —
 // costs one more string), then every row takes its run's id.
+// head_rows / head_ids (optional): the runs (first row, id), in row order.
 void intern_runs(const std::vector<Heads>& heads, std::vector<Head> Heads::*which, size_t n,
-                 std::vector<std::string_view>& uniq, RawArray<uint32_t>& id) {
+                 std::vector<std::string_view>& uniq, RawArray<uint32_t>& id,
+                 std::vector<size_t>* head_rows = nullptr, RawArray<uint32_t>* head_ids = nullptr) {
   std::vector<size_t> hix;
   std::vector<std::string_view> hv;
   size_t nh = 0;
@@ -504,6 +513,8 @@ void intern_runs(const std::vector<Heads>& heads, std::vector<Head> Heads::*whic
     const size_t e = k + 1 < hix.size() ? hix[k + 1] : n;
     for (size_t i = hix[k]; i < e; ++i) id[i] = hid[k];
   }
+  if (head_rows) *head_rows = std::move(hix);
+  if (head_ids) *head_ids = std::move(hid);
 }
 
 }  // namespace
@@ -625,7 +636,9 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->row_score = std::move(cols.score);
   RawArray<int32_t> row_micro = std::move(cols.micro);
   // ---- intern qids / docnos / iter / tag ---------------------------------------
-  intern_runs(heads, &Heads::q, E, rs->qids, rs->row_qid);
+  std::vector<size_t> qrun_row;  // runs of one qid (no run crosses a file: a file's
+  RawArray<uint32_t> qrun_id;    // first row starts a parse chunk, hence a run)
+  intern_runs(heads, &Heads::q, E, rs->qids, rs->row_qid, &qrun_row, &qrun_id);
   tm.mark("intern qid");
   intern(cols.d, rs->docnos, rs->row_docid, cols.dh.data());
   tm.mark("intern docno");
@@ -634,26 +647,43 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   tm.mark("intern iter/tag");
   if (rs->docnos.size() >= 0xFFFFFFFFull) { delete rs; return fail(QFIO_EINVAL, "too many docnos"); }
   // ---- CSR by (query, file), stable in file order -------------------------------
+  // from the qid runs: counts per list, each run's destination in run (= row)
+  // order, then the runs copied in parallel
   const int64_t Q = (int64_t)rs->qids.size(), R = n_files;
+  const size_t NR = qrun_row.size();
+  std::vector<int64_t> rlist(NR), rlen(NR), rdst(NR);
   std::vector<int64_t> cnt(Q * R + 1, 0);
-  for (int f = 0; f < n_files; ++f)
-    for (int64_t i = rs->file_off[f]; i < rs->file_off[f + 1]; ++i) ++cnt[(int64_t)rs->row_qid[i] * R + f];
+  {
+    int f = 0;
+    for (size_t k = 0; k < NR; ++k) {
+      const int64_t a = (int64_t)qrun_row[k], e = k + 1 < NR ? (int64_t)qrun_row[k + 1] : (int64_t)E;
+      while (a >= rs->file_off[f + 1]) ++f;
+      rlist[k] = (int64_t)qrun_id[k] * R + f;
+      rlen[k] = e - a;
+      cnt[rlist[k]] += rlen[k];
+    }
+  }
   rs->list_off.assign(Q * R + 1, 0);
   for (int64_t k = 0; k < Q * R; ++k) rs->list_off[k + 1] = rs->list_off[k] + cnt[k];
-  std::vector<int64_t> pos(rs->list_off.begin(), rs->list_off.end() - 1);
+  {
+    std::vector<int64_t> pos(rs->list_off.begin(), rs->list_off.end() - 1);
+    for (size_t k = 0; k < NR; ++k) {
+      rdst[k] = pos[rlist[k]];
+      pos[rlist[k]] += rlen[k];
+    }
+  }
   rs->docid.resize(E);
   rs->score.resize(E);
   rs->rank.resize(E);
   rs->micro.resize(rs->micro_ok ? E : 0);
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int f = 0; f < n_files; ++f)
-    for (int64_t i = rs->file_off[f]; i < rs->file_off[f + 1]; ++i) {
-      const int64_t d = pos[(int64_t)rs->row_qid[i] * R + f]++;
-      rs->docid[d] = rs->row_docid[i];
-      rs->score[d] = rs->row_score[i];
-      rs->rank[d] = rs->row_rank[i];
-      if (rs->micro_ok) rs->micro[d] = row_micro[i];
-    }
+#pragma omp parallel for schedule(dynamic, 16)
+  for (size_t k = 0; k < NR; ++k) {
+    const int64_t a = (int64_t)qrun_row[k], d = rdst[k], n = rlen[k];
+    memcpy(&rs->docid[d], &rs->row_docid[a], (size_t)n * sizeof(uint32_t));
+    memcpy(&rs->score[d], &rs->row_score[a], (size_t)n * sizeof(double));
+    memcpy(&rs->rank[d], &rs->row_rank[a], (size_t)n * sizeof(int64_t));
+    if (rs->micro_ok) memcpy(&rs->micro[d], &row_micro[a], (size_t)n * sizeof(int32_t));
+  }
   // list properties the device path keys on (qppfuse/runset.py _analyse): the
   // rank column is position + 1; every list is score-descending with rising ranks
   // and whether a docno repeats inside one list (open addressing per list)
