@@ -270,3 +270,36 @@ def test_pack_cache_follows_edits_of_arrow_frames(tmp_path, monkeypatch):
     c = fusion._pack(frames)
     assert c is not b and 123.0 in c.score
     assert fusion._pack(frames) is c
+
+
+def test_parse_line_shapes_against_pandas(tmp_path):
+    """Lines the SIMD field split does not take (>= 64 bytes, the mapping's last 64
+    bytes) next to ones it does; CRLF, tab separators, no final newline,
+    and a qid whose rows come in two separate runs of one file (its list keeps the
+    file order of both runs)."""
+    long_doc = "doc-" + "x" * 70
+    rows_a = [
+        "q1 Q0 d1 1 0.900000 A\r\n",
+        f"q1 Q0 {long_doc} 2 0.800000 A\r\n",
+        "q2\tQ0\td2 1 0.700000 A\n",
+        "q1 Q0 d3 3 0.600000\tA\n",   # q1 again, after q2: a second run of q1
+        "q2 Q0 d1 2 0.500000 A\n",
+        f"q3 Q0 {long_doc}y 1 0.400000 A",  # no final newline
+    ]
+    rows_b = ["q2 Q0 d9 1 0.300000 B\n", "q1 Q0 d1 1 0.200000 B\n"]
+    pa_, pb_ = tmp_path / "A.res", tmp_path / "B.res"
+    pa_.write_text("".join(rows_a))
+    pb_.write_text("".join(rows_b))
+    paths, names = [str(pa_), str(pb_)], ["A", "B"]
+    for threads in (1, 3):
+        rs, frames = fastio.parse_runs(paths, names, n_threads=threads)
+        pf = _pandas_frames(paths, names)
+        ref = pack_frames(pf)
+        assert rs.qids == ref.qids and list(rs.docnos) == list(ref.docnos)
+        np.testing.assert_array_equal(rs.list_off, ref.list_off)
+        np.testing.assert_array_equal(rs.docid, ref.docid)
+        assert rs.score.tobytes() == ref.score.tobytes()
+        np.testing.assert_array_equal(rs.rank, ref.rank)
+        for n in names:
+            for c in ("qid", "iter", "docno", "runid"):
+                assert frames[n][c].astype(str).tolist() == pf[n][c].astype(str).tolist()
