@@ -138,12 +138,14 @@ class TopkGather:
       pre-filled with docid -1 / NaN; engine.fused_topk writes this rank's rows
       straight into the first sizes[rank] rows (`buffers(i)`), so nothing is
       padded or copied per step;
-    * on `dst`, `depth` receive buffers [world, m, M, k], one contiguous block per
-      set; dist.gather lands every rank's rows in a view of it (the view lists are
-      made once).  result(i) returns per-rank views trimmed to each shard, and a
-      flat [sum(sizes), M, k] view when the shards are equal (no concatenation).
+    * on `dst`, `depth` receive buffers [world, bytes], one contiguous block per
+      set; dist.gather lands every rank's buffer in a row of it (the views are made
+      once).  result(i) returns per-rank (docid, score) views trimmed to each shard.
     With the gloo backend and device tensors (the one-GPU rehearsal) the send and
     receive sides go through preallocated host buffers.
+    A rank's docids and scores share one byte buffer (docids first, the scores at
+    the next 8-byte boundary), so a step is ONE gather (RCCL: one set of
+    point-to-point sends into dst) instead of one per column.
     Step i uses set i % depth: with depth 2 and the pipelined wait (step i waits for
     step i-1's gather before queuing step i+1), a set is never rewritten in flight.
     Bytes per step into dst: world * m * M * k * (4 + 8).
@@ -160,24 +162,33 @@ class TopkGather:
         self.m = max(self.sizes)
         dev = torch.device(device)
         self.host = dist.get_backend(group) == "gloo" and dev.type == "cuda"
-        shape = (self.m, self.M, self.k)
-        self.send_d = [torch.full(shape, -1, dtype=torch.int32, device=dev) for _ in range(depth)]
-        self.send_s = [torch.full(shape, float("nan"), dtype=torch.float64, device=dev)
-                       for _ in range(depth)]
+        cells = self.m * self.M * self.k
+        self._soff = (4 * cells + 7) // 8 * 8  # the scores' byte offset
+        self.nbytes = self._soff + 8 * cells
+        self.send = [torch.empty(self.nbytes, dtype=torch.uint8, device=dev) for _ in range(depth)]
+        for buf in self.send:  # padding rows: docid -1, score NaN (written once)
+            d, s = self._views(buf)
+            d.fill_(-1)
+            s.fill_(float("nan"))
         cdev = torch.device("cpu") if self.host else dev
         if self.host:
-            self.hsend_d = [torch.empty(shape, dtype=torch.int32).pin_memory() for _ in range(depth)]
-            self.hsend_s = [torch.empty(shape, dtype=torch.float64).pin_memory() for _ in range(depth)]
-        self.recv_d = self.recv_s = None
+            self.hsend = [torch.empty(self.nbytes, dtype=torch.uint8).pin_memory()
+                          for _ in range(depth)]
+        self.recv = None
         if self.rank == dst:
-            rshape = (self.world,) + shape
-            self.recv_d = [torch.empty(rshape, dtype=torch.int32, device=cdev) for _ in range(depth)]
-            self.recv_s = [torch.empty(rshape, dtype=torch.float64, device=cdev)
-                           for _ in range(depth)]
-            self._dl = [list(t.unbind(0)) for t in self.recv_d]
-            self._sl = [list(t.unbind(0)) for t in self.recv_s]
+            self.recv = [torch.empty((self.world, self.nbytes), dtype=torch.uint8, device=cdev)
+                         for _ in range(depth)]
+            self._rl = [list(t.unbind(0)) for t in self.recv]
+            self._rv = [[self._views(t[r]) for r in range(self.world)] for t in self.recv]
         n = self.sizes[self.rank]
-        self._out = [(self.send_d[i][:n], self.send_s[i][:n]) for i in range(depth)]
+        self._out = [tuple(v[:n] for v in self._views(buf)) for buf in self.send]
+
+    def _views(self, buf):
+        """(docid int32 [m, M, k], score float64 [m, M, k]) views of one byte buffer."""
+        import torch
+        shape, cells = (self.m, self.M, self.k), self.m * self.M * self.k
+        return (buf[:4 * cells].view(torch.int32).view(shape),
+                buf[self._soff:self._soff + 8 * cells].view(torch.float64).view(shape))
 
     def buffers(self, i: int):
         """(docid, score) [sizes[rank], M, k] views of set i % depth: engine.fused_topk's out."""
@@ -188,29 +199,21 @@ class TopkGather:
         makes the caller's stream wait for it (no host block on RCCL)."""
         import torch.distributed as dist
         j = i % self.depth
-        d, s = self.send_d[j], self.send_s[j]
-        if self.host:  # gloo rehearsal: host buffers (the copies synchronise the stream)
-            self.hsend_d[j].copy_(d)
-            self.hsend_s[j].copy_(s)
-            d, s = self.hsend_d[j], self.hsend_s[j]
+        buf = self.send[j]
+        if self.host:  # gloo rehearsal: host buffers (the copy synchronises the stream)
+            self.hsend[j].copy_(buf)
+            buf = self.hsend[j]
         mine = self.rank == self.dst
-        works = [dist.gather(d, self._dl[j] if mine else None, dst=self.dst, group=self.group,
-                             async_op=True),
-                 dist.gather(s, self._sl[j] if mine else None, dst=self.dst, group=self.group,
-                             async_op=True)]
-        return _TopkHandle(self, j, [w for w in works if w is not None])
+        w = dist.gather(buf, self._rl[j] if mine else None, dst=self.dst, group=self.group,
+                        async_op=True)
+        return _TopkHandle(self, j, [w] if w is not None else [])
 
     def result(self, i: int):
-        """On dst: (per-rank (docid, score) views trimmed to each shard, flat views or
-        None).  The flat [sum(sizes), M, k] views exist when every shard is full size."""
-        if self.recv_d is None:
+        """On dst: per-rank (docid, score) views trimmed to each shard (None elsewhere)."""
+        if self.recv is None:
             return None
         j = i % self.depth
-        per = [(self.recv_d[j][r, :n], self.recv_s[j][r, :n]) for r, n in enumerate(self.sizes)]
-        flat = None
-        if all(n == self.m for n in self.sizes):
-            flat = (self.recv_d[j].view(-1, self.M, self.k), self.recv_s[j].view(-1, self.M, self.k))
-        return per, flat
+        return [(d[:n], s[:n]) for (d, s), n in zip(self._rv[j], self.sizes)]
 
 
 class _TopkHandle:

@@ -47,6 +47,22 @@ def main():
         gd, gs = got
         assert gd.shape == (world * Q, 3, 100)
         assert torch.equal(gd[:Q], d) and torch.equal(gs[:Q].view(torch.int64), s.view(torch.int64))
+    # bench.py's allocation-free form: fused_topk straight into the send buffer
+    # (docids and scores in one byte buffer), one gather per step, two steps pipelined
+    from qppfuse.dist import TopkGather
+    g = TopkGather([Q] * world, 3, 100, dev)
+    pending = None
+    for step in range(2):
+        if pending is not None:
+            pending.wait()
+        engine.fused_topk(out, off, R, 100, dest=g.buffers(step))
+        pending = g.start(step)
+    per = pending.wait()
+    torch.cuda.synchronize()
+    if rank == 0:
+        assert len(per) == world
+        pd_, ps_ = per[0]
+        assert torch.equal(pd_, d) and torch.equal(ps_.view(torch.int64), s.view(torch.int64))
     dist.barrier()
     dist.destroy_process_group()
     print("rccl-ok", flush=True)

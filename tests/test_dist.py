@@ -162,17 +162,16 @@ def _topk_gather_worker(rank, world, port, sizes, M, k, steps, out):
 def _copy(res):
     if res is None:
         return None
-    per, flat = res
-    return ([(d.numpy().copy(), s.numpy().copy()) for d, s in per],
-            None if flat is None else flat[0].numpy().copy())
+    return [(d.numpy().copy(), s.numpy().copy()) for d, s in res]
 
 
 @pytest.mark.parametrize("world,total", [(4, 11157), (2, 10)])
 def test_topk_gather_preallocated_unequal_shards(world, total):
     """dist.TopkGather (bench.py's allocation-free N > 1 gather) with C4's unequal
     shard_range(11157, 4, r) shards (2790, 2789, 2789, 2789) on gloo, world 4:
-    three pipelined steps through the two buffer sets; rank 0 holds every rank's
-    rows, in rank order, trimmed to each shard (a flat view only when equal)."""
+    three pipelined steps through the two buffer sets, one gather per step (docids
+    and scores in one byte buffer); rank 0 holds every rank's rows, in rank order,
+    trimmed to each shard."""
     from qppfuse.dist import shard_range
     sizes = [e - b for b, e in (shard_range(total, world, r) for r in range(world))]
     M, k, steps = 2, 3, 3
@@ -182,12 +181,10 @@ def test_topk_gather_preallocated_unequal_shards(world, total):
              nprocs=world, join=True)
     for r in range(1, world):
         assert out[r] == [None] * steps
-    for step, (per, flat) in enumerate(out[0]):
-        assert (flat is None) == (len(set(sizes)) > 1)
+    for step, per in enumerate(out[0]):
+        assert len(per) == world
         for r, (d, s) in enumerate(per):
             want = np.arange(sizes[r] * M * k, dtype=np.int32).reshape(sizes[r], M, k) \
                 + 100000 * r + 10 * step
             np.testing.assert_array_equal(d, want)
             assert s.tobytes() == (want.astype(np.float64) / 3).tobytes()
-        if flat is not None:
-            np.testing.assert_array_equal(flat, np.concatenate([d for d, _ in per]))
