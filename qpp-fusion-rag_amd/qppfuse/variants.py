@@ -9,6 +9,12 @@ QPPrrf_argmax.py — (weighted) RRF with weight * (1 / (k + rank)) per row
 10_oracle_baseline.py — the oracle upper bound: per query the ranker with the
 best per-query metric (compute_oracle_run, :152-201), its evaluation and the
 selection statistics (:204-254).
+The scripts' evaluation mains — parse_measures (ProbFuse.py:198-222, AP(rel=2)
+for "map"), the argmax / weighted-RRF run lists (QPPrrf_argmax.py:137-160) and
+pyterrier's Experiment table over them — as parse_measures, argmax_runs and
+experiment (means on the device through IREvaluator; pyterrier is absent here,
+so its aggregation is restated as trec_eval's default — the run's queries that
+have qrels — and that parity is unpinned).
 
 The fusions and the per-query metrics run on the device through the same join + sort kernels as the main
 path (qf_fuse_probfuse with QF_PROBFUSE, qf_fuse with QF_WRRF_MUL): the per-row
@@ -24,7 +30,7 @@ from __future__ import annotations
 import math
 import os
 from collections import defaultdict
-from typing import Dict, List, Optional
+from typing import Dict, List, NamedTuple, Optional
 
 import numpy as np
 import pandas as pd
@@ -35,7 +41,8 @@ from .runset import pack_frames
 __all__ = ["pos_to_segment", "load_runs", "train_probfuse", "build_probfuse_run",
            "write_runfile", "load_qpp_estimates", "load_argmax_runs", "build_rrf_run",
            "build_adaptive_run", "load_all_runs", "parse_metric", "compute_per_query_scores",
-           "compute_oracle_run", "evaluate_run", "analyze_oracle_selections"]
+           "compute_oracle_run", "evaluate_run", "analyze_oracle_selections", "model_name_dict",
+           "Measure", "parse_measures", "parse_argmax_measures", "experiment", "argmax_runs"]
 
 
 # ------------------------------------------------------------- probFuse ------
@@ -391,3 +398,113 @@ def analyze_oracle_selections(selections, per_query_scores):
             "n_queries": total,
             "avg_improvement_over_others": np.mean(gains) if gains else 0,
             "max_improvement": max(gains) if gains else 0}
+
+
+# ------------------------------------------------ the scripts' evaluation mains ------
+
+# QPPrrf_argmax.py:9 — the names its per-column runs carry
+model_name_dict = {0: "SMV", 1: "Sigma_max", 2: "Sigma(%)", 3: "NQC", 4: "UEF", 5: "RSD",
+                   6: "QPP-PRP", 7: "WIG", 8: "SCNQC", 9: "QV-NQC", 10: "DM", 11: "NQA-QPP",
+                   12: "BERTQPP"}
+
+
+class Measure(NamedTuple):
+    """One pyterrier measure: its printed name, the IREvaluator metric and the
+    relevance level (judged grades below it count as non-relevant)."""
+    name: str
+    metric: str
+    rel: int = 1
+
+
+def parse_measures(metrics_list) -> List[Measure]:
+    """ProbFuse.py:198-222: map -> AP(rel=2), ndcg[@k] -> nDCG[@k], recip_rank / rr
+    -> RR, p<k> -> P@k; anything else raises ValueError."""
+    out = []
+    for m in metrics_list:
+        mlow = m.lower()
+        if mlow == "map":
+            out.append(Measure("AP(rel=2)", "AP", 2))
+        elif mlow.startswith("ndcg"):
+            if "@" in mlow:
+                k = int(mlow.split("@")[1])
+                out.append(Measure(f"nDCG@{k}", f"nDCG@{k}"))
+            else:
+                out.append(Measure("nDCG", "nDCG"))
+        elif mlow in ("recip_rank", "rr"):
+            out.append(Measure("RR", "RR"))
+        elif mlow.startswith("p"):
+            try:
+                k = int(mlow[1:])
+            except ValueError:
+                raise ValueError(f"Unsupported metric {m}") from None
+            out.append(Measure(f"P@{k}", f"P@{k}"))
+        else:
+            raise ValueError(f"Unsupported metric {m}")
+    return out
+
+
+def parse_argmax_measures(metrics) -> List[Measure]:
+    """QPPrrf_argmax.py:119-131: map -> AP(rel=2), a name containing "ndcg@10" ->
+    nDCG@k, recip_rank -> RR; other names are skipped, as there."""
+    out = []
+    for m in metrics:
+        if m.lower() == "map":
+            out.append(Measure("AP(rel=2)", "AP", 2))
+        elif "ndcg@10" in m.lower():
+            k = int(m.split("@")[1]) if "@" in m else None
+            out.append(Measure(f"nDCG@{k}", f"nDCG@{k}") if k else Measure("nDCG", "nDCG"))
+        elif m.lower() == "recip_rank":
+            out.append(Measure("RR", "RR"))
+    return out
+
+
+def experiment(runs, qrels, measures, names) -> pd.DataFrame:
+    """pyterrier's Experiment(runs, qrels, topics, eval_metrics, names) table as the
+    scripts print it: one row per run (`name`, then one mean per measure).  Runs
+    are DataFrames (qid, docno, score) or {qid: [(docno, score)]}; qrels a
+    {qid: {docno: grade}} dict or a (qid, docno, label) DataFrame."""
+    from .evaluation import IREvaluator
+    if isinstance(qrels, pd.DataFrame):
+        qrels = IREvaluator._convert_qrels(qrels)
+    measures = [m if isinstance(m, Measure) else Measure(str(m), str(m)) for m in measures]
+    by_rel: Dict[int, List[Measure]] = defaultdict(list)
+    for m in measures:
+        by_rel[int(m.rel)].append(m)
+    leveled = {t: (qrels if t <= 1 else
+                   {q: {d: (g if g >= t else 0) for d, g in docs.items()}
+                    for q, docs in qrels.items()})
+               for t in by_rel}
+    rows = []
+    for run, name in zip(runs, names):
+        row = {"name": name}
+        for t, ms in by_rel.items():
+            vals = IREvaluator([m.metric for m in ms]).evaluate(run, leveled[t])
+            for m in ms:
+                row[m.name] = float(vals[m.metric])
+        rows.append(row)
+    return pd.DataFrame(rows, columns=["name"] + [m.name for m in measures])
+
+
+def argmax_runs(strategy: str, runs, qpp_data):
+    """The runs and names QPPrrf_argmax.py's main() evaluates (:137-160): per QPP
+    column an adaptive (argmax) or weighted-RRF run, or one plain RRF run, then
+    every input run as a baseline."""
+    sample_scores = next(iter(next(iter(qpp_data.values())).values()))
+    n = len(sample_scores)
+    all_runs, all_names = [], []
+    if strategy == "adaptive":
+        for i in range(n):
+            all_runs.append(build_adaptive_run(qpp_data, runs, qpp_method_index=i))
+            all_names.append(f"Adaptive-QPP-{model_name_dict[i]}")
+    elif strategy == "wrrf":
+        for i in range(n):
+            all_runs.append(build_rrf_run(runs, qpp_data=qpp_data, qpp_method_index=i))
+            all_names.append(f"Weighted-RRF-QPP-{model_name_dict[i]}")
+    elif strategy == "rrf":
+        all_runs.append(build_rrf_run(runs))
+        all_names.append("RRF")
+    else:
+        raise ValueError(f"strategy must be adaptive, rrf or wrrf, not {strategy!r}")
+    all_runs.extend(runs.values())
+    all_names.extend(runs.keys())
+    return all_runs, all_names

@@ -235,3 +235,40 @@ def test_oracle_baseline_on_device(gpu, metric):
     for m in ms:
         col = list(_oracle_metric(oracle_run, qrels, m).values())
         assert ev[m] == pytest.approx(np.mean(col), rel=1e-12)
+
+
+def test_parse_measures_like_the_scripts():
+    """ProbFuse.py:198-222 and QPPrrf_argmax.py:119-131's measure lists."""
+    from qppfuse.variants import Measure, parse_argmax_measures, parse_measures
+    assert parse_measures(["map", "ndcg@10", "recip_rank", "p5", "ndcg", "rr"]) == [
+        Measure("AP(rel=2)", "AP", 2), Measure("nDCG@10", "nDCG@10"), Measure("RR", "RR"),
+        Measure("P@5", "P@5"), Measure("nDCG", "nDCG"), Measure("RR", "RR")]
+    for bad in ("mrr", "pX", "recall@10"):
+        with pytest.raises(ValueError, match="Unsupported metric"):
+            parse_measures([bad])
+    # the argmax script skips what it does not know, and only takes "ndcg@10" names
+    assert parse_argmax_measures(["map", "NDCG@10", "recip_rank", "p10", "ndcg@5"]) == [
+        Measure("AP(rel=2)", "AP", 2), Measure("nDCG@10", "nDCG@10"), Measure("RR", "RR")]
+
+
+@pytest.mark.gpu
+def test_experiment_table_with_rel2_ap(gpu):
+    """experiment(): one row per run, the mean of every measure; AP(rel=2) is AP
+    with grades below 2 non-relevant (judged), checked against the trec_eval
+    restatement on the leveled qrels."""
+    from qppfuse.variants import experiment, parse_measures
+    runs, qrels = _oracle_runs(5)
+    ms = parse_measures(["map", "ndcg@10", "recip_rank", "p10"])
+    table = experiment(list(runs.values()), qrels, ms, list(runs))
+    assert list(table.columns) == ["name", "AP(rel=2)", "nDCG@10", "RR", "P@10"]
+    assert table["name"].tolist() == list(runs)
+    lev = {q: {d: (g if g >= 2 else 0) for d, g in docs.items()} for q, docs in qrels.items()}
+    for i, (name, run) in enumerate(runs.items()):
+        ap2 = list(_oracle_metric(run, lev, "AP").values())
+        assert table.loc[i, "AP(rel=2)"] == pytest.approx(np.mean(ap2), rel=1e-12)
+        for col, m in (("nDCG@10", "nDCG@10"), ("RR", "RR"), ("P@10", "P@10")):
+            want = list(_oracle_metric(run, qrels, m).values())
+            assert table.loc[i, col] == pytest.approx(np.mean(want), rel=1e-12)
+    # AP(rel=2) differs from AP at rel 1 on these qrels (grades 1 and 2 both occur)
+    ap1 = experiment(list(runs.values()), qrels, ["AP"], list(runs))["AP"].to_numpy()
+    assert not np.allclose(ap1, table["AP(rel=2)"].to_numpy())

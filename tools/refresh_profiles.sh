@@ -14,7 +14,7 @@ timeout -k 10 300 python -u bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { 
 for w in c1 c3 c4 c5; do
   timeout -k 10 300 python -u bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
 done
-timeout -k 10 300 python -u tools/e2e.py > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }
+timeout -k 10 300 python -u tools/e2e.py --repeat 3 > $O/e2e.json 2> $O/e2e.err || { tail -20 $O/e2e.err; exit 1; }
 # the N > 1 step (sharding, the QPP min/max all-reduce, the pipelined top-k gather)
 # rehearsed with two gloo ranks on this box's one GPU
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
