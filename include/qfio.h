@@ -80,6 +80,9 @@ int qfio_gather_chars(const int64_t* tab_off, const char* tab_chars, const uint3
 /* Arrow offsets of n repeats of one len-byte string: out_off[i] = i * len, i <= n
  * (a column of one value: iter "Q0", a run's tag). */
 void qfio_repeat_offsets(int64_t len, int64_t n, int64_t* out_off);
+/* A 64-bit content digest of nbytes at data, hashed over the threads (the pack
+ * cache's fingerprint of the numeric columns load_runs returns; not cryptographic). */
+uint64_t qfio_hash_bytes(const void* data, int64_t nbytes);
 
 /* Python's f"{x:.6f}" of x into out (>= 400 bytes); returns the length. */
 size_t qfio_format_score(double x, char* out);

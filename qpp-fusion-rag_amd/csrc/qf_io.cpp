@@ -868,6 +868,39 @@ int qfio_gather_chars(const int64_t* tab_off, const char* tab_chars, const uint3
   return 0;
 }
 
+uint64_t qfio_hash_bytes(const void* data, int64_t nbytes) {
+  if (!data || nbytes <= 0) return 0x9E3779B97F4A7C15ull ^ (uint64_t)(nbytes < 0 ? 0 : nbytes);
+  // 1 MB blocks hashed in parallel (8-byte words, multiply-mix), then the block
+  // hashes combined in order: a content digest for the pack cache (not a
+  // cryptographic hash; any change of a word changes its block's value)
+  const char* p = (const char*)data;
+  constexpr int64_t kBlock = 1 << 20;
+  const int64_t nb = (nbytes + kBlock - 1) / kBlock;
+  std::vector<uint64_t> hb((size_t)nb);
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t a = b * kBlock, e = std::min(nbytes, a + kBlock);
+    uint64_t h0 = 0x243F6A8885A308D3ull ^ (uint64_t)b, h1 = 0x13198A2E03707344ull;
+    int64_t i = a;
+    for (; i + 16 <= e; i += 16) {
+      uint64_t w0, w1;
+      memcpy(&w0, p + i, 8);
+      memcpy(&w1, p + i + 8, 8);
+      h0 = (h0 ^ w0) * 0xff51afd7ed558ccdull;
+      h1 = (h1 ^ w1) * 0xc4ceb9fe1a85ec53ull;
+      h0 ^= h0 >> 29;
+      h1 ^= h1 >> 31;
+    }
+    if (i < e) {
+      uint64_t w = 0;
+      memcpy(&w, p + i, (size_t)(e - i));
+      h0 = (h0 ^ w) * 0xff51afd7ed558ccdull;
+    }
+    hb[(size_t)b] = hash_words((const char*)&h0, 8) ^ (hash_words((const char*)&h1, 8) * 3);
+  }
+  return hash_words((const char*)hb.data(), hb.size() * 8) ^ (uint64_t)nbytes;
+}
+
 void qfio_repeat_offsets(int64_t len, int64_t n, int64_t* out_off) {
   if (n < 0 || !out_off) return;
 #pragma omp parallel for schedule(static)

@@ -51,6 +51,8 @@ def lib() -> C.CDLL:
         L.qfio_gather_chars.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp]
         L.qfio_repeat_offsets.restype = None
         L.qfio_repeat_offsets.argtypes = [_i64, _i64, _vp]
+        L.qfio_hash_bytes.restype = C.c_uint64
+        L.qfio_hash_bytes.argtypes = [_vp, _i64]
         L.qfio_runset_drop_text.restype = None
         L.qfio_runset_drop_text.argtypes = [_vp]
         L.qfio_runset_views.restype = None
@@ -149,6 +151,12 @@ def frame_strings() -> str:
     if v not in ("arrow", "object"):
         raise ValueError(f"QPPFUSE_FRAME_STRINGS must be 'arrow' or 'object', not {v!r}")
     return v
+
+
+def hash_bytes(a: np.ndarray) -> int:
+    """64-bit content digest of a contiguous array (qfio_hash_bytes, multi-threaded)."""
+    a = np.ascontiguousarray(a)
+    return int(lib().qfio_hash_bytes(_p(a) if a.size else None, a.nbytes))
 
 
 def format_score(x: float) -> str:

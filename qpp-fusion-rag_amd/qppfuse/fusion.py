@@ -191,6 +191,9 @@ def _column_digest(col):
         h = xxhash.xxh3_64_intdigest(memoryview(ptrs).cast("B"))
         del ptrs
         return _Pinned(h, a)
+    if a.nbytes >= (1 << 22):  # large numeric columns: hashed over the threads
+        from . import fastio
+        return ("n", a.dtype.str, fastio.hash_bytes(a))
     return xxhash.xxh3_64_intdigest(memoryview(a).cast("B"))
 
 
