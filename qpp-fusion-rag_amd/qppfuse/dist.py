@@ -201,12 +201,21 @@ class TopkGather:
         import torch.distributed as dist
         j = i % self.depth
         buf = self.send[j]
-        if self.host:  # gloo rehearsal: host buffers (the copy synchronises the stream)
-            self.hsend[j].copy_(buf)
-            buf = self.hsend[j]
         mine = self.rank == self.dst
-        # gathered as float64 words (a bit copy: the docids pass through unchanged);
-        # gloo moves 8-byte elements about twice as fast as bytes
+        if self.host:
+            # gloo rehearsal: host buffers (the copy synchronises the stream), and the
+            # two columns as two typed gathers, which gloo runs side by side (one
+            # byte-buffer gather measured twice as slow there)
+            self.hsend[j].copy_(buf)
+            d, s = self._views(self.hsend[j])
+            rv = self._rv[j] if mine else None
+            works = [dist.gather(d, [x for x, _ in rv] if mine else None, dst=self.dst,
+                                 group=self.group, async_op=True),
+                     dist.gather(s, [y for _, y in rv] if mine else None, dst=self.dst,
+                                 group=self.group, async_op=True)]
+            return _TopkHandle(self, j, [w for w in works if w is not None])
+        # RCCL: one gather of the whole buffer, as float64 words (a bit copy: the
+        # docids pass through unchanged)
         w = dist.gather(buf.view(torch.float64), self._rl[j] if mine else None, dst=self.dst,
                         group=self.group, async_op=True)
         return _TopkHandle(self, j, [w] if w is not None else [])

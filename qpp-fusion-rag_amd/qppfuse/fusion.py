@@ -266,7 +266,16 @@ def _expand_weights(weights: Optional[np.ndarray], rs: RunSet, rv: RunSet):
 def _weights(rs: RunSet, qpp_data, qpp_index: int) -> np.ndarray:
     """[Q*R] weights in the reference's visiting order, raising as it does."""
     fusion_mode = qpp_index == -1
-    w = np.empty(rs.n_queries * rs.n_rankers, dtype=np.float64)
+    n = rs.n_queries * rs.n_rankers
+    try:  # every lookup present: one comprehension instead of a call per (qid, ranker)
+        if fusion_mode:
+            it = (sum(v) / len(v) for q in rs.qids for v in map(qpp_data[q].__getitem__, rs.rankers))
+        else:
+            it = (qpp_data[q][r][qpp_index] for q in rs.qids for r in rs.rankers)
+        return np.fromiter(it, dtype=np.float64, count=n)
+    except (KeyError, IndexError, TypeError, ValueError, ZeroDivisionError):
+        pass  # the loop below raises what the reference raises, where it raises it
+    w = np.empty(n, dtype=np.float64)
     k = 0
     for qid in rs.qids:
         for ranker in rs.rankers:
