@@ -478,6 +478,7 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   uniq.resize(U);
 #pragma omp parallel for schedule(static)
   for (size_t k = 0; k < U; ++k) {
+    if (k + 16 < U) __builtin_prefetch(&views[reps[keys[k + 16].u]]);
     rank[keys[k].u] = (uint32_t)k;
     uniq[k] = sv(views[reps[keys[k].u]]);
   }
@@ -752,7 +753,10 @@ static void copy_strings(const std::vector<std::string_view>& v, int64_t* off, c
   }
   // the bytes in parallel: the views point all over the mapped files
 #pragma omp parallel for schedule(static, 4096)
-  for (int64_t i = 0; i < (int64_t)v.size(); ++i) memcpy(chars + off[i], v[i].data(), v[i].size());
+  for (int64_t i = 0; i < (int64_t)v.size(); ++i) {
+    if (i + 8 < (int64_t)v.size()) __builtin_prefetch(v[i + 8].data());
+    memcpy(chars + off[i], v[i].data(), v[i].size());
+  }
 }
 
 int qfio_runset_csr(const qfio_runset* rs, int64_t* list_off, uint32_t* docid, double* score,
