@@ -316,10 +316,18 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
         q_of = torch.repeat_interleave(torch.arange(len(counts), device=dev), cnt,
                                        output_size=total)
         idx = qb[q_of] + (torch.arange(total, device=dev) - cb[q_of])
-        udoc = out.union_docid[idx].cpu().numpy().view(np.uint32)
-        perm = out.perm[:, idx].cpu().numpy().view(np.uint32 if out.wide else np.uint16)
-        fused = out.fused[:, idx].cpu().numpy()
-        qbase = cb.cpu().numpy()
+        # into pinned host buffers (torch's caching host allocator keeps them for the
+        # next call), three copies queued, one synchronisation
+        hosts = []
+        for t in (out.union_docid[idx], out.perm[:, idx], out.fused[:, idx], cb):
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            hosts.append(h)
+        torch.cuda.current_stream(dev).synchronize()
+        udoc = hosts[0].numpy().view(np.uint32)
+        perm = hosts[1].numpy().view(np.uint32 if out.wide else np.uint16)
+        fused = hosts[2].numpy()
+        qbase = hosts[3].numpy()
     else:
         udoc = out.union_docid.cpu().numpy()[:E].view(np.uint32)
         perm = out.perm.cpu().numpy()[:, :E].view(np.uint32 if out.wide else np.uint16)
