@@ -31,6 +31,22 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(header_functions())
 
 
+def test_io_library_exports_every_declared_symbol():
+    """libqfio.so (host run-file I/O) exports every qfio_ function include/qfio.h
+    declares, and qppfuse.fastio binds each with a ctypes signature."""
+    import ctypes
+    from qppfuse import fastio
+    text = (ROOT / "include" / "qfio.h").read_text()
+    names = sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(qfio_\w+)\s*\(", text, re.M)))
+    assert {"qfio_load_runs", "qfio_write_run", "qfio_gather_strings", "qfio_gather_chars",
+            "qfio_repeat_offsets", "qfio_hash_bytes"} <= set(names)
+    lib = fastio.lib()
+    for name in names:
+        fn = getattr(lib, name)
+        assert isinstance(fn, ctypes._CFuncPtr), name
+        assert fn.argtypes is not None or name in ("qfio_last_error",), f"{name} is not bound"
+
+
 def test_version_and_limits():
     from qppfuse import _lib
     assert "gfx950" in _lib.version()
