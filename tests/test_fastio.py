@@ -150,6 +150,14 @@ def test_write_run_matches_python_writer(tmp_path):
     fastio.write_run(str(out32), order, qbase, counts, ud, perm.astype(np.uint32), fused, rs,
                      "tag-1")
     assert out32.read_bytes() == out.read_bytes()
+    # the chunked, pipelined writer (each chunk written once the one before it has
+    # published its end): the same bytes over 1-8 threads, i.e. 8-64 chunks of 25
+    # queries, over an existing longer file (truncated)
+    out.write_text("x" * 100000)
+    for threads in (1, 3, 8):
+        fastio.write_run(str(out), order, qbase, counts, ud, perm, fused, rs, "tag-1",
+                         n_threads=threads)
+        assert out.read_text() == "".join(want), threads
 
 
 def test_write_run_uint32_perm_beyond_65535():
