@@ -196,16 +196,8 @@ class Pipeline:
         self.off, self.docid, self.raw = engine.synth_runs(self.q_begin, Q, R, K, seed=SEED)
         self.qids = None
         if args.workload == "c4" and args.queries is None:
-            # the real test qids of HotpotQA + SciFact + NQ, namespaced (qppfuse.multicorpus),
-            # in batch order; query texts as compute_qpp_for_res_file gets them
-            # (queries.jsonl; HotpotQA's is an LFS pointer, so its qid, src/qpp.py:312)
-            self.qids, texts = c4_queries()
-            self.qids, texts = (self.qids[self.q_begin:self.q_begin + Q],
-                                texts[self.q_begin:self.q_begin + Q])
-            from qppfuse import textfeat
-            nt, tf = textfeat.feature_arrays(texts)
-        else:
-            nt, tf = text_inputs(self.q_begin, Q)
+            self.qids = c4_queries()[0][self.q_begin:self.q_begin + Q]
+        nt, tf = self.text_arrays(self.q_begin, Q)
         self.nt = torch.from_numpy(nt).to(dev)
         self.tf = torch.from_numpy(tf).to(dev)
         E = Q * R * K
@@ -227,12 +219,78 @@ class Pipeline:
                                    for n in names]
         self.ev = []
         self.pending = None  # the previous step's top-k gather (dist.TopkGather handle)
-        self.gather, self.n_step = None, 0
+        self.gather, self.n_step, self.gathered = None, 0, None
         if world > 1 and args.gather_topk > 0:  # every buffer of the gather, made once
             from qppfuse.dist import TopkGather
             self.gather = TopkGather(self.shard_sizes, len(self.methods), args.gather_topk, dev,
                                      dst=0)
         torch.cuda.synchronize()
+
+    def shard_begin(self, r: int) -> int:
+        """First global query of rank r's shard (as __init__ computes its own)."""
+        if self.args.queries is not None or not self.args.wl["total"]:
+            return r * self.shard_sizes[r]
+        from qppfuse.dist import shard_range
+        return shard_range(self.args.wl["queries"], self.world, r)[0]
+
+    def text_arrays(self, q_begin: int, Q: int):
+        """numTerms / text-feature columns of the shard [q_begin, q_begin + Q)."""
+        if self.args.workload == "c4" and self.args.queries is None:
+            # the real test qids of HotpotQA + SciFact + NQ, namespaced (qppfuse.multicorpus),
+            # in batch order; query texts as compute_qpp_for_res_file gets them
+            # (queries.jsonl; HotpotQA's is an LFS pointer, so its qid, src/qpp.py:312)
+            from qppfuse import textfeat
+            return textfeat.feature_arrays(c4_queries()[1][q_begin:q_begin + Q])
+        return text_inputs(q_begin, Q)
+
+    def fuse_block(self, q_begin: int, Q_shard: int, start: int, n: int):
+        """Queries [start, start + n) of the shard beginning at global query q_begin
+        (of Q_shard queries), regenerated from the counter-based generator and run
+        through this step's kernels with the step's QPP min / max (after the
+        all-reduce: every rank normalises with the same global values)."""
+        e, a, R, K = self.engine, self.args, self.R, self.K
+        off, docid, raw = e.synth_runs(q_begin + start, n, R, K, seed=SEED)
+        _, micro = e.minmax_per_query(raw, off, want_norm=False)
+        w = None
+        if a.wl["qpp"]:
+            nt, tf = self.text_arrays(q_begin, Q_shard)
+            nt = torch.from_numpy(np.ascontiguousarray(nt[start:start + n])).to(self.dev)
+            tf = torch.from_numpy(np.ascontiguousarray(tf[start:start + n])).to(self.dev)
+            qraw = e.qpp_raw(raw, off, R, a.qpp_top_k, nt, tf)
+            learned = "learned" in self.methods
+            o = e.qpp_normalize(qraw, self.mm, off, R, "minmax", a.qpp_index,
+                                want_micro=learned, want_weights=not learned)
+            w = o["weights"]
+            if learned:
+                X = e.qpp_features(o["micro"], n, R, self.block_runs)
+                w = e.learned_weights(e.gbdt_predict(X, self.packed), self.run_to_booster)
+        out = e.fuse(off, docid, micro, R, self.methods, 60, weights=w, max_entries=R * K)
+        return e.fused_topk(out, off, R, a.gather_topk)
+
+    def gather_parity(self, per_block: int = 4):
+        """Rank 0: the gathered top-k rows of EVERY rank checked byte for byte against
+        rows rank 0 recomputes itself — each shard's first and last `per_block`
+        queries regenerated (qf_synth_runs is counter-based in the global query id)
+        and fused here.  None off rank 0 or without a gather."""
+        if self.gather is None or self.rank != 0 or self.gathered is None:
+            return None
+        ok, checked = True, 0
+        for r, (gd, gs) in enumerate(self.gathered):
+            n_r = self.shard_sizes[r]
+            q0 = self.shard_begin(r)
+            for start in sorted({0, max(0, n_r - per_block)}):
+                n = min(per_block, n_r - start)
+                if n <= 0:
+                    continue
+                d, sc = self.fuse_block(q0, n_r, start, n)
+                ok &= bool(torch.equal(gd[start:start + n].to(self.dev), d))
+                ok &= bool(torch.equal(gs[start:start + n].to(self.dev).view(torch.int64),
+                                       sc.view(torch.int64)))
+                checked += n
+        return {"ranks": len(self.gathered), "queries_checked": checked, "bit_exact": ok,
+                "how": "rank 0 regenerates the first and last queries of every rank's shard "
+                       "(counter-based generator), fuses them with the step's kernels and "
+                       "compares the gathered top-k rows byte for byte"}
 
     def step(self, timed=False):
         from qppfuse import _lib
@@ -581,22 +639,30 @@ def timed_loop(p: Pipeline, steps: int, world: int, dev) -> float:
     return elapsed
 
 
-def copy_ceiling_gbs(dev, nbytes: int = 1 << 30, reps: int = 40) -> float:
-    """Measured device-to-device copy rate (read + write bytes / s): the practical HBM
-    ceiling next to the 8 TB/s spec peak."""
+def copy_ceiling_gbs(dev, nbytes: int = 1 << 30, reps: int = 40) -> dict:
+    """Measured device-to-device copy rates (read + write bytes / s): the practical HBM
+    ceiling next to the 8 TB/s spec peak.  `kernel`: the library's
+    hand-written 16-byte-per-lane streaming copy (qf_stream_copy, csrc/qf_norm.hip) —
+    the ceiling; `blit`: torch's copy_ (the runtime's copyBuffer blit), for the record."""
+    from qppfuse import _lib
     a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
     a.fill_(1.0)
-    b.copy_(a)
-    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    s1.record()
-    torch.cuda.synchronize()
-    ms = s0.elapsed_time(s1) / reps
+    s = torch.cuda.current_stream().cuda_stream
+    kcopy = lambda: _lib.call("qf_stream_copy", b.data_ptr(), a.data_ptr(), nbytes, s)
+    out = {}
+    for name, fn in (("kernel", kcopy), ("blit", lambda: b.copy_(a))):
+        fn()
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(reps):
+            fn()
+        s1.record()
+        torch.cuda.synchronize()
+        ms = s0.elapsed_time(s1) / reps
+        out[name] = 2 * nbytes / (ms * 1e-3) / 1e9
     del a, b
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    return out
 
 
 def progress(msg: str):
@@ -624,7 +690,8 @@ def main():
     # the device-copy ceiling of the roofline object, measured before the warmup steps:
     # ~10 ms of HBM traffic that also takes the GPU out of its idle clocks, so a short
     # timed region (the driver's 5 + 20 steps) sees the steady-state step time
-    copy_gbs = copy_ceiling_gbs(dev)
+    copy = copy_ceiling_gbs(dev)
+    copy_gbs = copy["kernel"]
     for _ in range(args.warmup):
         p.step()
     p.drain()
@@ -652,6 +719,7 @@ def main():
     valu = pmc_valu(args)
     progress(f"rank {rank}: {elapsed / args.steps * 1e3:.3f} ms/step; parity + NDCG checks")
     parity = check_parity(p, min(args.check, p.Q)) if args.check > 0 else None
+    gparity = p.gather_parity()
     ndcg_vals, eval_ms = ndcg_device(p)
     result = None
     if rank == 0:
@@ -709,9 +777,13 @@ def main():
                              valu / N_SIMDS / (fuse_ms * 1e6) / VALU_PEAK_PER_SIMD_NS, 4),
                          "valu_insts_per_launch": valu,
                          "copy_ceiling_gbs": round(copy_gbs, 1),
+                         "copy_ceiling_source": "qf_stream_copy: 16 B/lane non-temporal "
+                                                "streaming copy kernel, 1 GiB, read + write",
+                         "copy_blit_gbs": round(copy["blit"], 1),
                          "frac_of_copy_ceiling": round(achieved / copy_gbs, 4)},
             "cpu_baseline": cpu,
             "parity_vs_oracle": {"queries": min(args.check, p.Q), "bit_exact": parity},
+            "gather_parity": gparity,
             "ndcg10": {m: round(float(np.nanmean(ndcg_vals[i])), 6)
                        for i, m in enumerate(p.methods)},
             "ndcg10_eval_ms": round(eval_ms, 4),

@@ -22,6 +22,8 @@ extern "C" {
 #define QFIO_ENOENT 2 /* a file cannot be opened (FileNotFoundError)  */
 #define QFIO_EIO    3
 #define QFIO_EPARSE 4 /* a line is not "qid Q0 docno rank score tag" */
+#define QFIO_EPYTHON 5 /* the file needs the reference's own Python reading (see
+                          qfio_read_score_lists); nothing is returned */
 
 typedef struct qfio_runset qfio_runset;
 
@@ -105,6 +107,26 @@ int qfio_write_run32(const char* path, int64_t n_out, const int64_t* order, cons
                      const double* fused, const int64_t* qid_off, const char* qid_chars,
                      const int64_t* docno_off, const char* docno_chars, const char* tag,
                      int32_t n_threads);
+
+/*
+ * compute_qpp_for_res_file's read of a RAW run file (src/qpp.py:292-305): every
+ * line with >= 5 whitespace-separated fields adds float(field 5) to its qid's
+ * list in file order; qids in first-appearance order; each list sorted descending
+ * (stable: -0.0 / 0.0 keep file order, as sorted(reverse=True)) and sliced
+ * [:top_k] with Python's slice semantics (negative top_k drops from the end).
+ * QFIO_EPARSE: a fifth field float() rejects (message = Python's ValueError text).
+ * QFIO_EPYTHON: the file holds something only Python's reading decides exactly
+ * (bytes >= 0x80 or 0x1c-0x1f, a lone '\r', digit underscores, a NaN score).
+ */
+typedef struct qfio_scorelists qfio_scorelists;
+int qfio_read_score_lists(const char* path, int32_t top_k, int32_t n_threads,
+                          qfio_scorelists** out);
+/* sizes[4]: n_queries, kept scores, qid bytes, rows read (lines with >= 5 fields) */
+void qfio_scorelists_sizes(const qfio_scorelists* s, int64_t* sizes);
+/* qid_off[Q+1] + qid_chars (first-appearance order), list_off[Q+1], scores */
+int qfio_scorelists_get(const qfio_scorelists* s, int64_t* qid_off, char* qid_chars,
+                        int64_t* list_off, double* scores);
+void qfio_scorelists_free(qfio_scorelists* s);
 
 #ifdef __cplusplus
 }

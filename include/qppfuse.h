@@ -359,6 +359,15 @@ int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int3
                   uint64_t seed, double p_shared, int64_t* list_off, uint32_t* docid,
                   double* score, void* stream);
 
+/*
+ * Measurement support (bench.py's roofline): a device-to-device streaming copy of
+ * nbytes (a multiple of 16; 16-byte aligned pointers), 16 bytes per lane per
+ * access, non-temporal.  Its rate (2 * nbytes / time) is the practical HBM
+ * ceiling the roofline object reports next to the 8 TB/s spec peak.  No
+ * counterpart in the reference.
+ */
+int qf_stream_copy(void* dst, const void* src, int64_t nbytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

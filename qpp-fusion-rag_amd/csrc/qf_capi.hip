@@ -395,4 +395,13 @@ int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int3
                "qf_synth_runs");
 }
 
+int qf_stream_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (nbytes < 0 || (nbytes > 0 && (!dst || !src)) || (nbytes & 15) ||
+      (((uintptr_t)dst | (uintptr_t)src) & 15))
+    return fail(QF_EINVAL, "qf_stream_copy: bad arguments (16-byte aligned sizes and pointers)");
+  if (nbytes == 0) return QF_OK;
+  return check(qf::stream_copy_launch(dst, src, nbytes / 16, (hipStream_t)stream),
+               "qf_stream_copy");
+}
+
 }  // extern "C"

@@ -35,6 +35,7 @@
 #include <string>
 #include <string_view>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/qfio.h"
@@ -908,10 +909,18 @@ uint64_t qfio_hash_bytes(const void* data, int64_t nbytes) {
       h0 ^= h0 >> 29;
       h1 ^= h1 >> 31;
     }
+    // the tail (0-15 bytes): up to 8 into h0, the rest into h1
+    if (i < e) {
+      uint64_t w = 0;
+      const int64_t n0 = std::min<int64_t>(8, e - i);
+      memcpy(&w, p + i, (size_t)n0);
+      h0 = (h0 ^ w ^ ((uint64_t)n0 << 56)) * 0xff51afd7ed558ccdull;
+      i += n0;
+    }
     if (i < e) {
       uint64_t w = 0;
       memcpy(&w, p + i, (size_t)(e - i));
-      h0 = (h0 ^ w) * 0xff51afd7ed558ccdull;
+      h1 = (h1 ^ w ^ ((uint64_t)(e - i) << 56)) * 0xc4ceb9fe1a85ec53ull;
     }
     hb[(size_t)b] = hash_words((const char*)&h0, 8) ^ (hash_words((const char*)&h1, 8) * 3);
   }
@@ -980,14 +989,20 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
   const size_t tl = strlen(tag);
   const int T = std::max(1, omp_get_max_threads());
   const int64_t chunks = std::min<int64_t>(std::max<int64_t>(n_out, 1), (int64_t)T * 8);
-  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  // Written to a temporary file beside the target and renamed over it on success,
+  // so a failure part way (out of memory, a short write) leaves an existing run file
+  // as it was, as the reference's buffered write would until its first flush.
+  const std::string tmp_path = std::string(path) + ".qfio-tmp." + std::to_string((long)getpid());
+  const int fd = open(tmp_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
   if (fd < 0) return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(errno));
   // Each chunk of queries is formatted into a raw buffer sized by an upper bound
   // (no per-field string appends, no snprintf for the rank) and written at its
   // offset as soon as the chunk before it has published its end: the writes (one
   // file's writes are serialised by the kernel) overlap the formatting of later
-  // chunks instead of following all of it.  Chunks are handed out in order
-  // (dynamic, 1), so the chunk a thread waits on is already being formatted.
+  // chunks instead of following all of it.  Chunks are handed out in increasing
+  // order by an atomic ticket, so the chunk a thread waits on has already been
+  // taken by a running thread (which waits only on earlier chunks): no deadlock,
+  // whatever order an OpenMP schedule would have used.
   // (Measured, not kept: the file sized once, mapped, and every chunk copied in by
   // its own thread — 0.145-0.185 s per 390 MB run on the GPU box's host, the same
   // as format-all-then-pwrite: the page-cache copy is the bound either way.)
@@ -995,8 +1010,10 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
   for (auto& x : at) x.store(-1, std::memory_order_relaxed);
   at[0].store(0, std::memory_order_release);
   int err = 0, werr = 0;
-#pragma omp parallel for schedule(dynamic, 1) reduction(| : err, werr)
-  for (int64_t c = 0; c < chunks; ++c) {
+  std::atomic<int64_t> ticket{0};
+#pragma omp parallel reduction(| : err, werr)
+  for (int64_t c = ticket.fetch_add(1, std::memory_order_relaxed); c < chunks;
+       c = ticket.fetch_add(1, std::memory_order_relaxed)) {
     const int64_t a = n_out * c / chunks, b = n_out * (c + 1) / chunks;
     size_t cap = 1 << 16;
     for (int64_t i = a; i < b; ++i) {
@@ -1066,8 +1083,17 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
     free(o);
   }
   tm.mark("write: format + pwrite");
-  if (close(fd) != 0 || werr) return fail(QFIO_EIO, std::string("short write to ") + path);
-  if (err) return fail(QFIO_EIO, "qfio_write_run: out of memory");
+  const bool closed = close(fd) == 0;
+  if (!closed || werr || err) {
+    unlink(tmp_path.c_str());
+    if (err) return fail(QFIO_EIO, "qfio_write_run: out of memory");
+    return fail(QFIO_EIO, std::string("short write to ") + path);
+  }
+  if (rename(tmp_path.c_str(), path) != 0) {
+    const int e = errno;
+    unlink(tmp_path.c_str());
+    return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(e));
+  }
   tm.mark("write: close");
   return QFIO_OK;
 }
@@ -1091,5 +1117,266 @@ int qfio_write_run32(const char* path, int64_t n_out, const int64_t* order, cons
   return write_run(path, n_out, order, qbase, counts, union_docid, perm, fused, qid_off, qid_chars,
                    docno_off, docno_chars, tag, n_threads);
 }
+
+}  // extern "C"
+
+// ---- compute_qpp_for_res_file's read of a raw run (src/qpp.py:292-305) -------------
+//
+// Every line with >= 5 whitespace-separated fields adds float(field 5) to its qid's
+// list, in file order, qids in first-appearance order (the reference's defaultdict);
+// then each list is sorted descending — stable, so equal values (-0.0 and 0.0) keep
+// file order, as Python's sorted(reverse=True) does — and sliced [:top_k].  Files
+// whose Python reading this does not reproduce byte for byte (a byte >= 0x80 or in
+// 0x1c-0x1f, which Python's str.split() may treat as whitespace; a lone '\r', a line
+// break in text mode; digit-group underscores, which float() accepts; a NaN, which
+// makes Python's sort order depend on its position) are reported as QFIO_EPYTHON:
+// the caller reads those with the reference's own Python loop.
+struct qfio_scorelists {
+  std::vector<int64_t> qid_off;
+  std::string qid_chars;
+  std::vector<int64_t> list_off;
+  std::vector<double> scores;
+  int64_t n_rows = 0;
+};
+
+namespace {
+
+inline bool ci_eq(std::string_view a, const char* b) {
+  const size_t n = strlen(b);
+  if (a.size() != n) return false;
+  for (size_t i = 0; i < n; ++i)
+    if ((char)(a[i] | 0x20) != b[i]) return false;
+  return true;
+}
+
+// Python's float(text) for one whitespace-free field: 0 = ok, 1 = not a float
+// (ValueError), 2 = a form only Python's reader should judge (underscores).
+int py_float(std::string_view t, double& v) {
+  if (t.find('_') != std::string_view::npos) return 2;
+  size_t i = 0;
+  if (i < t.size() && (t[i] == '+' || t[i] == '-')) ++i;
+  const std::string_view body = t.substr(i);
+  if (ci_eq(body, "inf") || ci_eq(body, "infinity") || ci_eq(body, "nan")) {
+    v = body[0] == 'n' || body[0] == 'N' ? NAN : INFINITY;
+    if (t[0] == '-') v = -v;
+    return 0;
+  }
+  size_t nd = 0;
+  while (i < t.size() && t[i] >= '0' && t[i] <= '9') { ++i; ++nd; }
+  if (i < t.size() && t[i] == '.') {
+    ++i;
+    while (i < t.size() && t[i] >= '0' && t[i] <= '9') { ++i; ++nd; }
+  }
+  if (nd == 0) return 1;
+  if (i < t.size() && (t[i] == 'e' || t[i] == 'E')) {
+    ++i;
+    if (i < t.size() && (t[i] == '+' || t[i] == '-')) ++i;
+    size_t ne = 0;
+    while (i < t.size() && t[i] >= '0' && t[i] <= '9') { ++i; ++ne; }
+    if (ne == 0) return 1;
+  }
+  if (i != t.size()) return 1;
+  int32_t m = 0;
+  bool mok = false;
+  if (!parse_score(t, v, m, mok)) {  // long texts: strtod on a heap copy
+    std::string s(t);
+    v = strtod(s.c_str(), nullptr);
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qfio_read_score_lists(const char* path, int32_t top_k, int32_t n_threads,
+                          qfio_scorelists** out) {
+  if (!path || !out) return fail(QFIO_EINVAL, "qfio_read_score_lists: bad arguments");
+  *out = nullptr;
+  if (n_threads > 0) omp_set_num_threads(n_threads);
+  Mapped m;
+  m.fd = open(path, O_RDONLY);
+  if (m.fd < 0) return fail(QFIO_ENOENT, std::string("cannot open ") + path + ": " + strerror(errno));
+  struct stat st;
+  fstat(m.fd, &st);
+  m.size = (size_t)st.st_size;
+  if (m.size) {
+    m.data = (const char*)mmap(nullptr, m.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, m.fd, 0);
+    if (m.data == MAP_FAILED) {
+      m.data = nullptr;
+      return fail(QFIO_EIO, std::string("cannot map ") + path);
+    }
+  }
+  const int T = std::max(1, omp_get_max_threads());
+  std::vector<const char*> cut((size_t)T + 1);
+  cut[0] = m.data;
+  cut[T] = m.data + m.size;
+  for (int t = 1; t < T; ++t) {
+    const char* x = m.data + (m.size * (size_t)t) / (size_t)T;
+    while (x < cut[T] && x > m.data && x[-1] != '\n') ++x;
+    cut[t] = std::max(x, cut[t - 1]);
+  }
+  // per chunk: rows (qid run index, score) and the qid runs (heads)
+  struct Chunk {
+    std::vector<std::string_view> head;  // qid of each run
+    std::vector<uint32_t> run_len;
+    std::vector<double> score;
+    int code = 0;
+    std::string err;
+  };
+  std::vector<Chunk> ch((size_t)T);
+#pragma omp parallel for schedule(static, 1)
+  for (int t = 0; t < T; ++t) {
+    Chunk& c = ch[(size_t)t];
+    c.score.reserve((size_t)(cut[t + 1] - cut[t]) / 32 + 16);
+    const char* p = cut[t];
+    const char* end = cut[t + 1];
+    while (p < end) {
+      const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+      const char* e = nl ? nl : end;
+      std::string_view f[5];
+      int nf = 0;
+      const char* q = p;
+      for (const char* x = p; x < e; ++x) {  // the bytes Python would read otherwise
+        const unsigned char b = (unsigned char)*x;
+        if (b >= 0x80 || (b >= 0x1c && b <= 0x1f) || (b == '\r' && x + 1 != e)) {
+          c.code = 2;
+          break;
+        }
+      }
+      if (c.code) break;
+      while (nf < 5) {
+        while (q < e && kSpace[(unsigned char)*q]) ++q;
+        if (q >= e) break;
+        const char* s = q;
+        while (q < e && !kSpace[(unsigned char)*q]) ++q;
+        f[nf++] = std::string_view(s, (size_t)(q - s));
+      }
+      p = nl ? nl + 1 : end;
+      if (nf < 5) continue;  // src/qpp.py:295: lines with fewer fields are skipped
+      double v;
+      const int r = py_float(f[4], v);
+      if (r == 1) {
+        c.code = 1;
+        c.err = "could not convert string to float: '" + std::string(f[4]) + "'";
+        break;
+      }
+      if (r == 2 || v != v) {
+        c.code = 2;
+        break;
+      }
+      if (c.head.empty() || c.head.back() != f[0]) {
+        c.head.push_back(f[0]);
+        c.run_len.push_back(0);
+      }
+      ++c.run_len.back();
+      c.score.push_back(v);
+    }
+  }
+  for (int t = 0; t < T; ++t) {  // the first failing chunk in file order decides
+    if (ch[(size_t)t].code == 1) return fail(QFIO_EPARSE, ch[(size_t)t].err);
+    if (ch[(size_t)t].code == 2) return fail(QFIO_EPYTHON, "needs the Python reader");
+  }
+  // qids in first-appearance order over the runs (few: one run per query and chunk)
+  auto* res = new qfio_scorelists();
+  std::vector<std::string_view> qids;
+  std::vector<int64_t> qcount;
+  struct SvHash {
+    size_t operator()(std::string_view v) const { return (size_t)hash_sv(v); }
+  };
+  std::unordered_map<std::string_view, uint32_t, SvHash> idx;
+  std::vector<std::vector<uint32_t>> run_q((size_t)T);
+  for (int t = 0; t < T; ++t) {
+    const Chunk& c = ch[(size_t)t];
+    run_q[(size_t)t].resize(c.head.size());
+    for (size_t k = 0; k < c.head.size(); ++k) {
+      auto it = idx.find(c.head[k]);
+      uint32_t id;
+      if (it == idx.end()) {
+        id = (uint32_t)qids.size();
+        idx.emplace(c.head[k], id);
+        qids.push_back(c.head[k]);
+        qcount.push_back(0);
+      } else {
+        id = it->second;
+      }
+      run_q[(size_t)t][k] = id;
+      qcount[id] += c.run_len[k];
+    }
+  }
+  const int64_t Q = (int64_t)qids.size();
+  // every query's scores in file order (runs placed in chunk order), then sorted
+  std::vector<int64_t> full_off((size_t)Q + 1, 0);
+  for (int64_t q = 0; q < Q; ++q) full_off[(size_t)q + 1] = full_off[(size_t)q] + qcount[(size_t)q];
+  res->n_rows = full_off[(size_t)Q];
+  std::vector<double> full((size_t)res->n_rows);
+  {
+    std::vector<int64_t> pos(full_off.begin(), full_off.end() - 1);
+    std::vector<std::vector<int64_t>> dst((size_t)T);
+    for (int t = 0; t < T; ++t) {
+      const Chunk& c = ch[(size_t)t];
+      dst[(size_t)t].resize(c.head.size());
+      for (size_t k = 0; k < c.head.size(); ++k) {
+        const uint32_t id = run_q[(size_t)t][k];
+        dst[(size_t)t][k] = pos[id];
+        pos[id] += c.run_len[k];
+      }
+    }
+#pragma omp parallel for schedule(static, 1)
+    for (int t = 0; t < T; ++t) {
+      const Chunk& c = ch[(size_t)t];
+      size_t a = 0;
+      for (size_t k = 0; k < c.head.size(); ++k) {
+        memcpy(&full[(size_t)dst[(size_t)t][k]], &c.score[a], c.run_len[k] * sizeof(double));
+        a += c.run_len[k];
+      }
+    }
+  }
+  // sorted(scores, reverse=True)[:top_k]: Python's slice of a list of n
+  auto keep = [&](int64_t n) -> int64_t {
+    if (top_k >= 0) return std::min<int64_t>(n, top_k);
+    return std::max<int64_t>(0, n + top_k);
+  };
+  res->list_off.assign((size_t)Q + 1, 0);
+  for (int64_t q = 0; q < Q; ++q)
+    res->list_off[(size_t)q + 1] = res->list_off[(size_t)q] + keep(qcount[(size_t)q]);
+  res->scores.resize((size_t)res->list_off[(size_t)Q]);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t q = 0; q < Q; ++q) {
+    double* a = &full[(size_t)full_off[(size_t)q]];
+    double* b = &full[(size_t)full_off[(size_t)q + 1]];
+    std::stable_sort(a, b, [](double x, double y) { return x > y; });
+    std::copy(a, a + keep(b - a), &res->scores[(size_t)res->list_off[(size_t)q]]);
+  }
+  res->qid_off.assign((size_t)Q + 1, 0);
+  for (int64_t q = 0; q < Q; ++q)
+    res->qid_off[(size_t)q + 1] = res->qid_off[(size_t)q] + (int64_t)qids[(size_t)q].size();
+  res->qid_chars.reserve((size_t)res->qid_off[(size_t)Q]);
+  for (const auto& v : qids) res->qid_chars.append(v.data(), v.size());
+  *out = res;
+  return QFIO_OK;
+}
+
+void qfio_scorelists_sizes(const qfio_scorelists* s, int64_t* sizes) {
+  if (!s || !sizes) return;
+  sizes[0] = (int64_t)s->list_off.size() - 1;
+  sizes[1] = (int64_t)s->scores.size();
+  sizes[2] = (int64_t)s->qid_chars.size();
+  sizes[3] = s->n_rows;
+}
+
+int qfio_scorelists_get(const qfio_scorelists* s, int64_t* qid_off, char* qid_chars,
+                        int64_t* list_off, double* scores) {
+  if (!s || !qid_off || !list_off || (!qid_chars && !s->qid_chars.empty()) ||
+      (!scores && !s->scores.empty()))
+    return fail(QFIO_EINVAL, "qfio_scorelists_get: bad arguments");
+  memcpy(qid_off, s->qid_off.data(), s->qid_off.size() * sizeof(int64_t));
+  memcpy(list_off, s->list_off.data(), s->list_off.size() * sizeof(int64_t));
+  if (!s->qid_chars.empty()) memcpy(qid_chars, s->qid_chars.data(), s->qid_chars.size());
+  if (!s->scores.empty()) memcpy(scores, s->scores.data(), s->scores.size() * sizeof(double));
+  return QFIO_OK;
+}
+
+void qfio_scorelists_free(qfio_scorelists* s) { delete s; }
 
 }  // extern "C"

@@ -60,6 +60,7 @@ SIGNATURES = {
     "qf_fuse_learned_f32": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, C.c_uint32, _i32,
                                       _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
+    "qf_stream_copy": (C.c_int, [_vp, _vp, _i64, _vp]),
 }
 for _n in ("qf_fuse", "qf_fuse_probfuse", "qf_fuse_learned_f32", "qf_fused_topk"):
     SIGNATURES[_n + "_wide"] = SIGNATURES[_n]

@@ -61,6 +61,14 @@ def lib() -> C.CDLL:
         L.qfio_runset_free.argtypes = [_vp]
         L.qfio_format_score.restype = C.c_size_t
         L.qfio_format_score.argtypes = [C.c_double, C.c_char_p]
+        L.qfio_read_score_lists.restype = C.c_int
+        L.qfio_read_score_lists.argtypes = [C.c_char_p, _i32, _i32, C.POINTER(_vp)]
+        L.qfio_scorelists_sizes.restype = None
+        L.qfio_scorelists_sizes.argtypes = [_vp, _vp]
+        L.qfio_scorelists_get.restype = C.c_int
+        L.qfio_scorelists_get.argtypes = [_vp] * 5
+        L.qfio_scorelists_free.restype = None
+        L.qfio_scorelists_free.argtypes = [_vp]
         for fn in (L.qfio_write_run, L.qfio_write_run32):
             fn.restype = C.c_int
             fn.argtypes = [C.c_char_p, _i64] + [_vp] * 10 + [C.c_char_p, _i32]
@@ -102,6 +110,35 @@ class _RunSetOwner:
 
 def _p(a: np.ndarray):
     return a.ctypes.data_as(_vp)
+
+
+def read_score_lists(path: str, top_k: int, n_threads: int = 0):
+    """compute_qpp_for_res_file's read of a raw run (src/qpp.py:292-305), natively
+    (qfio_read_score_lists): (qids in first-appearance order, list_off[Q+1], the
+    descending-sorted [:top_k] scores of every query, rows read).  None when the
+    file needs the reference's own Python reading (include/qfio.h QFIO_EPYTHON)."""
+    L = lib()
+    h = _vp()
+    rc = L.qfio_read_score_lists(path.encode(), int(top_k), n_threads, C.byref(h))
+    if rc == 5:
+        return None
+    if rc == 4:  # float()'s own ValueError text
+        raise ValueError(L.qfio_last_error().decode(errors="replace"))
+    _check(rc, "read_score_lists")
+    try:
+        sz = np.zeros(4, np.int64)
+        L.qfio_scorelists_sizes(h, _p(sz))
+        Q, n, qb, rows = (int(x) for x in sz)
+        qoff = np.empty(Q + 1, np.int64)
+        qch = np.empty(max(qb, 1), np.uint8)
+        loff = np.empty(Q + 1, np.int64)
+        sc = np.empty(max(n, 1), np.float64)
+        _check(L.qfio_scorelists_get(h, _p(qoff), _p(qch), _p(loff), _p(sc)), "read_score_lists")
+    finally:
+        L.qfio_scorelists_free(h)
+    raw = qch[:qb].tobytes()
+    qids = [raw[qoff[i]:qoff[i + 1]].decode() for i in range(Q)]  # ASCII (else EPYTHON)
+    return qids, loff, sc[:n], rows
 
 
 def _strings(off: np.ndarray, chars: np.ndarray) -> np.ndarray:
@@ -163,6 +200,11 @@ def format_score(x: float) -> str:
     buf = C.create_string_buffer(400)
     n = lib().qfio_format_score(float(x), buf)
     return buf.raw[:n].decode()
+
+
+def format_scores(x: np.ndarray) -> List[str]:
+    """[f"{v:.6f}" for v in x] (the .qpp writer's format, src/qpp.py:333)."""
+    return [f"{v:.6f}" for v in np.asarray(x, np.float64).tolist()]
 
 
 def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):

@@ -91,12 +91,18 @@ def java_floats(x: np.ndarray) -> np.ndarray:
 
 def _device_qpp(lists: List[List[float]], texts: List[str], top_k: int = 0) -> np.ndarray:
     """Raw predictors [L, 13] for L score lists (each used in the given order)."""
-    import torch
-    dev = engine.require_device()
     lens = np.fromiter((len(s) for s in lists), dtype=np.int64, count=len(lists))
     off = np.zeros(len(lists) + 1, dtype=np.int64)
     np.cumsum(lens, out=off[1:])
     flat = np.fromiter((float(x) for s in lists for x in s), dtype=np.float64, count=int(off[-1]))
+    return _device_qpp_flat(flat, off, texts, top_k)
+
+
+def _device_qpp_flat(flat: np.ndarray, off: np.ndarray, texts: List[str],
+                     top_k: int = 0) -> np.ndarray:
+    """Raw predictors [L, 13] of the lists flat[off[l]:off[l+1]] (qf_qpp_raw)."""
+    import torch
+    dev = engine.require_device()
     flat = java_floats(flat)  # Gson's float of the JSON decimal (QPPBridge.java:67-70)
     nt, tf = textfeat.feature_arrays(texts)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -143,7 +149,8 @@ class QPPBridge:
 
 
 def _read_scores(res_path: str):
-    """qid -> [scores] in file order, for lines with >= 5 fields (src/qpp.py:292-298)."""
+    """qid -> [scores] in file order, for lines with >= 5 fields (src/qpp.py:292-298):
+    the reference's own loop, for the files the native reader leaves to it."""
     runs = defaultdict(list)
     with open(res_path, "r") as fh:
         for line in fh:
@@ -153,10 +160,31 @@ def _read_scores(res_path: str):
     return runs
 
 
+def read_score_lists(res_path: str, top_k: int):
+    """(qids, list_off, scores): every query's scores sorted descending and cut to
+    top_k (src/qpp.py:292-305) — parsed and sorted natively (libqfio,
+    qfio_read_score_lists); a file only Python reads exactly (non-ASCII bytes,
+    digit underscores, NaN scores: include/qfio.h) goes through the reference's
+    loop and sorted()."""
+    from . import fastio
+    got = fastio.read_score_lists(res_path, top_k)
+    if got is not None:
+        return got[:3]
+    runs = _read_scores(res_path)
+    qids = list(runs.keys())
+    lists = [sorted(runs[q], reverse=True)[:top_k] for q in qids]
+    off = np.zeros(len(qids) + 1, np.int64)
+    np.cumsum([len(x) for x in lists], out=off[1:])
+    flat = np.fromiter((x for s in lists for x in s), np.float64, count=int(off[-1]))
+    return qids, off, flat
+
+
 def compute_qpp_for_res_file(res_path: str, output_path: Optional[str] = None,
                              top_k: int = None, normalize: str = None,
                              queries_path: Optional[str] = None) -> Dict[str, List[float]]:
-    """QPP of every query in a raw TREC .res file; writes <out>.qpp if asked."""
+    """QPP of every query in a raw TREC .res file; writes <out>.qpp if asked
+    (src/qpp.py:245-337).  Parse, per-query sort and top-k natively; the 13
+    predictors (qf_qpp_raw) and the per-column normalisation on device."""
     top_k = top_k or config.processing.retrieval.top_k
     normalize = normalize or config.qpp.normalization
     if not os.path.exists(res_path):
@@ -167,29 +195,41 @@ def compute_qpp_for_res_file(res_path: str, output_path: Optional[str] = None,
             for line in fh:
                 q = json.loads(line)
                 texts[q["_id"]] = q["text"]
-    runs = _read_scores(res_path)
-    if not runs:
+    qids, off, flat = read_score_lists(res_path, top_k)
+    if not qids:
         raise ValueError(f"No valid entries in run file: {res_path}")
-    qids = list(runs.keys())
-    # sorted(scores, reverse=True)[:top_k] per query (src/qpp.py:304-305)
-    lists = [sorted(runs[q], reverse=True)[:top_k] for q in qids]
     QPPBridge()
-    raw = _device_qpp(lists, [texts.get(q, q) for q in qids])
-    results = {q: raw[i].tolist() for i, q in enumerate(qids)}
+    raw = _device_qpp_flat(flat, off, [texts.get(q, q) for q in qids])
+    empty = np.diff(off) == 0  # Java's empty map: every name 0.0 (src/qpp.py:321)
+    if empty.any():
+        raw[empty] = 0.0
     # columns in config.qpp.methods order, absent names 0.0 (src/qpp.py:319-322)
     names = list(config.qpp.methods)
     if names != QPP_METHODS:
         pos = {n: i for i, n in enumerate(QPP_METHODS)}
-        results = {q: [v[pos[m]] if m in pos else 0.0 for m in names]
-                   for q, v in results.items()}
-    if normalize != "none" and results:
-        results = _normalize_qpp(results, normalize)
+        cols = np.zeros((len(qids), len(names)))
+        for j, m in enumerate(names):
+            if m in pos:
+                cols[:, j] = raw[:, pos[m]]
+        raw = cols
+    if normalize != "none":
+        raw = _normalize_array(raw, normalize)
+    results = {q: raw[i].tolist() for i, q in enumerate(qids)}
     if output_path:
-        with open(output_path, "w") as fh:
-            for qid in sorted(results.keys(), key=lambda x: int(x) if x.isdigit() else x):
-                fh.write(f"{qid}\t" + "\t".join(f"{s:.6f}" for s in results[qid]) + "\n")
+        order = sorted(range(len(qids)), key=lambda i: int(qids[i]) if qids[i].isdigit() else qids[i])
+        _write_qpp(output_path, [qids[i] for i in order], raw[order])
         print(f"Wrote QPP scores to {output_path}")
     return results
+
+
+def _write_qpp(path: str, qids: List[str], vals: np.ndarray) -> None:
+    """"{qid}\t" + "\t".join(f"{s:.6f}") per row (src/qpp.py:329-335)."""
+    from . import fastio
+    fmt = fastio.format_scores(np.ascontiguousarray(vals, np.float64).ravel())
+    n = vals.shape[1] if vals.ndim == 2 else 0
+    with open(path, "w") as fh:
+        fh.write("".join(f"{q}\t" + "\t".join(fmt[i * n:(i + 1) * n]) + "\n"
+                         for i, q in enumerate(qids)))
 
 
 def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, List[float]]:
@@ -197,10 +237,16 @@ def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, Li
     minmax (min / max) or zscore (numpy's mean / population std, bit-exact)."""
     qids = list(results.keys())
     arr = np.asarray([results[q] for q in qids], dtype=np.float64).reshape(len(qids), -1)
-    n_cols = arr.shape[1]
+    vals = _normalize_array(arr, method)
+    return {q: [float(v) for v in vals[i]] for i, q in enumerate(qids)}
+
+
+def _normalize_array(arr: np.ndarray, method: str) -> np.ndarray:
+    """_normalize_qpp of a [Q, n_cols] array (rows = queries in results order)."""
+    n_q, n_cols = arr.shape
     if n_cols > config.qpp.n_methods:  # method_values[i] of the reference (src/qpp.py:347-350)
         raise IndexError("list index out of range")
-    if method == "minmax" and (n_cols < config.qpp.n_methods or not qids):
+    if method == "minmax" and (n_cols < config.qpp.n_methods or not n_q):
         # the reference's minmax takes np.array([]).min() of every column no row
         # fills (config.qpp.methods shorter than n_methods, src/qpp.py:347-357)
         raise ValueError("zero-size array to reduction operation minimum which has no identity")
@@ -214,10 +260,9 @@ def _normalize_qpp(results: Dict[str, List[float]], method: str) -> Dict[str, Li
     dev = engine.require_device()
     raw = torch.from_numpy(arr).to(dev)
     # every list present; the padded row pieces of one query are the "retrievers"
-    off = torch.arange(len(qids) * rows_per + 1, dtype=torch.int64, device=dev)
+    off = torch.arange(n_q * rows_per + 1, dtype=torch.int64, device=dev)
     stats = (engine.qpp_colminmax if method == "minmax" else engine.qpp_colmeanstd)(
         raw, off, rows_per)
     norm = engine.qpp_normalize(raw, stats, off, rows_per, method, qpp_index=0, want_norm=True,
                                 want_micro=False, want_weights=False)["norm"]
-    vals = norm.cpu().numpy().reshape(len(qids), width)[:, :n_cols]
-    return {q: [float(v) for v in vals[i]] for i, q in enumerate(qids)}
+    return norm.cpu().numpy().reshape(n_q, width)[:, :n_cols]

@@ -24,19 +24,33 @@ def main():
     from qppfuse import engine
     from qppfuse.dist import PendingGather
     Q, R, K = 48, 5, 1000
-    off, docid, raw = engine.synth_runs(rank * Q, Q, R, K, seed=11)
-    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
-    nt = torch.full((Q,), 4, dtype=torch.int32, device=dev)
-    tf = torch.rand((Q, 2), dtype=torch.float64, device=dev)
+    methods = ["combsum", "rrf", "wcombsum"]
+
+    def shard(r):
+        """Rank r's inputs, regenerable on any rank (counter-based generator, seeded text)."""
+        import numpy as np
+        off, docid, raw = engine.synth_runs(r * Q, Q, R, K, seed=11)
+        g = np.random.default_rng([11, r])
+        nt = torch.from_numpy(g.integers(1, 12, Q).astype(np.int32)).to(dev)
+        tf = torch.from_numpy(g.random((Q, 2))).to(dev)
+        return off, docid, raw, nt, tf
+
+    def fuse_shard(r, mm):
+        off, docid, raw, nt, tf = shard(r)
+        _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+        qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
+        w = engine.qpp_normalize(qraw, mm, off, R, "minmax", 5)["weights"]
+        out = engine.fuse(off, docid, micro, R, methods, 60, weights=w, max_entries=R * K)
+        return out, off
+
+    off, docid, raw, nt, tf = shard(rank)
     qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
     mm = engine.qpp_colminmax(qraw, off, R)
     want = mm.clone()
     work = dist.all_reduce(mm, op=dist.ReduceOp.MIN, async_op=True)
     work.wait()
     assert torch.equal(mm, want) if world == 1 else bool((mm <= want).all())
-    w = engine.qpp_normalize(qraw, mm, off, R, "minmax", 5)["weights"]
-    out = engine.fuse(off, docid, micro, R, ["combsum", "rrf", "wcombsum"], 60, weights=w,
-                      max_entries=R * K)
+    out, off = fuse_shard(rank, mm)
     d, s = engine.fused_topk(out, off, R, 100)
     dl = [torch.empty_like(d) for _ in range(world)] if rank == 0 else None
     sl = [torch.empty_like(s) for _ in range(world)] if rank == 0 else None
@@ -60,9 +74,15 @@ def main():
     per = pending.wait()
     torch.cuda.synchronize()
     if rank == 0:
+        # every rank's rows: rank 0 regenerates each shard and fuses it with the
+        # global (all-reduced) QPP min / max — the rows must match byte for byte
         assert len(per) == world
-        pd_, ps_ = per[0]
-        assert torch.equal(pd_, d) and torch.equal(ps_.view(torch.int64), s.view(torch.int64))
+        for r in range(world):
+            o_r, off_r = fuse_shard(r, mm)
+            d_r, s_r = engine.fused_topk(o_r, off_r, R, 100)
+            pd_, ps_ = per[r]
+            assert torch.equal(pd_, d_r), r
+            assert torch.equal(ps_.view(torch.int64), s_r.view(torch.int64)), r
     dist.barrier()
     dist.destroy_process_group()
     print("rccl-ok", flush=True)

@@ -111,3 +111,37 @@ def test_product_never_imports_oracle():
     pkg = ROOT / "qpp-fusion-rag_amd"
     for f in pkg.rglob("*.py"):
         assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", f.read_text(), re.M), f
+
+
+def test_package_reexports_reference_names():
+    """src/__init__.py:28,37 re-exports these; qppfuse does too, lazily."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import qppfuse\n"
+        "from qppfuse import _lib\n"
+        "assert _lib._LIB is None, 'importing the package loaded the library'\n"
+        "assert 'qppfuse.fusion' not in sys.modules and 'torch' not in sys.modules\n"
+        "from qppfuse import (QPPBridge, compute_qpp_for_res_file, combsum, combmnz, rrf,\n"
+        "                     weighted_combsum, weighted_rrf, learned_fusion)\n"
+        "import qppfuse.fusion as F, qppfuse.qpp as Q\n"
+        "assert combsum is F.combsum and weighted_rrf is F.weighted_rrf\n"
+        "assert learned_fusion is F.learned_fusion and QPPBridge is Q.QPPBridge\n"
+        "assert compute_qpp_for_res_file is Q.compute_qpp_for_res_file\n"
+        "assert _lib._LIB is None\n"
+        "print('ok')\n") % str(ROOT / "qpp-fusion-rag_amd")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
+    import qppfuse
+    with pytest.raises(AttributeError):
+        qppfuse.no_such_name  # noqa: B018
+
+
+def test_stream_copy_validation():
+    from qppfuse import _lib
+    with pytest.raises(ValueError, match="16-byte"):
+        _lib.call("qf_stream_copy", 16, 16, 8, None)
+    with pytest.raises(ValueError, match="16-byte"):
+        _lib.call("qf_stream_copy", 17, 16, 16, None)
+    _lib.call("qf_stream_copy", None, None, 0, None)  # nothing to copy: no HIP call

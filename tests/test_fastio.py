@@ -160,6 +160,45 @@ def test_write_run_matches_python_writer(tmp_path):
         assert out.read_text() == "".join(want), threads
 
 
+def test_write_run_failure_leaves_existing_file(tmp_path):
+    """A failed write (here: the target is a directory entry we cannot replace)
+    leaves no temporary file behind and the old contents untouched."""
+    from qppfuse.runset import RunSet
+    rs = RunSet(qids=["q1"], rankers=["a"], docnos=np.array(["d0"], dtype=object),
+                list_off=np.zeros(2, np.int64), docid=np.zeros(0, np.uint32),
+                score=np.zeros(0), rank=np.zeros(0, np.int64))
+    target = tmp_path / "busy"
+    target.mkdir()  # rename(file, non-empty dir) fails
+    (target / "keep").write_text("old")
+    with pytest.raises(Exception):
+        fastio.write_run(str(target), np.zeros(1, np.int64), np.zeros(1, np.int64),
+                         np.array([1], np.int32), np.zeros(1, np.uint32), np.zeros(1, np.uint16),
+                         np.ones(1), rs, "t")
+    assert (target / "keep").read_text() == "old"
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["busy"]
+
+
+@pytest.mark.parametrize("dtype,n", [(np.int32, 4 * 2**20 // 4 + 3), (np.int8, 4 * 2**20 + 9),
+                                     (np.int8, 4 * 2**20 + 15), (np.float32, 2**20 + 7),
+                                     (np.int16, 13), (np.int8, 1)])
+def test_hash_bytes_tails(dtype, n):
+    """Every tail length of the 16-byte loop (9-15 bytes overflowed an 8-byte word
+    before round 4): the digest is deterministic and sees the last byte."""
+    rng = np.random.default_rng(n)
+    a = rng.integers(-100, 100, n).astype(dtype)
+    h = fastio.hash_bytes(a)
+    assert h == fastio.hash_bytes(a.copy())
+    b = a.copy()
+    b.view(np.uint8)[-1] ^= 0x5A
+    assert fastio.hash_bytes(b) != h
+    nbytes = a.nbytes
+    tail = nbytes % 16
+    for i in {nbytes - tail, nbytes - tail + 8} if tail > 8 else {nbytes - tail} if tail else ():
+        c = a.copy()
+        c.view(np.uint8)[i] ^= 1  # the first byte of each tail word
+        assert fastio.hash_bytes(c) != h, i
+
+
 def test_write_run_uint32_perm_beyond_65535():
     """A union of 70,000 documents: ranks past u = 65,535 through the uint32 perm."""
     import tempfile
@@ -311,3 +350,70 @@ def test_parse_line_shapes_against_pandas(tmp_path):
         for n in names:
             for c in ("qid", "iter", "docno", "runid"):
                 assert frames[n][c].astype(str).tolist() == pf[n][c].astype(str).tolist()
+
+
+def _py_score_lists(path, top_k):
+    """src/qpp.py:292-305 as the reference runs it."""
+    from collections import defaultdict
+    runs = defaultdict(list)
+    with open(path, "r") as f:
+        for line in f:
+            parts = line.strip().split()
+            if len(parts) >= 5:
+                runs[parts[0]].append(float(parts[4]))
+    return {q: sorted(v, reverse=True)[:top_k] for q, v in runs.items()}
+
+
+def _native_as_dict(got):
+    qids, off, sc = got[:3]
+    return {q: sc[off[i]:off[i + 1]].tolist() for i, q in enumerate(qids)}
+
+
+@pytest.mark.parametrize("top_k", [100, 3, 1, -2, 10**6])
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_read_score_lists_matches_reference_loop(tmp_path, top_k, threads):
+    rng = np.random.default_rng(7)
+    lines = []
+    qids = [f"q{i}" for i in rng.permutation(40)] + ["7", "test3", "10"]
+    for rep in range(2):  # qids interleaved: a query's rows in two blocks
+        for q in qids:
+            for k in range(int(rng.integers(0, 30))):
+                s = rng.choice([f"{rng.normal():.6f}", f"{rng.normal() * 1e5:.3e}", "0.0", "-0.0",
+                                "-0", "+1.5", "1.", ".5", "inf", "-Infinity", "1E-3",
+                                f"{rng.normal()!r}"])
+                tail = rng.choice(["bm25", "bm25 extra fields", ""])
+                lines.append(f"{q} Q0 d{k} {k + 1} {s} {tail}".rstrip())
+        lines += ["", "   ", "short line", "a b c d"]  # < 5 fields: skipped
+    p = tmp_path / "x.res"
+    p.write_text("\r\n".join(lines[:len(lines) // 2]) + "\r\n" + "\n".join(lines[len(lines) // 2:]))
+    want = _py_score_lists(p, top_k)
+    got = fastio.read_score_lists(str(p), top_k, n_threads=threads)
+    assert got is not None
+    assert list(want) == got[0]  # first-appearance order
+    g = _native_as_dict(got)
+    for q in want:  # bit-exact, -0.0 / 0.0 positions included
+        assert np.array(want[q]).tobytes() == np.array(g[q], np.float64).tobytes(), q
+    assert got[3] == sum(1 for ln in p.read_text().splitlines() if len(ln.split()) >= 5)
+
+
+@pytest.mark.parametrize("text", ["q1 Q0 d 1 0.5_1 t", "q1 Q0 d 1 nan t", "q1 Q0 dé 1 0.5 t",
+                                  "q1 Q0 d 1 0.5 t\rq2 Q0 e 1 0.25 t", "q1\x1cQ0 d 1 0.5 t"])
+def test_read_score_lists_defers_to_python(tmp_path, text):
+    p = tmp_path / "x.res"
+    p.write_text("q0 Q0 a 1 1.0 t\n" + text + "\n", newline="")
+    assert fastio.read_score_lists(str(p), 100) is None
+
+
+def test_read_score_lists_errors_like_float(tmp_path):
+    p = tmp_path / "x.res"
+    p.write_text("q0 Q0 a 1 1.0 t\nq0 Q0 b 2 0x1p3 t\n")
+    with pytest.raises(ValueError, match="could not convert string to float: '0x1p3'"):
+        fastio.read_score_lists(str(p), 100)
+    with pytest.raises(ValueError):
+        float("0x1p3")
+    with pytest.raises(FileNotFoundError):
+        fastio.read_score_lists(str(tmp_path / "missing.res"), 100)
+    e = tmp_path / "empty.res"
+    e.write_text("")
+    got = fastio.read_score_lists(str(e), 100)
+    assert got[0] == [] and got[1].tolist() == [0]

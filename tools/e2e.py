@@ -5,7 +5,11 @@ are generated once, then the reference's fusion entry points are timed through
 this package as scripts/05_fusion.py would call them:
   load_runs (native parse) -> load_qpp_scores -> fuse_many (6 methods: H2D,
   qf_fuse, D2H) -> write_runfile x 6 (native writer).
-python tools/e2e.py [--queries Q] [--dir DIR]
+--qpp: the 03_qpp stage instead — five raw `.res` files (the raw scores as
+02_retrieve writes them, "%.6f") through compute_qpp_for_res_file into `.qpp`
+files: in one warm process, file after file, and as scripts/03_qpp.py runs it
+(a fresh Python whose ProcessPoolExecutor gives every file its own worker).
+python tools/e2e.py [--queries Q] [--dir DIR] [--qpp]
 """
 import argparse
 import json
@@ -48,7 +52,7 @@ def ascii_table(prefix: bytes, ids: np.ndarray):
     return off, out.tobytes()
 
 
-def generate(d: Path, Q: int, R: int, K: int, cpu: bool = False):
+def generate(d: Path, Q: int, R: int, K: int, cpu: bool = False, raw_files: bool = False):
     from qppfuse import fastio
     if cpu:  # no GPU (loader work in the build container): numpy restatement + C oracle
         sys.path.insert(0, str(ROOT / "tools"))
@@ -80,6 +84,10 @@ def generate(d: Path, Q: int, R: int, K: int, cpu: bool = False):
         cnt = np.diff(off_h)[r::R][:Q].astype(np.int32)
         fastio.write_run(str(d / f"{name}.norm.res"), np.arange(Q), qb, cnt, ud, pos, sc_h, rs,
                          name)
+        if raw_files:  # the raw run 02_retrieve writes beside it (scripts/02_retrieve.py:80)
+            raw_h = raw if cpu else raw.cpu().numpy()
+            fastio.write_run(str(d / f"{name}.res"), np.arange(Q), qb, cnt, ud, pos, raw_h, rs,
+                             name)
     qd = d / "qpp"
     qd.mkdir(exist_ok=True)
     for r, name in enumerate(NAMES[:R]):
@@ -95,6 +103,7 @@ def main():
     ap.add_argument("--queries", type=int, default=3452)
     ap.add_argument("--dir", default=None)
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--qpp", action="store_true", help="time the 03_qpp stage (see above)")
     ap.add_argument("--load-only", action="store_true",
                     help="CPU only: generate with numpy, time load_runs (QFIO_TIMING=1 for phases)")
     a = ap.parse_args()
@@ -111,6 +120,8 @@ def main():
                               "rows": int(sum(len(df) for df in runs.values()))}), flush=True)
             del runs
         return
+    if a.qpp:
+        return qpp_stage(a, d)
     torch.cuda.set_device(0)
     t0 = time.perf_counter()
     E = generate(d, a.queries, 5, 1000)
@@ -142,6 +153,62 @@ def main():
     print(json.dumps({"queries": a.queries, "entries": E, "input_bytes": size,
                       "output_bytes": out_bytes, "generate_s": round(gen_s, 2), **best,
                       "e2e_fused_queries_per_s": round(a.queries * 6 / best["total_s"], 1),
+                      "cpu_threads": os.cpu_count()}), flush=True)
+
+
+POOL = """
+import os, sys
+sys.path[:0] = [{root!r}, {pkg!r}]
+from concurrent.futures import ProcessPoolExecutor, as_completed
+from qppfuse import compute_qpp_for_res_file
+
+def _process_qpp_file(job):  # scripts/03_qpp.py:31-36
+    compute_qpp_for_res_file(*job)
+    return job[0]
+
+if __name__ == "__main__":
+    d, out = sys.argv[1:3]
+    jobs = [(os.path.join(d, f), os.path.join(out, f.replace(".res", ".res.mmnorm.qpp")), 100,
+             "minmax", None) for f in sorted(os.listdir(d))
+            if f.endswith(".res") and not f.endswith(".norm.res")]
+    with ProcessPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+        for fut in as_completed([ex.submit(_process_qpp_file, j) for j in jobs]):
+            fut.result()
+"""
+
+
+def qpp_stage(a, d: Path):
+    """The 03_qpp stage file to file (see the module docstring)."""
+    import subprocess
+    from qppfuse.qpp import compute_qpp_for_res_file
+    torch.cuda.set_device(0)
+    if not any(d.glob("*.res")) or not (d / "BGE.res").exists():
+        generate(d, a.queries, 5, 1000, raw_files=True)
+    files = sorted(f for f in d.glob("*.res") if not f.name.endswith(".norm.res"))
+    size = sum(f.stat().st_size for f in files)
+    out = d / "qpp_one"
+    out.mkdir(exist_ok=True)
+    times = []
+    for _ in range(a.repeat + 1):  # the first pass warms the process (HIP context, caches)
+        t0 = time.perf_counter()
+        for f in files:
+            compute_qpp_for_res_file(str(f), str(out / f.name.replace(".res", ".res.mmnorm.qpp")))
+        times.append(time.perf_counter() - t0)
+    pool = d / "qpp_pool"
+    pool.mkdir(exist_ok=True)
+    script = d / "qpp03_pool.py"
+    script.write_text(POOL.format(root=str(ROOT), pkg=str(ROOT / "qpp-fusion-rag_amd")))
+    t0 = time.perf_counter()
+    subprocess.run([sys.executable, str(script), str(d), str(pool)], check=True,
+                   stdout=subprocess.DEVNULL)
+    pool_s = time.perf_counter() - t0
+    same = all((pool / f.name.replace(".res", ".res.mmnorm.qpp")).read_bytes() ==
+               (out / f.name.replace(".res", ".res.mmnorm.qpp")).read_bytes() for f in files)
+    print(json.dumps({"stage": "03_qpp", "files": len(files), "queries": a.queries,
+                      "input_bytes": size, "first_pass_s": round(times[0], 4),
+                      "warm_process_s": round(min(times[1:]), 4),
+                      "process_pool_wall_s": round(pool_s, 3),
+                      "pool_qpp_bytes_equal_single_process": same,
                       "cpu_threads": os.cpu_count()}), flush=True)
 
 
