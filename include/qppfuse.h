@@ -167,7 +167,8 @@ int qf_qpp_features(const int64_t* micro, int64_t n_queries, int32_t n_retriever
  * kernel (the same join in a global workspace + the bucket sort over the
  * workspace), launched only when max_entries > 10,240 (or n_retrievers > 16),
  * with a workspace allocated and freed stream-ordered (hipMallocAsync /
- * hipFreeAsync on `stream`) — the one internal allocation.  Larger queries (up
+ * hipFreeAsync on `stream`) — the one internal allocation; qf_fuse_ws below takes
+ * a caller-owned workspace instead.  Larger queries (up
  * to qf_max_entries_per_query_wide()) need qf_fuse_wide: u can exceed 65,535.
  * max_entries must bound every query's entry count (larger queries report
  * QF_QSTATUS_TOOBIG).  n_retrievers <= 32; with more than 16 every query takes
@@ -196,6 +197,27 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const int32_t* rank, const double* weights, int32_t methods, int32_t rrf_k,
             int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
             uint16_t* perm, double* fused, int64_t out_stride, void* stream);
+
+/*
+ * The explicit workspace of qf_fuse (the library allocates only in
+ * an explicit workspace).  qf_fuse_workspace_bytes: the bytes a call with these
+ * sizes would allocate stream-ordered for its workspace kernel (queries above
+ * 10,240 entries, or more than 16 runs); 0 when the call needs none.
+ * qf_fuse_ws = qf_fuse (wide = 0: uint16 perm) or qf_fuse_wide (wide = 1: uint32
+ * perm) with a caller-owned device workspace: ws = NULL keeps the stream-ordered
+ * allocation; otherwise ws_bytes must hold at least one workgroup's share (the
+ * call fails with QF_EINVAL naming it), and a workspace smaller than
+ * qf_fuse_workspace_bytes runs the workspace kernel with fewer workgroups (same
+ * results).  The workspace needs no initialisation and may be reused by the next
+ * call on the same stream; the library never frees it.
+ */
+int64_t qf_fuse_workspace_bytes(int64_t n_queries, int32_t n_retrievers, int32_t max_entries,
+                                int32_t methods, int32_t wide);
+int qf_fuse_ws(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+               const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
+               const double* weights, int32_t methods, int32_t rrf_k, int32_t max_entries,
+               uint32_t* union_docid, int32_t* union_count, void* perm, int32_t wide,
+               double* fused, int64_t out_stride, void* ws, size_t ws_bytes, void* stream);
 
 /*
  * qf_fuse, qf_fuse_probfuse, qf_fuse_learned_f32 and qf_fused_topk with a uint32

@@ -121,7 +121,8 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
                        int32_t rrf_k, const double* seg_prob, int32_t n_seg, int32_t seg_len,
                        int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
                        void* perm, int perm32, double* fused, int64_t out_stride,
-                       void* stream, const char* fn, uint32_t learned_f32 = 0u) {
+                       void* stream, const char* fn, uint32_t learned_f32 = 0u,
+                       void* ws = nullptr, size_t ws_bytes = 0) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "%s: n_retrievers must be in [1, %d]", fn, kMaxR);
   if (methods <= 0 ||
@@ -152,8 +153,15 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
     p.learned_f32 = learned_f32 & all;
     p.learned_sum_f32 = (learned_f32 & all) == all;
   }
+  if (ws) {
+    int64_t min_bytes = 0;
+    qf::fuse_workspace_bytes(n_queries, n_retrievers, max_entries, perm32, &min_bytes);
+    if ((int64_t)ws_bytes < min_bytes)
+      return fail(QF_EINVAL, "%s: workspace of %zu bytes, at least %lld needed", fn, ws_bytes,
+                  (long long)min_bytes);
+  }
   return check(qf::fuse_launch(p, score_kind, max_entries < 1 ? 1 : max_entries,
-                               (hipStream_t)stream),
+                               (hipStream_t)stream, ws, ws_bytes),
                fn);
 }
 
@@ -167,6 +175,27 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
   return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
                      methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
                      0, fused, out_stride, stream, "qf_fuse");
+}
+
+int64_t qf_fuse_workspace_bytes(int64_t n_queries, int32_t n_retrievers, int32_t max_entries,
+                                int32_t methods, int32_t wide) {
+  (void)methods;  // every method shares the one workspace per workgroup
+  if (n_queries <= 0 || n_retrievers <= 0 || n_retrievers > kMaxR || max_entries < 0 ||
+      max_entries > qf::fuse_max_entries(wide ? 1 : 0))
+    return 0;
+  return qf::fuse_workspace_bytes(n_queries, n_retrievers, max_entries, wide ? 1 : 0, nullptr);
+}
+
+int qf_fuse_ws(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+               const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
+               const double* weights, int32_t methods, int32_t rrf_k, int32_t max_entries,
+               uint32_t* union_docid, int32_t* union_count, void* perm, int32_t wide,
+               double* fused, int64_t out_stride, void* ws, size_t ws_bytes, void* stream) {
+  if (methods & QF_PROBFUSE)
+    return fail(QF_EINVAL, "qf_fuse_ws: QF_PROBFUSE needs qf_fuse_probfuse (segment table)");
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
+                     methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
+                     wide ? 1 : 0, fused, out_stride, stream, "qf_fuse_ws", 0u, ws, ws_bytes);
 }
 
 int qf_fuse_wide(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,

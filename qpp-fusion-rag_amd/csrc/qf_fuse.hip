@@ -136,11 +136,28 @@ __device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, ui
   return ~f64_asc_key(sx.sval[item & kUMask]);
 }
 
+// The lanes of the wave (active ones) whose kDigit-bit digit equals this lane's:
+// one ballot per digit bit, each lane keeping the lanes that agree with it.
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool active) {
+  uint64_t m = ballot(active);
+#pragma unroll
+  for (int b = 0; b < kDigit; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = ballot(bit);
+    m &= bit ? bb : ~bb;
+  }
+  return m;
+}
+
 // One stable counting-scatter pass on a kDigit-bit digit of the items.  Within a
-// wave every item takes its rank with one returning LDS atomic on its (wave,
-// digit) counter (lane order inside an instruction, program order across rows);
-// the (wave, digit) offsets are one block-wide exclusive scan in [digit][wave]
-// order.  Leaves the scattered sequence in sitem; `readback` reloads the registers.
+// wave every item's rank among the wave's items with its digit, in item order, is
+// built from orders the ISA fixes: inside a row, the lanes with its digit below it
+// (a ballot match, match_digit); across rows, the row's one returning LDS atomic
+// per digit — issued by the digit's lowest lane, adding the row's count — since a
+// wave's LDS instructions complete in program order.  No result depends on the
+// order in which one instruction's same-address atomics are applied.  The (wave,
+// digit) offsets are one block-wide exclusive scan in [digit][wave] order.  Leaves
+// the scattered sequence in sitem; `readback` reloads the registers.
 template <int ITEMS, int WAVES>
 __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
                                               uint32_t (&item)[ITEMS], int sh, bool readback) {
@@ -158,25 +175,29 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   QF_STAMP_INIT();
   for (int k = lane; k < kBuckets / 2; k += 64) hist[wid * (kBuckets / 2) + k] = 0u;
   // Rank of every item among its wave's items with the same digit, in item
-  // order: one returning LDS atomic per row on the (wave, digit) counter.  Rows
-  // are separate instructions (a wave's LDS ops are ordered), and inside one
-  // instruction gfx950 applies same-address LDS atomics in lane order — the
-  // property this stable sort rests on, measured by tools/lds_atomic_order.hip
-  // (12.6 M random and adversarial rows, 0 violations) and re-checked by the
-  // stability tests (tests/test_gpu_fusion.py).  This replaces a 9-ballot digit
-  // match per row (~45 VALU) with ~6 VALU and one ds_add_rtn.
+  // order (see above).  Round 3 took it from one ds_add_rtn per item, which is
+  // stable only because gfx950 happens to apply one instruction's same-address
+  // atomics in lane order (tools/lds_atomic_order.hip measured it; the ISA does
+  // not promise it): the match costs ~60 more VALU per row, on the paths that use
+  // this sort (small unions, the bucket sort's fallback pass, probFuse).
   uint32_t rank_in[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     rank_in[j] = 0u;
     if (j < rp) {  // wave-uniform
       const int i = (wid * rp + j) * 64 + lane;
-      if (i < sx.U) {
-        const uint32_t d = digit(item[j]);
-        const uint32_t hs = (d & 1u) * 16u;
-        const uint32_t old = atomicAdd(&hist[wid * (kBuckets / 2) + (d >> 1)], 1u << hs);
-        rank_in[j] = (old >> hs) & 0xFFFFu;
-      }
+      const bool act = i < sx.U;
+      const uint32_t d = act ? digit(item[j]) : 0u;
+      const uint64_t same = match_digit(d, act);
+      const uint32_t below = mbcnt(same);  // same-digit lanes before this one
+      const uint32_t hs = (d & 1u) * 16u;
+      uint32_t old = 0u;
+      if (act && below == 0u)  // the digit's lowest lane adds the row's count
+        old = atomicAdd(&hist[wid * (kBuckets / 2) + (d >> 1)],
+                        (uint32_t)__popcll(same) << hs);
+      const int leader = same ? __ffsll((unsigned long long)same) - 1 : lane;
+      old = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)old);
+      if (act) rank_in[j] = ((old >> hs) & 0xFFFFu) + below;
     }
   }
   QF_STAMP(8);
@@ -1316,6 +1337,34 @@ __device__ __forceinline__ uint32_t sel_if_eq_f64(double a, double s, uint32_t i
   return r;
 }
 
+// before + [member j precedes item i]: (kj > ki) or (kj == ki and tj < ti), for
+// ascending integer keys k (larger score first) and tie words t (smaller first) —
+// the borrow out of the 96-bit difference (ki, ~ti) - (kj, ~tj), added with carry:
+// four full-rate integer VALU ops and no scalar mask logic (the f64 compare form
+// needed two f64 compares, a u32 compare and three SALU combines per member).
+// The low word's ~ti - ~tj equals tj - ti (mod 2^32) with the same borrow.
+__device__ __forceinline__ uint32_t add_if_precedes(uint32_t before, uint64_t ki, uint32_t ti,
+                                                    uint64_t kj, uint32_t tj) {
+  uint32_t r, d;
+  asm("v_sub_co_u32_e32 %1, vcc, %3, %4\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %5, %6, vcc\n\t"
+      "v_subb_co_u32_e32 %1, vcc, %7, %8, vcc\n\t"
+      "v_addc_co_u32_e32 %0, vcc, 0, %2, vcc"
+      : "=v"(r), "=&v"(d)
+      : "v"(before), "v"(tj), "v"(ti), "v"((uint32_t)ki), "v"((uint32_t)kj),
+        "v"((uint32_t)(ki >> 32)), "v"((uint32_t)(kj >> 32))
+      : "vcc");
+  return r;
+}
+
+// The ascending integer key of a finite or infinite score, -0.0 folded into +0.0
+// (v + 0.0), so equal keys are exactly equal scores (NaN pairs take the fallback).
+__device__ __forceinline__ uint64_t bs_rank_key(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v + 0.0);
+  const uint64_t s = (uint64_t)((int64_t)b >> 63);
+  return b ^ (s | 0x8000000000000000ull);
+}
+
 // bsort_kernel's bucket-key constants for delta = range / 2^shift (every value
 // uniform over the workgroup): x = v + c (cform) or (v - smin) + delta, bucket key
 // (hi32(x) - b0) * scale >> 32.  ok = 0: a range the key cannot take.
@@ -1384,6 +1433,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   static_assert(kBcBytes >= 4 * kJsUMax && 6144 >= 8 * BLOCK, "region BC layout");
   __shared__ __attribute__((aligned(16))) unsigned char lds[8 * kJsUMax + kBcBytes];
   double* sval = (double*)lds;                                   // region A
+  uint64_t* skey = (uint64_t*)lds;  // region A from the scatter on: bs_rank_key by position
   uint32_t* sw = (uint32_t*)(lds + 8 * kJsUMax);                 // region BC: u << 20 | size << 8 | at
   uint16_t* bk = (uint16_t*)(lds + 8 * kJsUMax + 6144);          // bucket starts [NB + 8]
   uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                 // [NB + 1] u32
@@ -1631,7 +1681,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
       const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
       const uint32_t st = bk[b], nx = bk[b + 1];
       const uint32_t pos = st + at;
-      sval[pos] = v[j];
+      skey[pos] = bs_rank_key(v[j]);  // the rank phase compares integer keys
       if (BYDOC) sd[pos] = d[j];
       pa[j] = pos;
       pw[j] = ((uint32_t)u << 20) | ((nx - st) << 8) | at;
@@ -1652,7 +1702,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     P[j] = 0u;
     uo[j] = 0u;
     if (j < rows && i < U) {
-      const double vi = sval[i];
+      const uint64_t ki = skey[i];
       const uint32_t wi = sw[i];
       // the tie-break key: the whole word, whose top bits are u — distinct, so the
       // word order is the first-seen order — or, BYDOC, the docid
@@ -1662,25 +1712,21 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
       // the bucket's members by pointer (two per step; a bucket of one: nothing to
       // count): no index arithmetic inside the loop
       const uint32_t k0 = hi - lo > 1u ? lo : hi;
-      const double* pv = sval + k0;
-      const double* const pend = sval + hi;
-      const double* const plast = pend - 1;  // a pair remains while pv < plast
+      const uint64_t* pv = skey + k0;
+      const uint64_t* const pend = skey + hi;
+      const uint64_t* const plast = pend - 1;  // a pair remains while pv < plast
       const uint32_t* tp = BYDOC ? sd + k0 : sw + k0;
       for (; pv < plast; pv += 2, tp += 2) {
         // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the
         // compiler would merge them into (8 cycles: it serves 16 lanes at a time)
-        const double v0 = pv[0];
+        const uint64_t v0 = pv[0];
         asm volatile("" ::: "memory");
-        const double v1 = pv[1];
+        const uint64_t v1 = pv[1];
         const uint32_t t0 = tp[0], t1 = tp[1];
-        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (t0 < ti))) +
-                  (uint32_t)((v1 > vi) | ((v1 == vi) & (t1 < ti)));
+        before = add_if_precedes(before, ki, ti, v0, t0);
+        before = add_if_precedes(before, ki, ti, v1, t1);
       }
-      if (pv < pend) {
-        const double v0 = pv[0];
-        const uint32_t t0 = tp[0];
-        before += (uint32_t)((v0 > vi) | ((v0 == vi) & (t0 < ti)));
-      }
+      if (pv < pend) before = add_if_precedes(before, ki, ti, pv[0], tp[0]);
       P[j] = lo + before;
       uo[j] = wi >> 20;
     }
@@ -2509,22 +2555,61 @@ static void launch_sort_large(const FuseParams& p, int umin, hipStream_t st, int
 // Queries above the LDS join (QF_QSTATUS_TOOBIG after it): the workspace join,
 // which sorts only the unions the LDS sorts cannot hold (U > sort_min) and
 // leaves the rest, unsorted with their U, to the sort kernels launched after it.
-static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int nmin,
-                            int sort_min, hipStream_t st, void** ws_out) {
-  int tb = 1, pb = 0;
-  while ((1 << tb) < 2 * max_entries) ++tb;  // table load <= 1/2
-  while ((1 << pb) < max_entries) ++pb;
-  const int cap = p.perm32 ? kXlNMaxWide : kXlNMax;
-  const int nmax = max_entries < cap ? max_entries : cap;
-  const int64_t each = xl_ws_bytes(1 << tb, nmax, 1 << pb);
-  // workgroups: two per CU while the workspace stays within 4 GB (1.4 % of HBM);
-  // very large queries get fewer (each workgroup runs its queries in turn)
-  int64_t g = ((int64_t)4 << 30) / each;
+// The workspace kernel's shape for queries of up to max_entries entries: table /
+// partition bits, entries per query, bytes per workgroup, and the workgroups the
+// stream-ordered allocation would give it (two per CU while the workspace stays
+// within 4 GB — 1.4 % of HBM; very large queries get fewer, each workgroup runs its
+// queries in turn).
+struct XlShape {
+  int tb, pb, nmax;
+  int64_t each, grid;
+};
+static XlShape xl_shape(int64_t n_queries, int perm32, int max_entries) {
+  XlShape s{1, 0, 0, 0, 0};
+  while ((1 << s.tb) < 2 * max_entries) ++s.tb;  // table load <= 1/2
+  while ((1 << s.pb) < max_entries) ++s.pb;
+  const int cap = perm32 ? kXlNMaxWide : kXlNMax;
+  s.nmax = max_entries < cap ? max_entries : cap;
+  s.each = xl_ws_bytes(1 << s.tb, s.nmax, 1 << s.pb);
+  int64_t g = ((int64_t)4 << 30) / s.each;
   g = g < 1 ? 1 : (g > kXlGrid ? kXlGrid : g);
-  if (p.n_queries < g) g = p.n_queries;
-  hipError_t e = hipMallocAsync(ws_out, (size_t)(each * g), st);
-  if (e != hipSuccess) return e;
-  unsigned char* ws = (unsigned char*)*ws_out;
+  if (n_queries < g) g = n_queries;
+  s.grid = g < 1 ? 1 : g;
+  return s;
+}
+
+// Whether a call takes the workspace kernel (include/qppfuse.h qf_fuse).
+static bool needs_xl(int R, int max_entries) {
+  return R > kRMax || max_entries > JoinXL::kNMax;
+}
+
+int64_t fuse_workspace_bytes(int64_t n_queries, int R, int max_entries, int perm32,
+                             int64_t* min_bytes) {
+  if (min_bytes) *min_bytes = 0;
+  if (n_queries <= 0 || !needs_xl(R, max_entries)) return 0;
+  const XlShape s = xl_shape(n_queries, perm32, max_entries < 1 ? 1 : max_entries);
+  if (min_bytes) *min_bytes = s.each;
+  return s.each * s.grid;
+}
+
+static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int nmin,
+                            int sort_min, hipStream_t st, void** ws_out, void* ws_user,
+                            size_t ws_bytes) {
+  const XlShape s = xl_shape(p.n_queries, p.perm32, max_entries);
+  const int tb = s.tb, pb = s.pb, nmax = s.nmax;
+  const int64_t each = s.each;
+  int64_t g = s.grid;
+  unsigned char* ws;
+  if (ws_user) {  // the caller's workspace: as many workgroups as it holds (>= 1, checked)
+    const int64_t fit = (int64_t)(ws_bytes / (size_t)each);
+    if (fit < g) g = fit;
+    if (g < 1) return hipErrorInvalidValue;
+    ws = (unsigned char*)ws_user;
+  } else {
+    hipError_t e = hipMallocAsync(ws_out, (size_t)(each * g), st);
+    if (e != hipSuccess) return e;
+    ws = (unsigned char*)*ws_out;
+  }
   if (kind == 1)
     hipLaunchKernelGGL((join_sort_xl_kernel<1>), dim3((unsigned)g), dim3(kXlBlock), 0, st, p,
                        nmin, ws, each, nmax, tb, pb, sort_min);
@@ -2534,7 +2619,8 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
   return hipGetLastError();
 }
 
-hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st) {
+hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st,
+                       void* ws_user, size_t ws_bytes) {
   void* ws = nullptr;
   hipError_t e = hipSuccess;
   if (p.R <= kRMax && max_entries <= JoinXL::kNMax && max_entries > JoinS::kNMax) {
@@ -2556,7 +2642,8 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
   }
   if (p.R > kRMax) {
     // more runs than the LDS join's masks hold: every query takes the workspace join
-    e = launch_xl(p, kind, max_entries < 1 ? 1 : max_entries, -1, SortXL::kUMax, st, &ws);
+    e = launch_xl(p, kind, max_entries < 1 ? 1 : max_entries, -1, SortXL::kUMax, st, &ws,
+                  ws_user, ws_bytes);
   } else if (max_entries <= JoinS::kNMax) {
     launch_join<JoinS>(p, kind, st);
   } else {
@@ -2564,7 +2651,8 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
     else launch_join<JoinXL>(p, kind, st);
     if (max_entries > JoinXL::kNMax)
-      e = launch_xl(p, kind, max_entries, JoinXL::kNMax, SortXL::kUMax, st, &ws);
+      e = launch_xl(p, kind, max_entries, JoinXL::kNMax, SortXL::kUMax, st, &ws, ws_user,
+                    ws_bytes);
   }
   if (e == hipSuccess) {
     if (max_entries <= SortS::kUMax) {

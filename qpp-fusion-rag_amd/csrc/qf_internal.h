@@ -127,7 +127,14 @@ hipError_t mlp_weights_launch(const MlpParams& p, hipStream_t st);
 
 int fuse_max_entries(int wide);
 hipError_t eval_launch(const EvalParams& p, hipStream_t st);
-hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st);
+// ws_user (nullable): the caller's workspace of ws_bytes for the workspace kernel;
+// NULL = stream-ordered allocation (hipMallocAsync / hipFreeAsync on st)
+hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st,
+                       void* ws_user = nullptr, size_t ws_bytes = 0);
+// Bytes of the workspace fuse_launch would allocate (0: no workspace kernel);
+// *min_bytes: the least a caller's workspace may hold (one workgroup's share).
+int64_t fuse_workspace_bytes(int64_t n_queries, int R, int max_entries, int perm32,
+                             int64_t* min_bytes);
 hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
                        const int32_t* union_count, const uint32_t* union_docid,
                        const void* perm, int perm32, const double* fused, int64_t out_stride,

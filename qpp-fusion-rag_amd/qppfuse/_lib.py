@@ -61,6 +61,9 @@ SIGNATURES = {
                                       _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
     "qf_stream_copy": (C.c_int, [_vp, _vp, _i64, _vp]),
+    "qf_fuse_workspace_bytes": (C.c_int64, [_i64, _i32, _i32, _i32, _i32]),
+    "qf_fuse_ws": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
+                             _vp, _vp, _vp, _i32, _vp, _i64, _vp, C.c_size_t, _vp]),
 }
 for _n in ("qf_fuse", "qf_fuse_probfuse", "qf_fuse_learned_f32", "qf_fused_topk"):
     SIGNATURES[_n + "_wide"] = SIGNATURES[_n]
@@ -88,7 +91,10 @@ def lib() -> C.CDLL:
                 f"libqppfuse.so not built at {path}. Run `python __graft_entry__.py build` "
                 "(hipcc --offload-arch=gfx950). qppfuse has no CPU fallback.")
         handle = C.CDLL(str(path))
+        dev_build = "QPPFUSE_LIB" in os.environ  # an older build under A/B may lack new symbols
         for name, (res, args) in SIGNATURES.items():
+            if dev_build and not hasattr(handle, name):
+                continue
             fn = getattr(handle, name)
             fn.restype, fn.argtypes = res, args
         _LIB = handle

@@ -113,13 +113,16 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
          rank: Optional[torch.Tensor] = None, max_entries: Optional[int] = None,
          out: Optional[FuseOut] = None, seg_prob: Optional[torch.Tensor] = None,
          n_segments: int = 0, seg_len: int = 0,
-         learned_f32: Optional[int] = None) -> FuseOut:
+         learned_f32: Optional[int] = None,
+         workspace: Optional[torch.Tensor] = None) -> FuseOut:
     """qf_fuse over every query of a packed run set (see include/qppfuse.h); with
     "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table;
     methods == ["learned"] with learned_f32 (run bitmask: float32 model weights,
     FusionMLP), qf_fuse_learned_f32.  A query above qf_max_entries_per_query()
     (65,535) entries takes the _wide entry points (uint32 perm): `out` is then
-    allocated wide (alloc_fuse_out(..., wide=True))."""
+    allocated wide (alloc_fuse_out(..., wide=True)).  `workspace`: a caller-owned
+    device byte buffer for the workspace kernel (qf_fuse_ws; workspace_bytes() sizes
+    it) instead of the library's stream-ordered allocation."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
@@ -160,11 +163,28 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
                   _ptr(out.union_docid), _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused),
                   out.fused.shape[1], _stream())
         return out
+    if workspace is not None:
+        if workspace.device != out.fused.device or not workspace.is_contiguous():
+            raise ValueError("workspace must be a contiguous buffer on the fusion's device")
+        _lib.call("qf_fuse_ws", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
+                  _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
+                  _ptr(out.union_count), _ptr(out.perm), 1 if wide else 0, _ptr(out.fused),
+                  out.fused.shape[1], _ptr(workspace),
+                  workspace.numel() * workspace.element_size(), _stream())
+        return out
     _lib.call("qf_fuse" + sfx, Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
               _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
               _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused), out.fused.shape[1],
               _stream())
     return out
+
+
+def workspace_bytes(n_queries: int, n_retrievers: int, max_entries: int, methods) -> int:
+    """qf_fuse_workspace_bytes: the workspace a fuse() call of these sizes would
+    allocate (0: none; queries <= 10,240 entries and <= 16 runs need none)."""
+    return int(_lib.lib().qf_fuse_workspace_bytes(int(n_queries), int(n_retrievers),
+                                                  int(max_entries), methods_mask(methods),
+                                                  1 if needs_wide(max_entries) else 0))
 
 
 def minmax_per_query(score: torch.Tensor, list_off: torch.Tensor, want_norm=True,

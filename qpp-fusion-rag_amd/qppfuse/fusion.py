@@ -317,17 +317,15 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
                                        output_size=total)
         idx = qb[q_of] + (torch.arange(total, device=dev) - cb[q_of])
         # into pinned host buffers (torch's caching host allocator keeps them for the
-        # next call), three copies queued, one synchronisation
-        hosts = []
-        for t in (out.union_docid[idx], out.perm[:, idx], out.fused[:, idx], cb):
-            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            h.copy_(t, non_blocking=True)
-            hosts.append(h)
+        # next call) while the live pinned copy-backs stay under a cap, pageable
+        # beyond it; the copies queued, one synchronisation
+        hosts = [_host_copy(t) for t in (out.union_docid[idx], out.perm[:, idx],
+                                         out.fused[:, idx], cb)]
         torch.cuda.current_stream(dev).synchronize()
-        udoc = hosts[0].numpy().view(np.uint32)
-        perm = hosts[1].numpy().view(np.uint32 if out.wide else np.uint16)
-        fused = hosts[2].numpy()
-        qbase = hosts[3].numpy()
+        udoc = hosts[0].view(np.uint32)
+        perm = hosts[1].view(np.uint32 if out.wide else np.uint16)
+        fused = hosts[2]
+        qbase = hosts[3]
     else:
         udoc = out.union_docid.cpu().numpy()[:E].view(np.uint32)
         perm = out.perm.cpu().numpy()[:, :E].view(np.uint32 if out.wide else np.uint16)
@@ -339,6 +337,45 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
         res[name] = FusedRun(rs.qids, rs.docnos, qbase, counts, udoc, perm[m],
                              fused[m], order, rs)
     return res
+
+
+# Page-locked bytes held by live FusedRuns (their numpy views keep the host tensors
+# alive).  A FusedRun's arrays are pinned while the total stays under the cap
+# (QPPFUSE_PINNED_CAP_MB, default 4096): pinned pages cannot be swapped, and torch's
+# caching host allocator keeps freed pinned blocks for reuse rather than returning
+# them, so workflows that keep many runs alive (argmax_runs' 13 QPP-column runs,
+# experiment) would otherwise grow page-locked memory without bound.  Beyond the
+# cap the copy-back lands in pageable memory (~5x slower, same bytes).
+_PINNED = {"live": 0}
+
+
+def _pinned_cap() -> int:
+    return int(os.environ.get("QPPFUSE_PINNED_CAP_MB", "4096")) << 20
+
+
+def _release_pinned(nbytes: int) -> None:
+    _PINNED["live"] -= nbytes
+
+
+def _host_copy(t) -> np.ndarray:
+    """t's bytes queued for a copy into host memory (valid after a stream
+    synchronisation), as a numpy array — the object the FusedRun's views keep
+    alive (a tensor's .numpy() holds its storage, not the tensor)."""
+    import torch
+    nbytes = t.numel() * t.element_size()
+    pinned = _PINNED["live"] + nbytes <= _pinned_cap()
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pinned)
+    h.copy_(t, non_blocking=True)  # pageable: the runtime stages it
+    a = h.numpy()
+    if pinned:
+        _PINNED["live"] += nbytes
+        weakref.finalize(a, _release_pinned, nbytes)
+    return a
+
+
+def pinned_bytes_live() -> int:
+    """Page-locked bytes the live FusedRuns hold (see _PINNED)."""
+    return _PINNED["live"]
 
 
 def fuse_many(runs: Dict[str, pd.DataFrame], methods: Sequence[str], qpp_data=None,

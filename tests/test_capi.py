@@ -145,3 +145,26 @@ def test_stream_copy_validation():
     with pytest.raises(ValueError, match="16-byte"):
         _lib.call("qf_stream_copy", 17, 16, 16, None)
     _lib.call("qf_stream_copy", None, None, 0, None)  # nothing to copy: no HIP call
+
+
+def test_fuse_workspace_bytes():
+    """qf_fuse_workspace_bytes is host arithmetic: 0 without the workspace kernel,
+    the stream-ordered allocation's size with it (capped at 4 GB, two workgroups
+    per CU at most)."""
+    from qppfuse import engine
+    assert engine.workspace_bytes(3452, 5, 5000, ["combsum"]) == 0
+    assert engine.workspace_bytes(3452, 10, 10240, ["combsum"]) == 0
+    one = engine.workspace_bytes(1, 5, 100_000, ["combsum"])
+    two = engine.workspace_bytes(2, 5, 100_000, ["combsum"])
+    assert one > 0 and two == 2 * one
+    assert engine.workspace_bytes(10**6, 5, 100_000, ["rrf"]) <= 4 << 30
+    assert engine.workspace_bytes(4, 20, 500, ["rrf"]) > 0   # > 16 runs: the workspace kernel
+    assert engine.workspace_bytes(0, 5, 100_000, ["rrf"]) == 0
+
+
+def test_fuse_ws_rejects_a_short_workspace():
+    from qppfuse import _lib, engine
+    need = engine.workspace_bytes(1, 5, 100_000, ["rrf"])
+    with pytest.raises(ValueError, match="workspace"):
+        _lib.call("qf_fuse_ws", 1, 5, 8, 8, 8, 0, None, None, _lib.RRF, 60, 100_000, 8, 8, 8, 1,
+                  8, 16, 8, need - 1, None)

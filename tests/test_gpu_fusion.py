@@ -743,3 +743,50 @@ def test_wide_api_fuse_and_write_runfile(gpu, tmp_path):
     qrels = {"q1": {ranked[i]: 1 + i % 2 for i in (0, 7, 500, 70_000)} | {"dx": 1}}
     assert ev.evaluate(got["rrf"], qrels, per_query=True) == \
         ev.evaluate({"q1": got["rrf"]["q1"]}, qrels, per_query=True)
+
+
+@pytest.mark.parametrize("share", ["full", "one"])
+def test_caller_owned_workspace(gpu, share):
+    """qf_fuse_ws: the workspace kernel in the caller's buffer (the full size
+    qf_fuse_workspace_bytes names, or one workgroup's share: fewer workgroups),
+    100,000-entry and small queries in one call, bit-exact vs the oracle and
+    identical to the stream-ordered allocation's outputs; reused twice."""
+    from qppfuse import engine
+    R = 4
+    rng = np.random.default_rng(44)
+    sizes = [25000, 300, 16383, 0, 2600]
+    lists = []
+    for K in sizes:
+        pool = rng.choice(1 << 30, size=max(1, 2 * K), replace=False).astype(np.uint32)
+        for r in range(R):
+            k = K if r != 1 else K // 3
+            docs = rng.choice(pool, size=k, replace=False)
+            lists.append((docs, np.sort(rng.integers(0, 5000 + r * 7919, k))[::-1] / 1e6))
+    off, doc, sc, doff, ddoc, dsc = _csr(lists, gpu)
+    n_max = int(np.max(off[R::R] - off[0:-1:R]))
+    assert n_max > 65535  # the wide perm
+    w = rng.uniform(0.05, 1.0, len(sizes) * R)
+    wd = torch.from_numpy(w).to(gpu)
+    full = engine.workspace_bytes(len(sizes), R, n_max, ALL)
+    one = engine.workspace_bytes(1, R, n_max, ALL)
+    assert full >= one > 0
+    ws = torch.empty(full if share == "full" else one, dtype=torch.uint8, device=gpu)
+    ref = engine.fuse(doff, ddoc, dsc, R, ALL, 60, weights=wd, max_entries=n_max)
+    for _ in range(2):
+        out = engine.fuse(doff, ddoc, dsc, R, ALL, 60, weights=wd, max_entries=n_max,
+                          workspace=ws)
+        torch.cuda.synchronize()
+        assert torch.equal(out.union_count, ref.union_count)
+        assert torch.equal(out.union_docid, ref.union_docid)
+        assert torch.equal(out.perm, ref.perm)
+        assert torch.equal(out.fused.view(torch.int64), ref.fused.view(torch.int64))
+    uc = out.union_count.cpu().numpy()
+    perm = _perm_np(out)
+    fz = out.ranked_fused().cpu().numpy()
+    for m, name in enumerate(ALL):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off, doc, sc, R, name, 60, weights=w)
+        np.testing.assert_array_equal(uc, o_uc)
+        for q in range(len(sizes)):
+            b, n = off[q * R], uc[q]
+            np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=name)
+            assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)

@@ -4,10 +4,10 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "qpp-fusion-rag_amd")]
 import os
+if os.environ.get("QF_LIB"):  # a development build of the same sources
+    os.environ["QPPFUSE_LIB"] = os.environ["QF_LIB"]
 import torch
 from qppfuse import engine, _lib
-if os.environ.get("QF_LIB"):  # a development build of the same sources
-    _lib.LIB_PATH = Path(os.environ["QF_LIB"])
 Q, R, K = 3452, 5, 1000
 dev = torch.device("cuda", 0)
 off, docid, raw = engine.synth_runs(0, Q, R, K)
