@@ -1419,8 +1419,37 @@ __device__ __forceinline__ BsKey bs_key_params(double smin, double smax, bool na
 // loaded with the scores, the minimum's sub-buckets split by docid, the rank
 // compares docids (a u32 by position: 12 KB more LDS, 3 workgroups per CU).
 // Without BYDOC the learned slot is skipped (its own launch takes it).
+// The bucket sort's small shared state (block reductions, flags, key constants).
+template <int WAVES>
+struct BsShared {
+  uint32_t wtot[WAVES], big[WAVES];
+  double mn, mx;
+  int wnan[WAVES], nan;
+  uint32_t dmn, dmx;
+  BsKey key;  // wave 0's key constants for the first count
+};
+
+// LDS bytes of bsort_core's area (region A + region BC; BYDOC's docids after it).
+template <int BITS, bool BYDOC>
+struct BsLds {
+  static constexpr int kNB = 1 << BITS;
+  static constexpr int kBcBytes = 6144 + 2 * (kNB + 8);
+  static constexpr int kSd = 8 * kJsUMax + kBcBytes;  // BYDOC: docid by position
+  static constexpr int kBytes = kSd + (BYDOC ? 4 * kJsUMax : 0);
+};
+
+// The bucket sort of one (query, method slot) pair whose U scores are in
+// registers: item j of this lane is u = ub0 + j * ustep + lane (ub0, ustep
+// 64-aligned and wave-uniform; every u in [0, rows * BLOCK) held by exactly one
+// lane), v[j] its score, d[j] its docid (BYDOC).  lds: BsLds<BITS, BYDOC>::kBytes
+// of LDS no one else uses until the call returns.  Writes perm[po + i] (or marks
+// perm[po] for the fallback pass).  Every thread of the block calls it.
 template <int BLOCK, int BITS, bool BYDOC>
-__global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams p) {
+__device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* lds,
+                                           BsShared<BLOCK / 64>& sm,
+                                           double (&v)[(kJsUMax + BLOCK - 1) / BLOCK],
+                                           uint32_t (&d)[BYDOC ? (kJsUMax + BLOCK - 1) / BLOCK : 1],
+                                           int U, int ub0, int ustep, int64_t po) {
   constexpr int WAVES = BLOCK / 64, ROWS = (kJsUMax + BLOCK - 1) / BLOCK, NB = 1 << BITS;
   constexpr int MINSUB = NB / 16, MINBASE = NB - MINSUB;
   static_assert(2 * BLOCK * 8 + 4 * NB <= 8 * kJsUMax, "partials + counters overlay the scores");
@@ -1429,20 +1458,278 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   // region BC after it = the u | size | arrival words by position (u32 [kJsUMax],
   // from the scatter on), before that the bucket starts (u16, at BC + 6 KB), the
   // spare counter cnt[NB] (BC[0]) and BYDOC's docid partials (BC[0, 4 KB)).
-  constexpr int kBcBytes = 6144 + 2 * (NB + 8);
+  constexpr int kBcBytes = BsLds<BITS, BYDOC>::kBcBytes;
   static_assert(kBcBytes >= 4 * kJsUMax && 6144 >= 8 * BLOCK, "region BC layout");
-  __shared__ __attribute__((aligned(16))) unsigned char lds[8 * kJsUMax + kBcBytes];
   double* sval = (double*)lds;                                   // region A
   uint64_t* skey = (uint64_t*)lds;  // region A from the scatter on: bs_rank_key by position
   uint32_t* sw = (uint32_t*)(lds + 8 * kJsUMax);                 // region BC: u << 20 | size << 8 | at
   uint16_t* bk = (uint16_t*)(lds + 8 * kJsUMax + 6144);          // bucket starts [NB + 8]
   uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                 // [NB + 1] u32
-  __shared__ uint32_t sd[BYDOC ? kJsUMax : 1];  // docid by position (BYDOC)
-  __shared__ uint32_t s_wtot[WAVES], s_big[WAVES];
-  __shared__ double s_mn, s_mx;
-  __shared__ int s_wnan[WAVES], s_nan;
-  __shared__ uint32_t s_dmn, s_dmx;
-  __shared__ BsKey s_key;  // wave 0's key constants for the first count
+  uint32_t* sd = (uint32_t*)(lds + BsLds<BITS, BYDOC>::kSd);     // docid by position (BYDOC)
+  const int tid = threadIdx.x, lane = tid & 63,
+            wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rows = (U + BLOCK - 1) / BLOCK;
+  const int pbase = wid * rows * 64;  // this wave's positions: [pbase, pbase + rows * 64)
+  {  // zero the counters (region A beyond the partials)
+    uint4* c4 = (uint4*)cnt;
+#pragma unroll
+    for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  {  // score range (NaN flagged): every thread's partials, reduced by wave 0
+    double vmn = INFINITY, vmx = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = ub0 + j * ustep + lane;
+      if (j < rows && u < U) {
+        vmn = raw_min_f64(vmn, v[j]);
+        vmx = raw_max_f64(vmx, v[j]);
+        nan |= v[j] != v[j];
+      }
+    }
+    sval[tid] = vmn;
+    sval[BLOCK + tid] = vmx;
+    if (BYDOC) {  // docid range: partials in region B (free until the scatter)
+      uint32_t dmn = ~0u, dmx = 0u;
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) {
+        const int u = ub0 + j * ustep + lane;
+        if (j < rows && u < U) {
+          dmn = min(dmn, d[j]);
+          dmx = max(dmx, d[j]);
+        }
+      }
+      sw[tid] = dmn;
+      sw[BLOCK + tid] = dmx;
+    }
+    const bool anynan = ballot(nan) != 0ull;
+    if (lane == 0) sm.wnan[wid] = anynan ? 1 : 0;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    __builtin_amdgcn_s_setprio(3);  // the block waits on this wave
+    double mn = sval[lane], mx = sval[BLOCK + lane];
+#pragma unroll
+    for (int i = 1; i < WAVES; ++i) {
+      mn = raw_min_f64(mn, sval[i * 64 + lane]);
+      mx = raw_max_f64(mx, sval[BLOCK + i * 64 + lane]);
+    }
+    mn = wave_min_f64_dpp(mn);
+    mx = wave_max_f64_dpp(mx);
+    uint32_t dmn = 0u, dmx = 0u;
+    if (BYDOC) {
+      const uint32_t* sp = sw;
+      dmn = sp[lane];
+      dmx = sp[BLOCK + lane];
+#pragma unroll
+      for (int i = 1; i < WAVES; ++i) {
+        dmn = min(dmn, sp[i * 64 + lane]);
+        dmx = max(dmx, sp[BLOCK + i * 64 + lane]);
+      }
+      dmn = (uint32_t)wave_min_u64_dpp(dmn);
+      dmx = (uint32_t)wave_max_u64_dpp(dmx);
+    }
+    int anyn = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) anyn |= sm.wnan[w];
+    if (lane == 63) {
+      // the folded extremes (-0.0 == +0.0) and the first count's key constants,
+      // once here instead of in every wave after the barrier
+      const double fmx = f64_from_asc_key(f64_asc_key(mx)), fmn = f64_from_asc_key(f64_asc_key(mn));
+      sm.mn = fmn;
+      sm.mx = fmx;
+      sm.nan = anyn;
+      sm.dmn = dmn;
+      sm.dmx = dmx;
+      sm.key = bs_key_params<MINBASE, BYDOC>(fmn, fmx, anyn != 0, QF_BSORT_DELTA_SHIFT);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __syncthreads();
+  const bool nan = sm.nan != 0;
+  if (!BYDOC && sm.mn == sm.mx && !nan) {  // every score equal: first-seen order
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = ub0 + j * ustep + lane;
+      if (j < rows && u < U) perm_put(p, po + u, (uint32_t)u);
+    }
+    return;
+  }
+  const double smax = sm.mx, smin = sm.mn;
+  int ush = 0;  // U - 1 >> ush < MINSUB
+  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
+  const uint32_t dmin = BYDOC ? sm.dmn : 0u;
+  int dsh = 0;  // BYDOC: (dmax - dmin) >> dsh < MINSUB
+  if (BYDOC)
+    while (((sm.dmx - dmin) >> dsh) >= (uint32_t)MINSUB) ++dsh;
+  // the minimum's sub-bucket of row j: MINBASE + (ub0 + ustep j + lane) >> ush, with
+  // 64-aligned row bases and ush <= 6 (U <= kJsUMax): a per-lane part + a row part
+  static_assert(((kJsUMax - 1) >> 6) < MINSUB, "ush <= 6");
+  const uint32_t lane_sub = (uint32_t)lane >> ush;
+  uint32_t ws[ROWS];  // bucket | arrival index << 16
+  // count with delta = range / 2^shift: -1 = a range the key cannot take (the
+  // pair is marked), else whether some bucket exceeds kJsBucketMax
+  // one row pass of the count: CF = the v + c form.  Every row's atomic is issued
+  // before any result is used (one wait); a lane past U adds to the spare counter
+  // cnt[NB] (in region B, free until the scatter), so no branch surrounds them
+  auto count_rows = [&](auto cf, double c, double delta, uint32_t b0, uint32_t scale) -> bool {
+    constexpr bool CF = decltype(cf)::value;
+    uint32_t old[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (j < rows) {  // uniform
+        const int u = ub0 + j * ustep + lane;
+        const double x = CF ? v[j] + c : (v[j] - smin) + delta;
+        const uint32_t hx = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
+        const uint32_t minb = BYDOC ? (uint32_t)MINBASE + ((d[j] - dmin) >> dsh)
+                                    : (uint32_t)MINBASE + ((uint32_t)(ub0 + ustep * j) >> ush) + lane_sub;
+        const uint32_t key = __umulhi(hx - b0, scale);  // < MINBASE, non-decreasing in x
+        uint32_t b = sel_if_eq_f64(v[j], smin, minb, (uint32_t)(MINBASE - 1) - key);
+        b = u < U ? b : (uint32_t)NB;
+        ws[j] = b;
+        old[j] = atomicAdd(&cnt[b], 1u);
+      }
+    }
+    bool bigl = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (j < rows) {
+        bigl |= (old[j] >= (uint32_t)kJsBucketMax) & (ws[j] < (uint32_t)NB);
+        ws[j] |= old[j] << 16;
+      }
+    }
+    return bigl;
+  };
+  // count with delta = range / 2^shift: -1 = a range the key cannot take (the
+  // pair is marked), else whether some bucket exceeds kJsBucketMax
+  auto count = [&](const BsKey& kp) -> int {
+    if (!kp.ok) return -1;  // uniform
+    const double c = rfl_f64(kp.c), delta = kp.delta;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(kp.b0);
+    const uint32_t scale = __builtin_amdgcn_readfirstlane(kp.scale);
+    const bool cform = kp.cform != 0;
+    const bool bigl = cform ? count_rows(std::true_type{}, c, delta, b0, scale)
+                            : count_rows(std::false_type{}, c, delta, b0, scale);
+    {
+      const bool wbig = ballot(bigl) != 0ull;
+      if (lane == 0) sm.big[wid] = wbig ? 1u : 0u;
+    }
+    __syncthreads();
+    bool anybig = false;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) anybig |= sm.big[w] != 0u;
+    return anybig ? 1 : 0;
+  };
+  int cs = count(sm.key);
+  if (cs == 1) {  // uniform: every wave has read the flags; zero the counters, recount
+    __syncthreads();
+    uint4* c4 = (uint4*)cnt;
+    for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    cs = count(bs_key_params<MINBASE, BYDOC>(smin, smax, nan, QF_BS_RETRY_SHIFT));
+  }
+  if (cs != 0) {  // uniform: a range the key cannot take, or a bucket still too big
+    if (tid == 0) perm_put(p, po, kJsUnsorted);
+    return;
+  }
+  // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
+  {
+    constexpr int kPer = NB / BLOCK;  // counters per thread
+    static_assert(kPer == 8, "two uint4 counter loads per thread");
+    const uint4 c0 = ((const uint4*)cnt)[tid * 2], c1 = ((const uint4*)cnt)[tid * 2 + 1];
+    uint32_t c[kPer] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    uint32_t tot = 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t x = c[i];
+      c[i] = tot;
+      tot += x;
+    }
+    const uint32_t incl = wave_incl_scan_dpp(tot);
+    if (lane == 63) sm.wtot[wid] = incl;
+    __syncthreads();  // also: every counter read before the scatter overwrites them
+    uint32_t pre = incl - tot;
+#pragma unroll
+    for (int w = 0; w < WAVES - 1; ++w) pre += w < wid ? sm.wtot[w] : 0u;
+    ((uint4*)bk)[tid] = make_uint4((pre + c[0]) | ((pre + c[1]) << 16),
+                                   (pre + c[2]) | ((pre + c[3]) << 16),
+                                   (pre + c[4]) | ((pre + c[5]) << 16),
+                                   (pre + c[6]) | ((pre + c[7]) << 16));
+    if (tid == 0) bk[NB] = (uint16_t)U;
+  }
+  __syncthreads();
+  // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
+  uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = ub0 + j * ustep + lane;
+    if (j < rows && u < U) {
+      const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
+      const uint32_t st = bk[b], nx = bk[b + 1];
+      const uint32_t pos = st + at;
+      skey[pos] = bs_rank_key(v[j]);  // the rank phase compares integer keys
+      if (BYDOC) sd[pos] = d[j];
+      pa[j] = pos;
+      pw[j] = ((uint32_t)u << 20) | ((nx - st) << 8) | at;
+    }
+  }
+  __syncthreads();  // the starts are dead: the u | size | arrival words over them
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = ub0 + j * ustep + lane;
+    if (j < rows && u < U) sw[pa[j]] = pw[j];
+  }
+  __syncthreads();
+  // ---- rank inside the bucket, in position order --------------------------------------
+  uint32_t P[ROWS], uo[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = pbase + j * 64 + lane;
+    P[j] = 0u;
+    uo[j] = 0u;
+    if (j < rows && i < U) {
+      const uint64_t ki = skey[i];
+      const uint32_t wi = sw[i];
+      // the tie-break key: the whole word, whose top bits are u — distinct, so the
+      // word order is the first-seen order — or, BYDOC, the docid
+      const uint32_t ti = BYDOC ? sd[i] : wi;
+      const uint32_t lo = (uint32_t)i - (wi & 0xFFu), hi = lo + ((wi >> 8) & 0xFFFu);
+      uint32_t before = 0u;
+      // the bucket's members by pointer (two per step; a bucket of one: nothing to
+      // count): no index arithmetic inside the loop
+      const uint32_t k0 = hi - lo > 1u ? lo : hi;
+      const uint64_t* pv = skey + k0;
+      const uint64_t* const pend = skey + hi;
+      const uint64_t* const plast = pend - 1;  // a pair remains while pv < plast
+      const uint32_t* tp = BYDOC ? sd + k0 : sw + k0;
+      for (; pv < plast; pv += 2, tp += 2) {
+        // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the
+        // compiler would merge them into (8 cycles: it serves 16 lanes at a time)
+        const uint64_t v0 = pv[0];
+        asm volatile("" ::: "memory");
+        const uint64_t v1 = pv[1];
+        const uint32_t t0 = tp[0], t1 = tp[1];
+        before = add_if_precedes(before, ki, ti, v0, t0);
+        before = add_if_precedes(before, ki, ti, v1, t1);
+      }
+      if (pv < pend) before = add_if_precedes(before, ki, ti, pv[0], tp[0]);
+      P[j] = lo + before;
+      uo[j] = wi >> 20;
+    }
+  }
+  // ---- outputs (every row's position before any store) ----------------------------------
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = pbase + j * 64 + lane;
+    if (j < rows && i < U) perm_put(p, po + P[j], uo[j]);
+  }
+}
+
+template <int BLOCK, int BITS, bool BYDOC>
+__global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams p) {
+  constexpr int WAVES = BLOCK / 64, ROWS = (kJsUMax + BLOCK - 1) / BLOCK;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[BsLds<BITS, BYDOC>::kBytes];
+  __shared__ BsShared<WAVES> sm;
   // wid is wave-uniform: readfirstlane puts it (and every row base derived from
   // it) in SGPRs, so the per-row address arithmetic is scalar
   const int tid = threadIdx.x, lane = tid & 63,
@@ -1484,260 +1771,110 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     v[j] = (j < rows && u < U) ? io[u] : 0.0;
     if (BYDOC) d[j] = (j < rows && u < U) ? p.union_docid[base + u] : 0u;
   }
-  {  // zero the counters (region A beyond the partials)
-    uint4* c4 = (uint4*)cnt;
-#pragma unroll
-    for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-  }
-  {  // score range (NaN flagged): every thread's partials, reduced by wave 0
-    double vmn = INFINITY, vmx = -INFINITY;
-    bool nan = false;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = wbase + j * 64 + lane;
-      if (j < rows && u < U) {
-        vmn = raw_min_f64(vmn, v[j]);
-        vmx = raw_max_f64(vmx, v[j]);
-        nan |= v[j] != v[j];
-      }
-    }
-    sval[tid] = vmn;
-    sval[BLOCK + tid] = vmx;
-    if (BYDOC) {  // docid range: partials in region B (free until the scatter)
-      uint32_t dmn = ~0u, dmx = 0u;
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        const int u = wbase + j * 64 + lane;
-        if (j < rows && u < U) {
-          dmn = min(dmn, d[j]);
-          dmx = max(dmx, d[j]);
-        }
-      }
-      sw[tid] = dmn;
-      sw[BLOCK + tid] = dmx;
-    }
-    const bool anynan = ballot(nan) != 0ull;
-    if (lane == 0) s_wnan[wid] = anynan ? 1 : 0;
-  }
-  __syncthreads();
-  if (wid == 0) {
-    __builtin_amdgcn_s_setprio(3);  // the block waits on this wave
-    double mn = sval[lane], mx = sval[BLOCK + lane];
-#pragma unroll
-    for (int i = 1; i < WAVES; ++i) {
-      mn = raw_min_f64(mn, sval[i * 64 + lane]);
-      mx = raw_max_f64(mx, sval[BLOCK + i * 64 + lane]);
-    }
-    mn = wave_min_f64_dpp(mn);
-    mx = wave_max_f64_dpp(mx);
-    uint32_t dmn = 0u, dmx = 0u;
-    if (BYDOC) {
-      const uint32_t* sp = sw;
-      dmn = sp[lane];
-      dmx = sp[BLOCK + lane];
-#pragma unroll
-      for (int i = 1; i < WAVES; ++i) {
-        dmn = min(dmn, sp[i * 64 + lane]);
-        dmx = max(dmx, sp[BLOCK + i * 64 + lane]);
-      }
-      dmn = (uint32_t)wave_min_u64_dpp(dmn);
-      dmx = (uint32_t)wave_max_u64_dpp(dmx);
-    }
-    int anyn = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) anyn |= s_wnan[w];
-    if (lane == 63) {
-      // the folded extremes (-0.0 == +0.0) and the first count's key constants,
-      // once here instead of in every wave after the barrier
-      const double fmx = f64_from_asc_key(f64_asc_key(mx)), fmn = f64_from_asc_key(f64_asc_key(mn));
-      s_mn = fmn;
-      s_mx = fmx;
-      s_nan = anyn;
-      s_dmn = dmn;
-      s_dmx = dmx;
-      s_key = bs_key_params<MINBASE, BYDOC>(fmn, fmx, anyn != 0, QF_BSORT_DELTA_SHIFT);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-  __syncthreads();
-  const bool nan = s_nan != 0;
-  if (!BYDOC && s_mn == s_mx && !nan) {  // every score equal: first-seen order
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = wbase + j * 64 + lane;
-      if (j < rows && u < U) perm_put(p, po + u, (uint32_t)u);
-    }
+  bsort_core<BLOCK, BITS, BYDOC>(p, lds, sm, v, d, U, wbase, 64, po);
+}
+
+// ============================================================================
+// join_learned_kernel — learned fusion alone (C5: QF_LEARNED is the call's one
+// method), join and sort in one workgroup per query.  The LDS join as join_kernel
+// (JoinM: N <= 5,120, micro-unit scores), then each thread's documents u = j *
+// 512 + tid take pandas' Kahan sums (src/fusion.py:436-446) — stored as
+// join_kernel stores them — and stay in registers with their docids (the group's
+// first entry's input docid), and the bucket sort by docid ties (bsort_core,
+// BYDOC) ranks them in the join's dead LDS.  The separate sort kernel re-read
+// every score from HBM and ran at 3 workgroups per CU for the docid array;
+// here the scores never leave the registers.  A union above kJsUMax (or a query
+// with a status) is left unsorted to fuse_large_kernel, as the join_kernel path
+// leaves it.
+// ============================================================================
+template <class C>
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(FuseParams p) {
+  constexpr int BLOCK = C::kBlock, ROWS = (kJsUMax + BLOCK - 1) / BLOCK;
+  static_assert(BLOCK == 512, "bsort_core is instantiated for 512 threads");
+  constexpr int kSortLds = BsLds<12, true>::kBytes;
+  __shared__ JoinShared<C, 1, kSortLds> sh;
+  __shared__ BsShared<BLOCK / 64> sm;
+  const int64_t q = block_id();
+  if (q >= p.n_queries) return;
+  const int N = join_groups<C, 1, kSortLds>(p, sh, q);
+  if (N < 0) return;
+  const int U = sh.U;
+  if (U > kJsUMax || sh.status) {  // uniform: the separate sort kernels' share
+    store_unsorted_sums<C, 1, kSortLds>(p, sh, N);
+    if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : U;
     return;
   }
-  const double smax = s_mx, smin = s_mn;
-  int ush = 0;  // U - 1 >> ush < MINSUB
-  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
-  const uint32_t dmin = BYDOC ? s_dmn : 0u;
-  int dsh = 0;  // BYDOC: (dmax - dmin) >> dsh < MINSUB
-  if (BYDOC)
-    while (((s_dmx - dmin) >> dsh) >= (uint32_t)MINSUB) ++dsh;
-  // the minimum's sub-bucket of row j: MINBASE + (wbase + 64 j + lane) >> ush, with
-  // 64-aligned row bases and ush <= 6 (U <= kJsUMax): a per-lane part + a row part
-  static_assert(((kJsUMax - 1) >> 6) < MINSUB, "ush <= 6");
-  const uint32_t lane_sub = (uint32_t)lane >> ush;
-  uint32_t ws[ROWS];  // bucket | arrival index << 16
-  // count with delta = range / 2^shift: -1 = a range the key cannot take (the
-  // pair is marked), else whether some bucket exceeds kJsBucketMax
-  // one row pass of the count: CF = the v + c form.  Every row's atomic is issued
-  // before any result is used (one wait); a lane past U adds to the spare counter
-  // cnt[NB] (in region B, free until the scatter), so no branch surrounds them
-  auto count_rows = [&](auto cf, double c, double delta, uint32_t b0, uint32_t scale) -> bool {
-    constexpr bool CF = decltype(cf)::value;
-    uint32_t old[ROWS];
+  using L = JoinLds<C, 1>;
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t base = sh.off[0];
+  const int32_t* gsc = (const int32_t*)(sh.smem + L::kGscOff);
+  const uint32_t* gpr = (const uint32_t*)(sh.smem + L::kGprOff);
+  const uint16_t* ugo = (const uint16_t*)(sh.smem + L::kGoOff);
+  double v[ROWS];
+  uint32_t d[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = j * BLOCK + tid;
+    v[j] = 0.0;
+    d[j] = 0u;
+    if (u < U) {
+      const int gs = ugo[u], ge = u + 1 < U ? (int)ugo[u + 1] : N;
+      const uint32_t g0 = gpr[gs];  // the first-seen entry: the document's docid
+      d[j] = p.docid[sh.off[g0 >> 16] + (g0 & 0xFFFFu)];
+      double a6 = 0.0, c6 = 0.0;
+      for (int k = gs; k < ge; ++k) {
+        const double s = ScoreIn<1>::val(gsc[k]);
+        const int r = (int)(gpr[k] >> 16);
+        learned_add(p, s, sh.w[r], r, a6, c6);  // src/fusion.py:436-446
+      }
+      v[j] = a6;
+      p.fused[base + u] = a6;  // the one method slot
+    }
+  }
+  if (tid == 0) p.union_count[q] = U;
+  __syncthreads();  // the groups are dead: their LDS is the sort's
+  bsort_core<BLOCK, 12, true>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK, base);
+}
+
+#ifdef QF_JOIN_SORT_ALL
+// (Development A/B) every method's sort in the join's workgroup: the sums stored
+// as join_kernel stores them, then per method slot the same thread reads back the
+// scores it stored (program order: no fence needed; L2-hot) and bsort_core ranks
+// them in the join's dead LDS — no second kernel re-reading the scores from HBM.
+template <class C>
+__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_sort_all_kernel(FuseParams p) {
+  constexpr int BLOCK = C::kBlock, ROWS = (kJsUMax + BLOCK - 1) / BLOCK;
+  static_assert(BLOCK == 512, "bsort_core is instantiated for 512 threads");
+  constexpr int kSortLds = BsLds<12, false>::kBytes;
+  __shared__ JoinShared<C, 1, kSortLds> sh;
+  __shared__ BsShared<BLOCK / 64> sm;
+  const int64_t q = block_id();
+  if (q >= p.n_queries) return;
+  const int N = join_groups<C, 1, kSortLds>(p, sh, q);
+  if (N < 0) return;
+  store_unsorted_sums<C, 1, kSortLds>(p, sh, N);
+  const int U = sh.U, st = sh.status;
+  if (threadIdx.x == 0) p.union_count[q] = st ? st : U;
+  if (st || U > kJsUMax) return;  // uniform: fuse_large_kernel's
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t base = sh.off[0];
+  const int M = __popc(p.methods);
+  __syncthreads();  // every wave is past the sums: the group LDS is free
+  for (int ms = 0; ms < M; ++ms) {
+    const double* io = p.fused + (int64_t)ms * p.out_stride + base;
+    double v[ROWS];
+    uint32_t d[1] = {0u};
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
-      if (j < rows) {  // uniform
-        const int u = wbase + j * 64 + lane;
-        const double x = CF ? v[j] + c : (v[j] - smin) + delta;
-        const uint32_t hx = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
-        const uint32_t minb = BYDOC ? (uint32_t)MINBASE + ((d[j] - dmin) >> dsh)
-                                    : (uint32_t)MINBASE + ((uint32_t)(wbase + 64 * j) >> ush) + lane_sub;
-        const uint32_t key = __umulhi(hx - b0, scale);  // < MINBASE, non-decreasing in x
-        uint32_t b = sel_if_eq_f64(v[j], smin, minb, (uint32_t)(MINBASE - 1) - key);
-        b = u < U ? b : (uint32_t)NB;
-        ws[j] = b;
-        old[j] = atomicAdd(&cnt[b], 1u);
-      }
+      const int u = j * BLOCK + tid;  // the u this thread's sums stored
+      v[j] = u < U ? io[u] : 0.0;
     }
-    bool bigl = false;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      if (j < rows) {
-        bigl |= (old[j] >= (uint32_t)kJsBucketMax) & (ws[j] < (uint32_t)NB);
-        ws[j] |= old[j] << 16;
-      }
-    }
-    return bigl;
-  };
-  // count with delta = range / 2^shift: -1 = a range the key cannot take (the
-  // pair is marked), else whether some bucket exceeds kJsBucketMax
-  auto count = [&](const BsKey& kp) -> int {
-    if (!kp.ok) return -1;  // uniform
-    const double c = rfl_f64(kp.c), delta = kp.delta;
-    const uint32_t b0 = __builtin_amdgcn_readfirstlane(kp.b0);
-    const uint32_t scale = __builtin_amdgcn_readfirstlane(kp.scale);
-    const bool cform = kp.cform != 0;
-    const bool bigl = cform ? count_rows(std::true_type{}, c, delta, b0, scale)
-                            : count_rows(std::false_type{}, c, delta, b0, scale);
-    {
-      const bool wbig = ballot(bigl) != 0ull;
-      if (lane == 0) s_big[wid] = wbig ? 1u : 0u;
-    }
-    __syncthreads();
-    bool anybig = false;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) anybig |= s_big[w] != 0u;
-    return anybig ? 1 : 0;
-  };
-  int cs = count(s_key);
-  if (cs == 1) {  // uniform: every wave has read the flags; zero the counters, recount
-    __syncthreads();
-    uint4* c4 = (uint4*)cnt;
-    for (int i = tid; i < NB / 4; i += BLOCK) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    cs = count(bs_key_params<MINBASE, BYDOC>(smin, smax, nan, QF_BS_RETRY_SHIFT));
-  }
-  if (cs != 0) {  // uniform: a range the key cannot take, or a bucket still too big
-    if (tid == 0) perm_put(p, po, kJsUnsorted);
-    return;
-  }
-  // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
-  {
-    constexpr int kPer = NB / BLOCK;  // counters per thread
-    static_assert(kPer == 8, "two uint4 counter loads per thread");
-    const uint4 c0 = ((const uint4*)cnt)[tid * 2], c1 = ((const uint4*)cnt)[tid * 2 + 1];
-    uint32_t c[kPer] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    uint32_t tot = 0u;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const uint32_t x = c[i];
-      c[i] = tot;
-      tot += x;
-    }
-    const uint32_t incl = wave_incl_scan_dpp(tot);
-    if (lane == 63) s_wtot[wid] = incl;
-    __syncthreads();  // also: every counter read before the scatter overwrites them
-    uint32_t pre = incl - tot;
-#pragma unroll
-    for (int w = 0; w < WAVES - 1; ++w) pre += w < wid ? s_wtot[w] : 0u;
-    ((uint4*)bk)[tid] = make_uint4((pre + c[0]) | ((pre + c[1]) << 16),
-                                   (pre + c[2]) | ((pre + c[3]) << 16),
-                                   (pre + c[4]) | ((pre + c[5]) << 16),
-                                   (pre + c[6]) | ((pre + c[7]) << 16));
-    if (tid == 0) bk[NB] = (uint16_t)U;
-  }
-  __syncthreads();
-  // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
-  uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int u = wbase + j * 64 + lane;
-    if (j < rows && u < U) {
-      const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
-      const uint32_t st = bk[b], nx = bk[b + 1];
-      const uint32_t pos = st + at;
-      skey[pos] = bs_rank_key(v[j]);  // the rank phase compares integer keys
-      if (BYDOC) sd[pos] = d[j];
-      pa[j] = pos;
-      pw[j] = ((uint32_t)u << 20) | ((nx - st) << 8) | at;
-    }
-  }
-  __syncthreads();  // the starts are dead: the u | size | arrival words over them
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int u = wbase + j * 64 + lane;
-    if (j < rows && u < U) sw[pa[j]] = pw[j];
-  }
-  __syncthreads();
-  // ---- rank inside the bucket, in position order --------------------------------------
-  uint32_t P[ROWS], uo[ROWS];
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int i = wbase + j * 64 + lane;
-    P[j] = 0u;
-    uo[j] = 0u;
-    if (j < rows && i < U) {
-      const uint64_t ki = skey[i];
-      const uint32_t wi = sw[i];
-      // the tie-break key: the whole word, whose top bits are u — distinct, so the
-      // word order is the first-seen order — or, BYDOC, the docid
-      const uint32_t ti = BYDOC ? sd[i] : wi;
-      const uint32_t lo = (uint32_t)i - (wi & 0xFFu), hi = lo + ((wi >> 8) & 0xFFFu);
-      uint32_t before = 0u;
-      // the bucket's members by pointer (two per step; a bucket of one: nothing to
-      // count): no index arithmetic inside the loop
-      const uint32_t k0 = hi - lo > 1u ? lo : hi;
-      const uint64_t* pv = skey + k0;
-      const uint64_t* const pend = skey + hi;
-      const uint64_t* const plast = pend - 1;  // a pair remains while pv < plast
-      const uint32_t* tp = BYDOC ? sd + k0 : sw + k0;
-      for (; pv < plast; pv += 2, tp += 2) {
-        // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the
-        // compiler would merge them into (8 cycles: it serves 16 lanes at a time)
-        const uint64_t v0 = pv[0];
-        asm volatile("" ::: "memory");
-        const uint64_t v1 = pv[1];
-        const uint32_t t0 = tp[0], t1 = tp[1];
-        before = add_if_precedes(before, ki, ti, v0, t0);
-        before = add_if_precedes(before, ki, ti, v1, t1);
-      }
-      if (pv < pend) before = add_if_precedes(before, ki, ti, pv[0], tp[0]);
-      P[j] = lo + before;
-      uo[j] = wi >> 20;
-    }
-  }
-  // ---- outputs (every row's position before any store) ----------------------------------
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int i = wbase + j * 64 + lane;
-    if (j < rows && i < U) perm_put(p, po + P[j], uo[j]);
+    bsort_core<BLOCK, 12, false>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK,
+                                 (int64_t)ms * p.out_stride + base);
+    __syncthreads();  // the LDS is the next slot's
   }
 }
+#endif
 
 // ============================================================================
 // join_sort_xl_kernel — queries beyond the LDS join (JoinXL::kNMax < N <= 65,535,
@@ -2625,14 +2762,30 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
   hipError_t e = hipSuccess;
   if (p.R <= kRMax && max_entries <= JoinXL::kNMax && max_entries > JoinS::kNMax) {
     // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
-    if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
-    else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
-    else launch_join<JoinXL>(p, kind, st);
+    const bool learned_only = p.methods == QF_LEARNED && kind == 1 &&
+                              max_entries <= JoinM::kNMax;
+    bool sorted_in_join = false;
+#ifdef QF_JOIN_SORT_ALL
+    sorted_in_join = !(p.methods & QF_LEARNED) && kind == 1 && max_entries <= JoinM::kNMax;
+#endif
+    if (learned_only) {  // join + sort in one kernel (C5)
+      hipLaunchKernelGGL((join_learned_kernel<JoinM>), grid_for(p.n_queries), dim3(512), 0, st,
+                         p);
+#ifdef QF_JOIN_SORT_ALL
+    } else if (sorted_in_join) {
+      hipLaunchKernelGGL((join_sort_all_kernel<JoinM>), grid_for(p.n_queries), dim3(512), 0, st,
+                         p);
+#endif
+    } else {
+      if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
+      else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
+      else launch_join<JoinXL>(p, kind, st);
+    }
     const int M = __builtin_popcount((unsigned)p.methods);
-    if (p.methods & ~QF_LEARNED)
+    if ((p.methods & ~QF_LEARNED) && !sorted_in_join)
       hipLaunchKernelGGL((bsort_kernel<512, 12, false>), grid_for((p.n_queries + 7) / 8 * 8 * M),
                          dim3(512), 0, st, p);
-    if (p.methods & QF_LEARNED)
+    if ((p.methods & QF_LEARNED) && !learned_only)
       hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),
                          dim3(512), 0, st, p);
     // unions above kJsUMax and the pairs the bucket sort marked: one pass

@@ -117,6 +117,31 @@ def test_learned_fusion_matches_reference_pandas(gpu, name, ties, tmp_path, caps
     assert p.read_text() == ref_port.runfile_text(want, "learned")
 
 
+@pytest.mark.parametrize("k,ties", [(1000, False), (1000, True), (700, True)])
+def test_learned_fusion_large_lists_join_and_sort_in_one_kernel(gpu, k, ties):
+    """5 runs x top-k (C5's shape: 1,025-5,120 entries per query, micro-unit
+    scores) take join_learned_kernel — the join, the Kahan sums and the docid-tie
+    bucket sort in one workgroup — bit for bit the reference's pandas calls."""
+    from qppfuse import fusion
+    rng = np.random.default_rng(k + ties)
+    model = _model("fusion_multioutput")
+    qids = [f"test{i}" for i in range(12)]
+    runs = _runs(rng, qids, ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade"], k, ties=ties)
+    qpp = {q: {r: [float(np.round(v, 6)) for v in rng.uniform(0, 1, 13)]
+               for r in model.retrievers} for q in qids}
+    got = fusion.learned_fusion(runs, qpp, str(GOLD / "nq_fusion_multioutput.json.gz"))
+    wd = lgbm_oracle.weights_dict(runs, qpp, model)
+    want = ref_port.learned_fusion_from_weights(runs, wd, len(model.retrievers))
+    assert list(got.keys()) == sorted(want.keys())
+    for q in want:
+        assert got[q] == want[q], q
+    for q in qids[:3]:  # and the ranked order write_runfile takes
+        ids, sc = got.arrays(q)
+        w = sorted(want[q], key=lambda x: x[1], reverse=True)
+        assert [s for _, s in w] == sc.tolist()
+        assert [d for d, _ in w] == got._docnos[ids].tolist()  # ties in docno order
+
+
 @pytest.mark.parametrize("dups", [False, True])
 def test_learned_fusion_18_runs_and_duplicates(gpu, dups):
     """18 runs (5 the model knows + 13 it does not: weight 1/n_retrievers,

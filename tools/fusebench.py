@@ -14,7 +14,7 @@ off, docid, raw = engine.synth_runs(0, Q, R, K)
 _, micro = engine.minmax_per_query(raw, off, want_norm=False)
 torch.manual_seed(7)
 w = torch.rand(Q * R, dtype=torch.float64, device=dev)
-M = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+M = os.environ.get("FUSEBENCH_METHODS", "combsum,combmnz,rrf,wcombsum,wcombmnz,wrrf").split(",")
 out = engine.alloc_fuse_out(Q, Q * R * K, engine.methods_mask(M), dev)
 for _ in range(5):
     engine.fuse(off, docid, micro, R, M, weights=w, max_entries=R * K, out=out)
