@@ -1546,6 +1546,15 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
+#if defined(QF_BS_STOP) && QF_BS_STOP == 1  // development: the phases before it only
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) acc += (uint32_t)__double2loint(v[j]);
+    if (acc == 12345u) perm_put(p, po, acc);
+    return;
+  }
+#endif
   const bool nan = sm.nan != 0;
   if (!BYDOC && sm.mn == sm.mx && !nan) {  // every score equal: first-seen order
 #pragma unroll
@@ -1632,6 +1641,16 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     if (tid == 0) perm_put(p, po, kJsUnsorted);
     return;
   }
+#if defined(QF_BS_STOP) && QF_BS_STOP == 2  // development: the phases before it only
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) acc += ws[j];
+    if (acc == 12345u) perm_put(p, po, acc);
+    return;
+  }
+#endif
+
   // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
   {
     constexpr int kPer = NB / BLOCK;  // counters per thread
@@ -1658,6 +1677,16 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     if (tid == 0) bk[NB] = (uint16_t)U;
   }
   __syncthreads();
+#if defined(QF_BS_STOP) && QF_BS_STOP == 3  // development: the phases before it only
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) acc += ws[j] + bk[j];
+    if (acc == 12345u) perm_put(p, po, acc);
+    return;
+  }
+#endif
+
   // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
   uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
 #pragma unroll
@@ -1680,6 +1709,16 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     if (j < rows && u < U) sw[pa[j]] = pw[j];
   }
   __syncthreads();
+#if defined(QF_BS_STOP) && QF_BS_STOP == 4  // development: the phases before it only
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) acc += pa[j] + sw[j];
+    if (acc == 12345u) perm_put(p, po, acc);
+    return;
+  }
+#endif
+
   // ---- rank inside the bucket, in position order --------------------------------------
   uint32_t P[ROWS], uo[ROWS];
 #pragma unroll
@@ -1717,6 +1756,15 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
       uo[j] = wi >> 20;
     }
   }
+#if defined(QF_BS_STOP) && QF_BS_STOP == 5  // development: the phases before it only
+  {
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) acc += P[j] + uo[j];
+    if (acc == 12345u) perm_put(p, po, acc);
+    return;
+  }
+#endif
   // ---- outputs (every row's position before any store) ----------------------------------
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {

@@ -26,4 +26,6 @@ FUSEBENCH_METHODS=learned REPS=3 bash tools/ab_kernels.sh tools/ab/lib_chain.so 
 cat $O/ab_c5.txt
 timeout -k 10 300 python -u bench.py --workload c5 --warmup 5 --steps 20 > $O/bench_c5.json 2> $O/bench_c5.err || { tail -30 $O/bench_c5.err; exit 1; }
 cat $O/bench_c5.json
+BSPH_OUT=$O/bsph bash tools/gpu_bs_phases.sh > $O/bs_phases.txt 2>&1 || { tail -20 $O/bs_phases.txt; exit 1; }
+cat $O/bs_phases.txt
 echo all-done
