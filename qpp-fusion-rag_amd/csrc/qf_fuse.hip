@@ -656,6 +656,9 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   uint32_t defer = 0u;  // lane 63: rows whose successor (lane 0 of the next wave) is checked below
   const bool ranx = p.methods & (QF_COMBSUM | QF_COMBMNZ | QF_RRF);
   int r = 0;  // entry e's list; e grows with j, so the search resumes where it stopped
+  // the end of list r (32-bit boundaries relative to the query's base), carried
+  // from row to row: a row reads a boundary only when it crosses one
+  int end = sh.offr[1];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const int e = j * BLOCK + tid;
@@ -666,7 +669,6 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     if (e < N) {
       const uint32_t d = dk[j];
       if (d == kEmpty) status = QF_QSTATUS_BADDOC;
-      int end = sh.offr[r + 1];  // 32-bit boundaries relative to the query's base
       while (e >= end) end = sh.offr[++r + 1];
       rj[j] = (uint32_t)r;
       uint32_t h = (d * 0x9E3779B1u) >> (32 - C::kTB);

@@ -20,7 +20,7 @@ SQPMC_OUT=$O/sqpmc bash tools/gpu_sqpmc.sh > $O/sqpmc.txt 2>&1 || { tail -30 $O/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --native-sample 0 --check 0 > $O/bench_trace.log 2>&1 || { tail -30 $O/bench_trace.log; exit 1; }
 REPS=3 bash tools/ab_kernels.sh tools/ab/lib_base.so tools/ab/lib_chain.so > $O/ab_chain.txt 2>&1 || { tail -20 $O/ab_chain.txt; exit 1; }
 cat $O/ab_chain.txt
-REPS=3 bash tools/ab_kernels.sh tools/ab/lib_cur.so tools/ab/lib_jsa.so > $O/ab_jsa.txt 2>&1 || { tail -20 $O/ab_jsa.txt; exit 1; }
+REPS=3 bash tools/ab_kernels.sh tools/ab/lib_cur.so tools/ab/lib_jsa.so tools/ab/lib_hoist.so > $O/ab_jsa.txt 2>&1 || { tail -20 $O/ab_jsa.txt; exit 1; }
 cat $O/ab_jsa.txt
 FUSEBENCH_METHODS=learned REPS=3 bash tools/ab_kernels.sh tools/ab/lib_chain.so tools/ab/lib_cur.so > $O/ab_c5.txt 2>&1 || { tail -20 $O/ab_c5.txt; exit 1; }
 cat $O/ab_c5.txt
