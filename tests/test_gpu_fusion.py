@@ -772,14 +772,18 @@ def test_caller_owned_workspace(gpu, share):
     assert full >= one > 0
     ws = torch.empty(full if share == "full" else one, dtype=torch.uint8, device=gpu)
     ref = engine.fuse(doff, ddoc, dsc, R, ALL, 60, weights=wd, max_entries=n_max)
+    rc = ref.union_count.cpu().numpy()
     for _ in range(2):
         out = engine.fuse(doff, ddoc, dsc, R, ALL, 60, weights=wd, max_entries=n_max,
                           workspace=ws)
         torch.cuda.synchronize()
         assert torch.equal(out.union_count, ref.union_count)
-        assert torch.equal(out.union_docid, ref.union_docid)
-        assert torch.equal(out.perm, ref.perm)
-        assert torch.equal(out.fused.view(torch.int64), ref.fused.view(torch.int64))
+        for q in range(len(sizes)):  # every query's slots (the rest is never written)
+            b, n = int(off[q * R]), int(rc[q])
+            assert torch.equal(out.union_docid[b:b + n], ref.union_docid[b:b + n])
+            assert torch.equal(out.perm[:, b:b + n], ref.perm[:, b:b + n])
+            assert torch.equal(out.fused[:, b:b + n].view(torch.int64),
+                               ref.fused[:, b:b + n].view(torch.int64))
     uc = out.union_count.cpu().numpy()
     perm = _perm_np(out)
     fz = out.ranked_fused().cpu().numpy()
