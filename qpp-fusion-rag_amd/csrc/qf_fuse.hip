@@ -1818,8 +1818,20 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {  // every row's load in flight before the first use
     const int u = wbase + j * 64 + lane;
+#if defined(QF_BS_CLAMPED_LOAD) || defined(QF_BS_NT_LOAD)
+    // (development A/B) every row loads, past U a clamped duplicate (bsort_core
+    // masks items past U itself): no exec-mask branch around the loads
+    const uint32_t uc = min((uint32_t)u, (uint32_t)(U - 1));
+#ifdef QF_BS_NT_LOAD
+    v[j] = __builtin_nontemporal_load(&io[uc]);
+#else
+    v[j] = io[uc];
+#endif
+    if (BYDOC) d[j] = p.union_docid[base + uc];
+#else
     v[j] = (j < rows && u < U) ? io[u] : 0.0;
     if (BYDOC) d[j] = (j < rows && u < U) ? p.union_docid[base + u] : 0u;
+#endif
   }
   bsort_core<BLOCK, BITS, BYDOC>(p, lds, sm, v, d, U, wbase, 64, po);
 }

@@ -18,11 +18,11 @@ timeout -k 10 300 python -u tools/e2e.py --qpp --repeat 2 > $O/e2e_qpp.json 2> $
 cat $O/e2e_qpp.json
 SQPMC_OUT=$O/sqpmc bash tools/gpu_sqpmc.sh > $O/sqpmc.txt 2>&1 || { tail -30 $O/sqpmc.txt; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-sample 0 --native-sample 0 --check 0 > $O/bench_trace.log 2>&1 || { tail -30 $O/bench_trace.log; exit 1; }
-REPS=3 bash tools/ab_kernels.sh tools/ab/lib_base.so tools/ab/lib_chain.so > $O/ab_chain.txt 2>&1 || { tail -20 $O/ab_chain.txt; exit 1; }
+REPS=2 bash tools/ab_kernels.sh tools/ab/lib_base.so tools/ab/lib_chain.so > $O/ab_chain.txt 2>&1 || { tail -20 $O/ab_chain.txt; exit 1; }
 cat $O/ab_chain.txt
-REPS=3 bash tools/ab_kernels.sh tools/ab/lib_cur.so tools/ab/lib_jsa.so tools/ab/lib_hoist.so > $O/ab_jsa.txt 2>&1 || { tail -20 $O/ab_jsa.txt; exit 1; }
+REPS=2 bash tools/ab_kernels.sh tools/ab/lib_cur.so tools/ab/lib_jsa.so tools/ab/lib_hoist.so tools/ab/lib_clamp.so tools/ab/lib_ntload.so > $O/ab_jsa.txt 2>&1 || { tail -20 $O/ab_jsa.txt; exit 1; }
 cat $O/ab_jsa.txt
-FUSEBENCH_METHODS=learned REPS=3 bash tools/ab_kernels.sh tools/ab/lib_chain.so tools/ab/lib_cur.so > $O/ab_c5.txt 2>&1 || { tail -20 $O/ab_c5.txt; exit 1; }
+FUSEBENCH_METHODS=learned REPS=2 bash tools/ab_kernels.sh tools/ab/lib_chain.so tools/ab/lib_cur.so > $O/ab_c5.txt 2>&1 || { tail -20 $O/ab_c5.txt; exit 1; }
 cat $O/ab_c5.txt
 timeout -k 10 300 python -u bench.py --workload c5 --warmup 5 --steps 20 > $O/bench_c5.json 2> $O/bench_c5.err || { tail -30 $O/bench_c5.err; exit 1; }
 cat $O/bench_c5.json
