@@ -1689,6 +1689,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
   }
 #endif
 
+  const bool nonneg = smin >= 0.0;  // block-uniform (smin folds -0.0 into +0.0)
   // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
   uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
 #pragma unroll
@@ -1698,7 +1699,9 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
       const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
       const uint32_t st = bk[b], nx = bk[b + 1];
       const uint32_t pos = st + at;
-      skey[pos] = bs_rank_key(v[j]);  // the rank phase compares integer keys
+      // the rank phase compares integer keys: for a pair without negative scores
+      // (every C2 fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
+      skey[pos] = nonneg ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);
       if (BYDOC) sd[pos] = d[j];
       pa[j] = pos;
       pw[j] = ((uint32_t)u << 20) | ((nx - st) << 8) | at;
@@ -1818,20 +1821,12 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {  // every row's load in flight before the first use
     const int u = wbase + j * 64 + lane;
-#if defined(QF_BS_CLAMPED_LOAD) || defined(QF_BS_NT_LOAD)
-    // (development A/B) every row loads, past U a clamped duplicate (bsort_core
-    // masks items past U itself): no exec-mask branch around the loads
+    // every row loads, past U a clamped duplicate (bsort_core masks the items past
+    // U itself: no exec-mask branch around the loads), non-temporal: the scores
+    // are read this once (round 4: 1.5-2 us of the sort)
     const uint32_t uc = min((uint32_t)u, (uint32_t)(U - 1));
-#ifdef QF_BS_NT_LOAD
     v[j] = __builtin_nontemporal_load(&io[uc]);
-#else
-    v[j] = io[uc];
-#endif
     if (BYDOC) d[j] = p.union_docid[base + uc];
-#else
-    v[j] = (j < rows && u < U) ? io[u] : 0.0;
-    if (BYDOC) d[j] = (j < rows && u < U) ? p.union_docid[base + u] : 0u;
-#endif
   }
   bsort_core<BLOCK, BITS, BYDOC>(p, lds, sm, v, d, U, wbase, 64, po);
 }
@@ -1897,46 +1892,6 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(F
   __syncthreads();  // the groups are dead: their LDS is the sort's
   bsort_core<BLOCK, 12, true>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK, base);
 }
-
-#ifdef QF_JOIN_SORT_ALL
-// (Development A/B) every method's sort in the join's workgroup: the sums stored
-// as join_kernel stores them, then per method slot the same thread reads back the
-// scores it stored (program order: no fence needed; L2-hot) and bsort_core ranks
-// them in the join's dead LDS — no second kernel re-reading the scores from HBM.
-template <class C>
-__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_sort_all_kernel(FuseParams p) {
-  constexpr int BLOCK = C::kBlock, ROWS = (kJsUMax + BLOCK - 1) / BLOCK;
-  static_assert(BLOCK == 512, "bsort_core is instantiated for 512 threads");
-  constexpr int kSortLds = BsLds<12, false>::kBytes;
-  __shared__ JoinShared<C, 1, kSortLds> sh;
-  __shared__ BsShared<BLOCK / 64> sm;
-  const int64_t q = block_id();
-  if (q >= p.n_queries) return;
-  const int N = join_groups<C, 1, kSortLds>(p, sh, q);
-  if (N < 0) return;
-  store_unsorted_sums<C, 1, kSortLds>(p, sh, N);
-  const int U = sh.U, st = sh.status;
-  if (threadIdx.x == 0) p.union_count[q] = st ? st : U;
-  if (st || U > kJsUMax) return;  // uniform: fuse_large_kernel's
-  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t base = sh.off[0];
-  const int M = __popc(p.methods);
-  __syncthreads();  // every wave is past the sums: the group LDS is free
-  for (int ms = 0; ms < M; ++ms) {
-    const double* io = p.fused + (int64_t)ms * p.out_stride + base;
-    double v[ROWS];
-    uint32_t d[1] = {0u};
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = j * BLOCK + tid;  // the u this thread's sums stored
-      v[j] = u < U ? io[u] : 0.0;
-    }
-    bsort_core<BLOCK, 12, false>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK,
-                                 (int64_t)ms * p.out_stride + base);
-    __syncthreads();  // the LDS is the next slot's
-  }
-}
-#endif
 
 // ============================================================================
 // join_sort_xl_kernel — queries beyond the LDS join (JoinXL::kNMax < N <= 65,535,
@@ -2826,25 +2781,21 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
     const bool learned_only = p.methods == QF_LEARNED && kind == 1 &&
                               max_entries <= JoinM::kNMax;
-    bool sorted_in_join = false;
-#ifdef QF_JOIN_SORT_ALL
-    sorted_in_join = !(p.methods & QF_LEARNED) && kind == 1 && max_entries <= JoinM::kNMax;
-#endif
+    // (Measured, not kept, round 4: every method's sort in the join's workgroup too —
+    // the sums stored, each slot read back L2-hot by the thread that stored it and
+    // ranked by bsort_core in the join's dead LDS: 349-352 us against join 126 +
+    // bsort 202-204 us; the six sorts in turn at 3 workgroups per CU lose more than
+    // the HBM re-read they save.)
     if (learned_only) {  // join + sort in one kernel (C5)
       hipLaunchKernelGGL((join_learned_kernel<JoinM>), grid_for(p.n_queries), dim3(512), 0, st,
                          p);
-#ifdef QF_JOIN_SORT_ALL
-    } else if (sorted_in_join) {
-      hipLaunchKernelGGL((join_sort_all_kernel<JoinM>), grid_for(p.n_queries), dim3(512), 0, st,
-                         p);
-#endif
     } else {
       if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
       else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
       else launch_join<JoinXL>(p, kind, st);
     }
     const int M = __builtin_popcount((unsigned)p.methods);
-    if ((p.methods & ~QF_LEARNED) && !sorted_in_join)
+    if (p.methods & ~QF_LEARNED)
       hipLaunchKernelGGL((bsort_kernel<512, 12, false>), grid_for((p.n_queries + 7) / 8 * 8 * M),
                          dim3(512), 0, st, p);
     if ((p.methods & QF_LEARNED) && !learned_only)

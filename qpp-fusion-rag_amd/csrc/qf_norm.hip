@@ -156,32 +156,23 @@ hipError_t synth_launch(int64_t q_begin, int64_t n_queries, int32_t R, int32_t K
 }
 
 // ---- the HBM copy ceiling (measurement support) ------------------------------------
-// A streaming copy, 16 bytes per lane per access, 4 accesses in flight per lane
-// (all loads issued before the first store), a grid-stride loop over enough
-// workgroups to fill every CU: the practical read + write rate of HBM that the
-// roofline's achieved bytes are compared with (the microarchitecture guide
-// measures 6.29 TB/s for a float4 copy).  Non-temporal: neither side is re-read.
+// A streaming copy, 16 bytes per lane per access, non-temporal, a grid-stride loop
+// over 4 workgroups of 256 threads per CU: the practical read + write rate of HBM
+// the roofline's achieved bytes are compared with.  tools/copy_probe.hip measured
+// the shapes on MI355X (1 GiB, r04): this one 6.15 TB/s; 2 or 4 per CU, or 4 or 8
+// accesses in flight per lane at grid strides, 4.3-5.7 TB/s; plain stores 5.7.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void stream_copy_kernel(u32x4* __restrict__ dst,
                                                           const u32x4* __restrict__ src,
                                                           int64_t n16) {
-  constexpr int kUnroll = 4;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < n16; i += kUnroll * stride) {
-    u32x4 v[kUnroll];
-#pragma unroll
-    for (int k = 0; k < kUnroll; ++k) v[k] = __builtin_nontemporal_load(&src[i + k * stride]);
-#pragma unroll
-    for (int k = 0; k < kUnroll; ++k) __builtin_nontemporal_store(v[k], &dst[i + k * stride]);
-  }
-  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
 }
 
 hipError_t stream_copy_launch(void* dst, const void* src, int64_t n16, hipStream_t st) {
-  // 8 workgroups of 256 threads per CU (256 CUs): 32 waves per CU resident
   const int64_t want = (n16 + 255) / 256;
-  const int blocks = (int)(want < 2048 ? (want > 0 ? want : 1) : 2048);
+  const int blocks = (int)(want < 1024 ? (want > 0 ? want : 1) : 1024);
   hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, st, (u32x4*)dst,
                      (const u32x4*)src, n16);
   return hipGetLastError();
