@@ -304,17 +304,22 @@ class Pipeline:
             minmax()
         else:
             e.qpp_raw(self.raw, self.off, self.R, a.qpp_top_k, self.nt, self.tf, out=self.qraw)
-            e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
-            work = None
-            if self.world > 1:  # the path's only exchange: ~1 KB over RCCL/xGMI,
-                from qppfuse.dist import allreduce_minmax  # hidden behind the min-max kernel
-                work = allreduce_minmax(self.mm, async_op=True)
-            minmax()
-            if work is not None:
-                work.wait()
             learned = "learned" in self.methods
-            o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
-                                want_micro=learned, want_weights=not learned)
+            if self.world > 1:
+                e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
+                # the path's only exchange: ~1 KB over RCCL/xGMI, hidden behind the
+                # min-max kernel
+                from qppfuse.dist import allreduce_minmax
+                work = allreduce_minmax(self.mm, async_op=True)
+                minmax()
+                work.wait()
+                o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
+                                    want_micro=learned, want_weights=not learned)
+            else:  # every query here: column extremes and normalisation in one launch
+                minmax()
+                o = e.qpp_minmax_normalize(self.qraw, self.off, self.R, a.qpp_index,
+                                           mm_out=self.mm, want_micro=learned,
+                                           want_weights=not learned)
             w = o["weights"]
             if learned:  # the .qpp values as features, GBDT, normalised weights
                 X = e.qpp_features(o["micro"], self.Q, self.R, self.block_runs, out=self.X)

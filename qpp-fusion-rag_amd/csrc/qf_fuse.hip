@@ -1598,7 +1598,11 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
         uint32_t b = sel_if_eq_f64(v[j], smin, minb, (uint32_t)(MINBASE - 1) - key);
         b = u < U ? b : (uint32_t)NB;
         ws[j] = b;
+#if defined(QF_BS_STOP) && defined(QF_BS_PROBE_CNT)  // development timing probe: conflict-free counters
+        old[j] = atomicAdd(&cnt[(uint32_t)(tid + j * BLOCK) & (uint32_t)(NB - 1)], 1u);
+#else
         old[j] = atomicAdd(&cnt[b], 1u);
+#endif
       }
     }
     bool bigl = false;
@@ -1698,7 +1702,11 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     if (j < rows && u < U) {
       const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
       const uint32_t st = bk[b], nx = bk[b + 1];
+#if defined(QF_BS_STOP) && defined(QF_BS_PROBE_SCAT)  // development timing probe: linear positions
+      const uint32_t pos = (uint32_t)u + 0u * (st + at);
+#else
       const uint32_t pos = st + at;
+#endif
       // the rank phase compares integer keys: for a pair without negative scores
       // (every C2 fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
       skey[pos] = nonneg ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);

@@ -18,8 +18,8 @@ for w in c1 c4 c5 c3; do
 done
 bash tools/profile.sh $O/prof > $O/profile.log 2>&1 || { tail -30 $O/profile.log; exit 1; }
 SQPMC_OUT=$O/sqpmc bash tools/gpu_sqpmc.sh > $O/sqpmc.txt 2>&1 || { tail -30 $O/sqpmc.txt; exit 1; }
-REPS=3 bash tools/ab_kernels.sh tools/ab/lib_ntload.so tools/ab/lib_new.so > $O/ab_nonneg.txt 2>&1 || { tail -20 $O/ab_nonneg.txt; exit 1; }
-cat $O/ab_nonneg.txt
+REPS=2 bash tools/ab_kernels.sh tools/ab/lib_stop2.so tools/ab/lib_stop2c.so tools/ab/lib_stop4.so tools/ab/lib_stop4s.so tools/ab/lib_stop4cs.so > $O/ab_conflict.txt 2>&1 || { tail -20 $O/ab_conflict.txt; exit 1; }
+cat $O/ab_conflict.txt
 timeout -k 10 300 python -u tools/e2e.py --repeat 3 > $O/e2e.json 2> $O/e2e.err || { tail -30 $O/e2e.err; exit 1; }
 cat $O/e2e.json
 echo all-done
