@@ -147,17 +147,6 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
                      double* w_out, void* stream);
 
 /*
- * qf_qpp_colminmax + qf_qpp_normalize(QF_NORM_MINMAX) in ONE launch, for a
- * device that holds every query of the batch (no shard all-reduce between the
- * two): the same mm (mm_out, nullable), norm_out, micro_out and w_out bits.
- * One workgroup per retriever.  Replaces src/qpp.py:347-372 + the .qpp round
- * trip of get_qpp_weight (src/fusion.py:116-158) when unsharded.
- */
-int qf_qpp_minmax_normalize(const double* raw, const int64_t* list_off, int64_t n_queries,
-                            int32_t n_retrievers, int32_t qpp_index, double* mm_out,
-                            double* norm_out, int64_t* micro_out, double* w_out, void* stream);
-
-/*
  * Learned fusion's feature matrix on device: X[q, j*13 + c] = the "%.6f" value
  * of normalised predictor c of run run_of_block[j] (micro_out of
  * qf_qpp_normalize, / 1e6 exactly as the .qpp text reads back), i.e. the

@@ -96,19 +96,6 @@ int qf_qpp_normalize(const double* raw, const double* mm, const int64_t* list_of
                "qf_qpp_normalize");
 }
 
-int qf_qpp_minmax_normalize(const double* raw, const int64_t* list_off, int64_t n_queries,
-                            int32_t n_retrievers, int32_t qpp_index, double* mm_out,
-                            double* norm_out, int64_t* micro_out, double* w_out, void* stream) {
-  if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off)
-    return fail(QF_EINVAL, "qf_qpp_minmax_normalize: bad arguments");
-  if (qpp_index < -1 || qpp_index >= QF_QPP_COLS)
-    return fail(QF_EINVAL, "qf_qpp_minmax_normalize: qpp_index %d out of range", qpp_index);
-  return check(qf::qpp_minmax_normalize_launch(raw, list_off, n_queries, n_retrievers, qpp_index,
-                                               mm_out, norm_out, micro_out, w_out,
-                                               (hipStream_t)stream),
-               "qf_qpp_minmax_normalize");
-}
-
 int qf_qpp_features(const int64_t* micro, int64_t n_queries, int32_t n_retrievers,
                     const int32_t* run_of_block, int32_t n_blocks, double* X, void* stream) {
   if (n_queries < 0 || n_retrievers <= 0 || n_blocks <= 0 || n_blocks > qf::kMaxFeatureBlocks ||

@@ -137,16 +137,20 @@ __device__ __forceinline__ uint64_t full_key(const SortCtx<ITEMS, WAVES>& sx, ui
 }
 
 // The lanes of the wave (active ones) whose kDigit-bit digit equals this lane's:
-// one ballot per digit bit, each lane keeping the lanes that agree with it.
+// one ballot per digit bit; a lane disagrees with the lanes set in ballot ^ t (t =
+// its own bit as 0 / all ones, one v_bfe_i32), whose union is accumulated — five
+// VALU per bit (bfe, compare, two xor, or) where the select form took nine.
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool active) {
-  uint64_t m = ballot(active);
+  uint32_t dl = 0u, dh = 0u;  // lanes whose digit differs from this lane's
 #pragma unroll
   for (int b = 0; b < kDigit; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t bb = ballot(bit);
-    m &= bit ? bb : ~bb;
+    uint32_t t = (uint32_t)__builtin_amdgcn_sbfe((int)d, (uint32_t)b, 1u);
+    asm("" : "+v"(t));  // compare t itself (not a shifted copy of d: one op more)
+    const uint64_t bb = ballot(t != 0u);
+    dl |= (uint32_t)bb ^ t;
+    dh |= (uint32_t)(bb >> 32) ^ t;
   }
-  return m;
+  return ballot(active) & ~(((uint64_t)dh << 32) | dl);
 }
 
 // One stable counting-scatter pass on a kDigit-bit digit of the items.  Within a
@@ -646,7 +650,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     uint32_t acc = 0u;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    if (acc == 12345u) p.union_count[q] = 0;
+    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
+    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
     return -1;
   }
 #endif
@@ -711,7 +716,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     uint32_t acc = 0u;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    if (acc == 12345u) p.union_count[q] = 0;
+    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
+    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
     return -1;
   }
 #endif
@@ -768,7 +774,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     uint32_t acc = 0u;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    if (acc == 12345u) p.union_count[q] = 0;
+    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
+    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
     return -1;
   }
 #endif
@@ -806,7 +813,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     uint32_t acc = 0u;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    if (acc == 12345u) p.union_count[q] = 0;
+    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
+    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
     return -1;
   }
 #endif
@@ -830,7 +838,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     uint32_t acc = 0u;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    if (acc == 12345u) p.union_count[q] = 0;
+    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
+    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
     return -1;
   }
 #endif

@@ -154,10 +154,6 @@ struct QppBlocks {
 };
 hipError_t qpp_features_launch(const int64_t* micro, int64_t Q, int32_t R, const QppBlocks& blk,
                                double* X, hipStream_t st);
-hipError_t qpp_minmax_normalize_launch(const double* raw, const int64_t* list_off, int64_t Q,
-                                       int32_t R, int32_t qpp_index, double* mm_out,
-                                       double* norm_out, int64_t* micro_out, double* w_out,
-                                       hipStream_t st);
 hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64_t* list_off,
                                 int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
                                 double* norm_out, int64_t* micro_out, double* w_out,

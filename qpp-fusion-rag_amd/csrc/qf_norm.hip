@@ -23,7 +23,11 @@ __global__ __launch_bounds__(256) void minmax_per_query_kernel(
 #pragma unroll
     for (int j = 0; j < kRegRows; ++j) {  // every load in flight before the first use
       const int64_t i = a + j * 64 + lane;
+#ifdef QF_MINMAX_NT  // development A/B: the raw scores read once, non-temporal
+      v[j] = i < b ? __builtin_nontemporal_load(&score[i]) : 0.0;
+#else
       v[j] = i < b ? score[i] : 0.0;
+#endif
     }
 #pragma unroll
     for (int j = 0; j < kRegRows; ++j)

@@ -545,17 +545,23 @@ __global__ __launch_bounds__(256) void qpp_colmeanstd_kernel(
 }
 
 // Normalise (src/qpp.py:356-372), round as "%.6f" (src/qpp.py:333), and derive
-// the fusion weight the .qpp text round trip gives (src/fusion.py:150-158): list
-// l's 13 raw values xs, with m0 / m1 = [min, -max] (minmax) or [mean, scale]
-// (zscore) of its retriever's columns.  Shared by qpp_normalize_kernel and the
-// one-launch qpp_minmax_normalize_kernel, so both round the same bits.
-__device__ __forceinline__ void normalize_list(int64_t l, bool present,
-                                               const double (&xs)[kQppCols],
-                                               const double (&m0)[kQppCols],
-                                               const double (&m1)[kQppCols], int32_t mode,
-                                               int32_t qpp_index, double* __restrict__ norm_out,
-                                               int64_t* __restrict__ micro_out,
-                                               double* __restrict__ w_out) {
+// the fusion weight the .qpp text round trip gives (src/fusion.py:150-158).
+__global__ __launch_bounds__(256) void qpp_normalize_kernel(
+    const double* __restrict__ raw, const double* __restrict__ mm,
+    const int64_t* __restrict__ list_off, int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
+    double* __restrict__ norm_out, int64_t* __restrict__ micro_out, double* __restrict__ w_out) {
+  const int64_t l = block_id() * blockDim.x + threadIdx.x;  // list index q*R + r
+  if (l >= Q * R) return;
+  const int r = (int)(l % R);
+  const bool present = list_off[l + 1] > list_off[l];
+  // every load in flight before the first use (one memory latency per thread)
+  double xs[kQppCols], m0[kQppCols], m1[kQppCols];
+#pragma unroll
+  for (int c = 0; c < kQppCols; ++c) {
+    xs[c] = raw[l * kQppCols + c];
+    m0[c] = mode != 0 ? mm[r * kQppCols + c] : 0.0;
+    m1[c] = mode != 0 ? mm[R * kQppCols + r * kQppCols + c] : 0.0;
+  }
   double wsum = 0.0, wsel = 0.0;
 #pragma unroll
   for (int c = 0; c < kQppCols; ++c) {
@@ -580,106 +586,6 @@ __device__ __forceinline__ void normalize_list(int64_t l, bool present,
     if (c == qpp_index) wsel = back;
   }
   if (w_out) w_out[l] = qpp_index < 0 ? wsum / (double)kQppCols : wsel;
-}
-
-__global__ __launch_bounds__(256) void qpp_normalize_kernel(
-    const double* __restrict__ raw, const double* __restrict__ mm,
-    const int64_t* __restrict__ list_off, int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
-    double* __restrict__ norm_out, int64_t* __restrict__ micro_out, double* __restrict__ w_out) {
-  const int64_t l = block_id() * blockDim.x + threadIdx.x;  // list index q*R + r
-  if (l >= Q * R) return;
-  const int r = (int)(l % R);
-  const bool present = list_off[l + 1] > list_off[l];
-  // every load in flight before the first use (one memory latency per thread)
-  double xs[kQppCols], m0[kQppCols], m1[kQppCols];
-#pragma unroll
-  for (int c = 0; c < kQppCols; ++c) {
-    xs[c] = raw[l * kQppCols + c];
-    m0[c] = mode != 0 ? mm[r * kQppCols + c] : 0.0;
-    m1[c] = mode != 0 ? mm[R * kQppCols + r * kQppCols + c] : 0.0;
-  }
-  normalize_list(l, present, xs, m0, m1, mode, qpp_index, norm_out, micro_out, w_out);
-}
-
-// The unsharded min-max normalisation in ONE launch (one device holds every query,
-// so no all-reduce sits between the column extremes and their use): one workgroup
-// per retriever reduces its 13 column minima / maxima over the present queries
-// (the values qpp_colminmax_kernel gives; min / max do not depend on the order)
-// and normalises its lists with them (normalize_list, as qpp_normalize_kernel).
-// Replaces two dependent launches of a few microseconds each on the step's path.
-constexpr int kMnBlock = 1024, kMnWaves = kMnBlock / 64, kMnRows = 4;
-__global__ __launch_bounds__(kMnBlock) void qpp_minmax_normalize_kernel(
-    const double* __restrict__ raw, const int64_t* __restrict__ list_off, int64_t Q, int32_t R,
-    int32_t qpp_index, double* __restrict__ mm_out, double* __restrict__ norm_out,
-    int64_t* __restrict__ micro_out, double* __restrict__ w_out) {
-  __shared__ double s_mn[kMnWaves][kQppCols], s_mx[kMnWaves][kQppCols];
-  __shared__ double s_m0[kQppCols], s_m1[kQppCols];
-  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  double vmin[kQppCols], vmax[kQppCols];
-#pragma unroll
-  for (int c = 0; c < kQppCols; ++c) {
-    vmin[c] = INFINITY;
-    vmax[c] = -INFINITY;
-  }
-  // kMnRows rows per thread per step, their 13 x kMnRows loads in flight together
-  for (int64_t q0 = tid; q0 < Q; q0 += (int64_t)kMnBlock * kMnRows) {
-    double v[kMnRows][kQppCols];
-    bool pr[kMnRows];
-#pragma unroll
-    for (int t = 0; t < kMnRows; ++t) {
-      const int64_t q = q0 + (int64_t)t * kMnBlock;
-      const int64_t l = (q < Q ? q : 0) * R + r;
-      pr[t] = q < Q && list_off[l + 1] > list_off[l];
-#pragma unroll
-      for (int c = 0; c < kQppCols; ++c) v[t][c] = raw[l * kQppCols + c];
-    }
-#pragma unroll
-    for (int t = 0; t < kMnRows; ++t)
-      if (pr[t]) {
-#pragma unroll
-        for (int c = 0; c < kQppCols; ++c) {
-          vmin[c] = fmin(vmin[c], v[t][c]);
-          vmax[c] = fmax(vmax[c], v[t][c]);
-        }
-      }
-  }
-#pragma unroll
-  for (int c = 0; c < kQppCols; ++c) {
-    const double a = wave_min(vmin[c]), b = wave_max(vmax[c]);
-    if (lane == 0) {
-      s_mn[wid][c] = a;
-      s_mx[wid][c] = b;
-    }
-  }
-  __syncthreads();
-  if (tid < kQppCols) {
-    double a = s_mn[0][tid], b = s_mx[0][tid];
-    for (int w = 1; w < kMnWaves; ++w) {
-      a = fmin(a, s_mn[w][tid]);
-      b = fmax(b, s_mx[w][tid]);
-    }
-    s_m0[tid] = a;
-    s_m1[tid] = -b;
-    if (mm_out) {  // the [min, -max] layout of qf_qpp_colminmax
-      mm_out[r * kQppCols + tid] = a;
-      mm_out[R * kQppCols + r * kQppCols + tid] = -b;
-    }
-  }
-  __syncthreads();
-  double m0[kQppCols], m1[kQppCols];
-#pragma unroll
-  for (int c = 0; c < kQppCols; ++c) {
-    m0[c] = s_m0[c];
-    m1[c] = s_m1[c];
-  }
-  for (int64_t q = tid; q < Q; q += kMnBlock) {  // the rows again (L2-hot)
-    const int64_t l = q * R + r;
-    const bool present = list_off[l + 1] > list_off[l];
-    double xs[kQppCols];
-#pragma unroll
-    for (int c = 0; c < kQppCols; ++c) xs[c] = raw[l * kQppCols + c];
-    normalize_list(l, present, xs, m0, m1, 1, qpp_index, norm_out, micro_out, w_out);
-  }
 }
 
 hipError_t qpp_raw_launch(const double* score, const int64_t* list_off, int64_t Q, int32_t R,
@@ -739,16 +645,6 @@ __global__ __launch_bounds__(256) void qpp_features_kernel(const int64_t* __rest
     v = (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m) : (double)m / 1e6;
   }
   X[i] = v;
-}
-
-hipError_t qpp_minmax_normalize_launch(const double* raw, const int64_t* list_off, int64_t Q,
-                                       int32_t R, int32_t qpp_index, double* mm_out,
-                                       double* norm_out, int64_t* micro_out, double* w_out,
-                                       hipStream_t st) {
-  if (Q * R == 0) return hipSuccess;
-  hipLaunchKernelGGL(qpp_minmax_normalize_kernel, dim3(R), dim3(kMnBlock), 0, st, raw, list_off,
-                     Q, R, qpp_index, mm_out, norm_out, micro_out, w_out);
-  return hipGetLastError();
 }
 
 hipError_t qpp_features_launch(const int64_t* micro, int64_t Q, int32_t R, const QppBlocks& blk,

@@ -44,7 +44,6 @@ SIGNATURES = {
     "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "qf_qpp_colmeanstd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
-    "qf_qpp_minmax_normalize": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "qf_qpp_features": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
                           _vp, _vp, _vp, _vp, _i64, _vp]),

@@ -278,26 +278,6 @@ def qpp_normalize(raw: torch.Tensor, mm: Optional[torch.Tensor], list_off: torch
     return {"norm": norm, "micro": micro, "weights": w}
 
 
-def qpp_minmax_normalize(raw: torch.Tensor, list_off: torch.Tensor, n_retrievers: int,
-                         qpp_index: int = 5, mm_out: Optional[torch.Tensor] = None,
-                         want_norm=False, want_micro=True, want_weights=True
-                         ) -> Dict[str, torch.Tensor]:
-    """qpp_colminmax + qpp_normalize(mode="minmax") in one launch, for a batch whose
-    every query is on this device (no shard all-reduce): the same values, one
-    dependent launch fewer.  mm_out (optional, [2*R*13]) receives the column
-    [min, -max] as qpp_colminmax writes them."""
-    require_device()
-    R = int(n_retrievers)
-    Q = (list_off.numel() - 1) // R
-    dev = raw.device
-    norm = torch.empty_like(raw) if want_norm else None
-    micro = torch.empty(raw.shape, dtype=torch.int64, device=dev) if want_micro else None
-    w = torch.empty(Q * R, dtype=torch.float64, device=dev) if want_weights else None
-    _lib.call("qf_qpp_minmax_normalize", _ptr(raw), _ptr(list_off), Q, R, int(qpp_index),
-              _ptr(mm_out), _ptr(norm), _ptr(micro), _ptr(w), _stream())
-    return {"norm": norm, "micro": micro, "weights": w}
-
-
 def qpp_features(micro: torch.Tensor, n_queries: int, n_retrievers: int, run_of_block,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """qf_qpp_features: learned fusion's X [Q, 13 * len(run_of_block)] float64 from the

@@ -261,12 +261,8 @@ def _normalize_array(arr: np.ndarray, method: str) -> np.ndarray:
     raw = torch.from_numpy(arr).to(dev)
     # every list present; the padded row pieces of one query are the "retrievers"
     off = torch.arange(n_q * rows_per + 1, dtype=torch.int64, device=dev)
-    if method == "minmax":  # every query on this device: extremes + normalisation, one launch
-        norm = engine.qpp_minmax_normalize(raw, off, rows_per, qpp_index=0, want_norm=True,
-                                           want_micro=False, want_weights=False)["norm"]
-    else:
-        stats = engine.qpp_colmeanstd(raw, off, rows_per)
-        norm = engine.qpp_normalize(raw, stats, off, rows_per, method, qpp_index=0,
-                                    want_norm=True, want_micro=False,
-                                    want_weights=False)["norm"]
+    stats = (engine.qpp_colminmax if method == "minmax" else engine.qpp_colmeanstd)(
+        raw, off, rows_per)
+    norm = engine.qpp_normalize(raw, stats, off, rows_per, method, qpp_index=0, want_norm=True,
+                                want_micro=False, want_weights=False)["norm"]
     return norm.cpu().numpy().reshape(n_q, width)[:, :n_cols]

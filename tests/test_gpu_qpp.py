@@ -115,37 +115,6 @@ def test_normalize_weights_and_rounding(gpu):
         assert (micro[7] == 0).all()
 
 
-@pytest.mark.parametrize("Q", [300, 11157])
-def test_minmax_normalize_one_launch_equals_two(gpu, Q):
-    """qf_qpp_minmax_normalize (one workgroup per retriever) == qf_qpp_colminmax +
-    qf_qpp_normalize bit for bit: mm, unrounded values, micro-units and weights —
-    with absent lists, a constant column, signed zeros and more queries than one
-    pass of the workgroup's rows (11,157 = C4)."""
-    from qppfuse import engine
-    rng = np.random.default_rng(Q)
-    R = 5
-    raw = rng.gamma(2, 3, (Q * R, 13))
-    raw[:, 3] = 0.25                                   # constant column: scale 1.0
-    raw[::7, 5] = -0.0
-    raw[1::7, 5] = 0.0
-    raw[::11, 9] = -rng.random(len(raw[::11, 9]))      # negatives
-    n = rng.integers(0, 3, Q * R)
-    n[[2, 9, 17]] = 0                                  # absent lists
-    off = np.zeros(Q * R + 1, np.int64)
-    off[1:] = np.cumsum(n)
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
-    graw, goff = t(raw), t(off)
-    for idx in (5, -1, 0, 12):
-        mm = engine.qpp_colminmax(graw, goff, R)
-        a = engine.qpp_normalize(graw, mm, goff, R, "minmax", idx, want_norm=True)
-        mm1 = torch.empty_like(mm)
-        b = engine.qpp_minmax_normalize(graw, goff, R, idx, mm_out=mm1, want_norm=True)
-        assert torch.equal(mm.view(torch.int64), mm1.view(torch.int64))
-        for k in ("norm", "weights"):
-            assert torch.equal(a[k].view(torch.int64), b[k].view(torch.int64)), (k, idx)
-        assert torch.equal(a["micro"], b["micro"]), idx
-
-
 def test_compute_qpp_for_res_file(gpu, tmp_path):
     from qppfuse.qpp import compute_qpp_for_res_file
     from qppfuse import textfeat

@@ -22,6 +22,17 @@ torch.cuda.synchronize()
 # a digest of the outputs (union sizes + every ranked list): equal across libraries
 # means the same results
 import hashlib
-h = hashlib.sha256(out.union_count.cpu().numpy().tobytes())
-h.update(out.ranked_fused().cpu().numpy().tobytes())
+# (raw buffers, no gather through perm: a development build that stops before the
+# sort's stores leaves perm uninitialised, and an index through it could fault)
+# (gathered on the host, over the slots each query owns: a development build that
+# stops before the sort's stores leaves perm uninitialised, and a device gather
+# through it could fault)
+uc = out.union_count.cpu().numpy()
+h = hashlib.sha256(uc.tobytes())
+perm, fused, lo = out.perm.cpu().numpy(), out.fused.cpu().numpy(), off.cpu().numpy()
+for q in range(Q):
+    b, u = int(lo[q * R]), int(uc[q])
+    if u > 0:
+        h.update(perm[:, b:b + u].tobytes())
+        h.update(fused[:, b:b + u].tobytes())
 print("ok", h.hexdigest()[:16])
