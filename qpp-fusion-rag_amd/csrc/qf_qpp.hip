@@ -114,6 +114,7 @@ constexpr int kQppBlock = 64 * kQppLists;
 constexpr int kChains = 6;   // cum, smv, wig, skew, snqc, uw
 constexpr int kRow = 65;     // padded LDS row (doubles)
 constexpr int kQppK = 50;    // k = min(50, n), QPPBridge.java:141
+constexpr int kPf = 4;       // the serial chains' LDS reads issued this many steps ahead
 
 __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
@@ -178,11 +179,17 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const int kl = s_k[lane];
     Kahan kp;
     kahan_init(kp);
+    // the row's values kPf steps ahead in a rotating buffer: each step's LDS read
+    // was issued right before its use and waited on, one latency per element
+    double pf[kPf];
+#pragma unroll
+    for (int t = 0; t < kPf; ++t) pf[t] = s_x[lane][t];
 #pragma unroll
     for (int j = 0; j < kQppK; ++j) {
-      const double v = s_x[lane][j];
+      const double v = pf[j % kPf];
+      if (j + kPf < kQppK) pf[j % kPf] = s_x[lane][j + kPf];
+      kahan_add_if(kp, v, j < kl);
       if (j < kl) {
-        kahan_add(kp, v);
         s_pf[lane][j] = kahan_final_sum(kp);
         s_ps[lane][j] = kp.simple;
       }
@@ -198,10 +205,14 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     if (kl >= 2 && nf >= 2) {
       Kahan kf;
       kahan_init(kf);
+      double pf[kPf];
+#pragma unroll
+      for (int t = 0; t < kPf; ++t) pf[t] = s_x[lane][t];
 #pragma unroll
       for (int j = 0; j < kQppK; ++j) {
-        const double v = s_x[lane][j];
-        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kf, v);
+        const double v = pf[j % kPf];
+        if (j + kPf < kQppK) pf[j % kPf] = s_x[lane][j + kPf];
+        kahan_add_if(kf, v, j < kl && ((fm >> j) & 1ull));
       }
       mf = kahan_final(kf) / (double)nf;
     }
@@ -224,11 +235,14 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   Kahan kv;
   kahan_init(kv);
   double sq = 0.0;
+  const int lim = k - 1 < lane ? k - 1 : lane;  // prefix i = lane: j = 0..i, j < k
 #pragma unroll
   for (int j = 0; j < kQppK; ++j) {
-    const double del = s_x[w][j] - mean_i;
+    // x_j from lane j's register (two v_readlane into SGPRs): the LDS broadcast it
+    // replaces was sunk into the predicated block and waited on every step
+    const double del = readlane_f64(x, j) - mean_i;
     const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
-    if (j < k && j <= lane) {
+    if (j <= lim) {
       sq += d2;
       kahan_add(kv, d2);
     }
@@ -282,10 +296,14 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       const double mf = s_mf[lane];
       Kahan kfv;
       kahan_init(kfv);
+      double pf[kPf];
+#pragma unroll
+      for (int t = 0; t < kPf; ++t) pf[t] = s_x[lane][t];
 #pragma unroll
       for (int j = 0; j < kQppK; ++j) {
-        const double dv = s_x[lane][j] - mf;
-        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
+        const double dv = pf[j % kPf] - mf;
+        if (j + kPf < kQppK) pf[j % kPf] = s_x[lane][j + kPf];
+        kahan_add_if(kfv, dv * dv, j < kl && ((fm >> j) & 1ull));
       }
       sigmax = sqrt(kahan_final(kfv) / (double)nf);
     }
@@ -296,11 +314,15 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const int kl = s_k[ll];
     const int len = c == 5 ? (kl < 20 ? kl : 20) : kl;
     const double* row = s_t[ll][c];
-    double acc = 0.0;
+    double acc = 0.0, pf[kPf];
+#pragma unroll
+    for (int t = 0; t < kPf; ++t) pf[t] = row[t];
 #pragma unroll
     for (int j = 0; j < kQppK; ++j) {
-      const double v = row[j];
-      if (j < len) acc += v;
+      const double v = pf[j % kPf];
+      if (j + kPf < kQppK) pf[j % kPf] = row[j + kPf];
+      const double a2 = acc + v;
+      acc = j < len ? a2 : acc;  // a select: the load is not sunk into a branch
     }
     s_res[ll][c] = acc;
   }
