@@ -43,64 +43,144 @@ namespace qf {
 // serial GBDT::PredictRaw sum from 0.0, tree by tree, bit for bit.  (Was: one
 // thread per (row, booster) walking its ~30 trees serially — C5: 17,260 threads,
 // ~270 waves on 256 CUs, each a chain of ~30 tree walks of dependent loads.)
-constexpr int kGbdtWaves = 4;
-constexpr int kGbdtMaxFeatures = 256;  // staged in LDS; more features: read from X
+// Round 4: the whole model is staged in LDS when it fits (the reference's NQ
+// model: 4,470 nodes + 4,619 leaves = 133 KB with the rows), one 16-wave
+// workgroup per CU, so a tree level costs two dependent LDS reads instead of a
+// dependent L1 / L2 load; a larger model walks the global arrays (same code).
+constexpr int kGbdtWaves = 16;
+constexpr int kGbdtMaxFeatures = 256;      // staged in LDS; more features: read from X
+constexpr int kGbdtLds = 148 * 1024;       // model + rows; 1 workgroup per CU
 
-__device__ __forceinline__ double gbdt_walk(const GbdtParams& p, const double* x, int t) {
+// A model's node arrays: the global SoA (feature, dtype apart) or its LDS image
+// (feature | dtype << 24 in one word).
+struct GbdtGlobal {
+  const GbdtParams& p;
+  __device__ int node_off(int t) const { return p.node_off[t]; }
+  __device__ int leaf_off(int t) const { return p.leaf_off[t]; }
+  __device__ int feature(int k) const { return p.feature[k]; }
+  __device__ int dtype(int k) const { return p.dtype[k]; }
+  __device__ double threshold(int k) const { return p.threshold[k]; }
+  __device__ int left(int k) const { return p.left[k]; }
+  __device__ int right(int k) const { return p.right[k]; }
+  __device__ double leaf(int i) const { return p.leaf_value[i]; }
+};
+struct GbdtLds {
+  const double *thr, *lv;
+  const uint32_t* fd;
+  const int32_t *lc, *rc, *no, *lo;
+  __device__ int node_off(int t) const { return no[t]; }
+  __device__ int leaf_off(int t) const { return lo[t]; }
+  __device__ int feature(int k) const { return (int)(fd[k] & 0xFFFFFFu); }
+  __device__ int dtype(int k) const { return (int)(fd[k] >> 24); }
+  __device__ double threshold(int k) const { return thr[k]; }
+  __device__ int left(int k) const { return lc[k]; }
+  __device__ int right(int k) const { return rc[k]; }
+  __device__ double leaf(int i) const { return lv[i]; }
+};
+
+template <class M>
+__device__ __forceinline__ double gbdt_walk(const M& m, const double* x, int t) {
   const double kZero = (double)1e-35f;  // LightGBM kZeroThreshold (a float)
-  const int nb = p.node_off[t], lb = p.leaf_off[t];
+  const int nb = m.node_off(t), lb = m.leaf_off(t);
   int leaf = 0;
-  if (p.leaf_off[t + 1] - lb > 1) {
+  if (m.leaf_off(t + 1) - lb > 1) {
     int node = 0;
     while (node >= 0) {
       const int k = nb + node;
-      double fv = x[p.feature[k]];
-      const int dt = p.dtype[k];
+      double fv = x[m.feature(k)];
+      const int dt = m.dtype(k);
       const int missing = (dt >> 2) & 3;  // 0 none, 1 zero, 2 NaN
       if (isnan(fv) && missing != 2) fv = 0.0;
       bool left;
       if ((missing == 1 && fv >= -kZero && fv <= kZero) || (missing == 2 && isnan(fv)))
         left = (dt & 2) != 0;  // default side
       else
-        left = fv <= p.threshold[k];
-      node = left ? p.left[k] : p.right[k];
+        left = fv <= m.threshold(k);
+      node = left ? m.left(k) : m.right(k);
     }
     leaf = ~node;
   }
-  return p.leaf_value[lb + leaf];
+  return m.leaf(lb + leaf);
+}
+
+// The rows of wave wid, strided over the grid: stage the row, walk, sum.
+template <class M>
+__device__ __forceinline__ void gbdt_rows(const GbdtParams& p, const M& m, double* sxw,
+                                          double* sl, int wid, int lane, int T, bool staged) {
+  const int b = lane < p.n_boosters ? lane : 0;
+  for (int64_t row = (int64_t)blockIdx.x * kGbdtWaves + wid; row < p.n_rows;
+       row += (int64_t)gridDim.x * kGbdtWaves) {
+    const double* xg = p.X + row * p.n_features;
+    if (staged) {
+      for (int i = lane; i < p.n_features; i += 64) sxw[i] = xg[i];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    const double* x = staged ? sxw : xg;
+    // lane b < n_boosters: booster b's trees [tb, te) and its running sum
+    const int tb = p.tree_off[b], te = p.tree_off[b + 1];
+    double s = 0.0;
+    for (int c0 = 0; c0 < T; c0 += 64) {
+      const int t = c0 + lane;
+      if (t < T) sl[lane] = gbdt_walk(m, x, t);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (lane < p.n_boosters) {
+        const int lo = tb > c0 ? tb : c0, hi = te < c0 + 64 ? te : c0 + 64;
+        for (int i = lo; i < hi; ++i) s += sl[i - c0];
+      }
+      __builtin_amdgcn_wave_barrier();  // every sum read before the next chunk's writes
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    if (lane < p.n_boosters) p.out[row * p.n_boosters + lane] = s;
+    __builtin_amdgcn_wave_barrier();  // the row's features read before the next row's
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
 }
 
 __global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParams p) {
-  __shared__ double sx[kGbdtWaves][kGbdtMaxFeatures];
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kGbdtLds];
   __shared__ double sleaf[kGbdtWaves][64];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t row = block_id() * kGbdtWaves + wid;
-  if (row >= p.n_rows) return;  // whole waves: no block barrier below
-  const double* xg = p.X + row * p.n_features;
-  const bool staged = p.n_features <= kGbdtMaxFeatures;
-  if (staged)
-    for (int i = lane; i < p.n_features; i += 64) sx[wid][i] = xg[i];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  const double* x = staged ? sx[wid] : xg;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int T = p.tree_off[p.n_boosters];
-  // lane b < n_boosters: booster b's trees [tb, te) and its running sum
-  const int b = lane < p.n_boosters ? lane : 0;
-  const int tb = p.tree_off[b], te = p.tree_off[b + 1];
-  double s = 0.0;
-  for (int c0 = 0; c0 < T; c0 += 64) {
-    const int t = c0 + lane;
-    if (t < T) sleaf[wid][lane] = gbdt_walk(p, x, t);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (lane < p.n_boosters) {
-      const int lo = tb > c0 ? tb : c0, hi = te < c0 + 64 ? te : c0 + 64;
-      for (int i = lo; i < hi; ++i) s += sleaf[wid][i - c0];
+  const int NN = p.node_off[T], NL = p.leaf_off[T], nf = p.n_features;
+  const bool staged = nf <= kGbdtMaxFeatures;
+  const int64_t xbytes = staged ? (int64_t)8 * kGbdtWaves * nf : 0;
+  // LDS image: rows f64 [kGbdtWaves][nf] | thresholds f64 [NN] | leaves f64 [NL] |
+  // feature|dtype u32 [NN] | left, right i32 [NN] | node_off, leaf_off i32 [T + 1]
+  const int64_t need = xbytes + 8 * (int64_t)NN + 8 * (int64_t)NL + 12 * (int64_t)NN +
+                       8 * (int64_t)(T + 1);
+  const bool fits = need <= kGbdtLds && nf <= (1 << 24);  // uniform; features fit 24 bits
+  double* sx = (double*)lds;
+  if (fits) {
+    double* thr = (double*)(lds + xbytes);
+    double* lv = thr + NN;
+    uint32_t* fd = (uint32_t*)(lv + NL);
+    int32_t* lc = (int32_t*)(fd + NN);
+    int32_t* rc = lc + NN;
+    int32_t* no = rc + NN;
+    int32_t* lo = no + (T + 1);
+#pragma unroll 4
+    for (int i = tid; i < NN; i += 64 * kGbdtWaves) {
+      thr[i] = p.threshold[i];
+      // the walk reads decision-type bits 1-3 only: its low byte is kept
+      fd[i] = (uint32_t)p.feature[i] | ((uint32_t)(p.dtype[i] & 0xFF) << 24);
+      lc[i] = p.left[i];
+      rc[i] = p.right[i];
     }
-    __builtin_amdgcn_wave_barrier();  // every sum read before the next chunk's writes
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll 4
+    for (int i = tid; i < NL; i += 64 * kGbdtWaves) lv[i] = p.leaf_value[i];
+    for (int i = tid; i <= T; i += 64 * kGbdtWaves) {
+      no[i] = p.node_off[i];
+      lo[i] = p.leaf_off[i];
+    }
+    __syncthreads();
+    const GbdtLds m{thr, lv, fd, lc, rc, no, lo};
+    gbdt_rows(p, m, sx + (int64_t)wid * nf, sleaf[wid], wid, lane, T, staged);
+  } else {
+    const GbdtGlobal m{p};
+    gbdt_rows(p, m, staged ? sx + (int64_t)wid * nf : nullptr, sleaf[wid], wid, lane, T, staged);
   }
-  if (lane < p.n_boosters) p.out[row * p.n_boosters + lane] = s;
 }
 
 // numpy's pairwise_sum for n < 128 (numpy/_core/src/umath/loops_utils.h.src)
@@ -217,8 +297,11 @@ hipError_t mlp_weights_launch(const MlpParams& p, hipStream_t st) {
 
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st) {
   if (p.n_rows * p.n_boosters == 0) return hipSuccess;
-  hipLaunchKernelGGL(gbdt_predict_kernel, grid_for((p.n_rows + kGbdtWaves - 1) / kGbdtWaves),
-                     dim3(64 * kGbdtWaves), 0, st, p);
+  // one workgroup per CU at most (its LDS image of the model), each wave striding
+  // over the rows
+  const int64_t want = (p.n_rows + kGbdtWaves - 1) / kGbdtWaves;
+  const unsigned grid = (unsigned)(want < 256 ? want : 256);
+  hipLaunchKernelGGL(gbdt_predict_kernel, dim3(grid), dim3(64 * kGbdtWaves), 0, st, p);
   return hipGetLastError();
 }
 

@@ -576,28 +576,6 @@ __global__ __launch_bounds__(256) void qpp_normalize_kernel(
   if (l >= Q * R) return;
   const int r = (int)(l % R);
   const bool present = list_off[l + 1] > list_off[l];
-  if (!norm_out && !micro_out && qpp_index >= 0) {
-    // the weights alone (the fusion step): only column qpp_index is read and
-    // rounded — the same operations as the loop below for that column
-    const int c = qpp_index;
-    const double x = raw[l * kQppCols + c];
-    const double a = mode != 0 ? mm[r * kQppCols + c] : 0.0;
-    const double b = mode != 0 ? mm[R * kQppCols + r * kQppCols + c] : 0.0;
-    double v = x;
-    if (mode == 1) {
-      const double vmin = a, vmax = -b;
-      const double scale = vmax > vmin ? vmax - vmin : 1.0;
-      v = scale > 0.0 ? (x - vmin) / scale : 0.0;
-    } else if (mode == 2) {
-      v = (x - a) / b;
-    }
-    if (!present) v = 0.0;
-    const long long m = round6(v);
-    if (w_out)
-      w_out[l] = (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m)
-                                                         : (double)m / 1e6;
-    return;
-  }
   // every load in flight before the first use (one memory latency per thread)
   double xs[kQppCols], m0[kQppCols], m1[kQppCols];
 #pragma unroll

@@ -61,6 +61,29 @@ def test_gbdt_missing_types_and_single_leaf_trees(gpu):
     assert got.tobytes() == want.tobytes()
 
 
+def test_gbdt_model_beyond_lds_walks_global_arrays(gpu):
+    """A model too large for the kernel's LDS image (the NQ boosters' trees
+    repeated 8 times: ~36 k nodes) takes the global-array walk — bit-exact too;
+    and a row count that strides every wave over several rows."""
+    import dataclasses
+    from qppfuse import engine, lgbm
+    m = _model("fusion_multioutput")
+    big = [dataclasses.replace(b, trees=b.used_trees * 8, best_iteration=0) for b in m.boosters]
+    mb = dataclasses.replace(m, boosters=big)
+    p = lgbm.pack_model(mb)
+    assert len(p.threshold) * 20 > 148 * 1024
+    rng = np.random.default_rng(11)
+    X = _X(rng, 97, p.n_features)
+    got = engine.gbdt_predict(torch.from_numpy(X).to(gpu), p).cpu().numpy()
+    want = np.column_stack([lgbm_oracle.booster_predict(b, X) for b in big])
+    assert got.tobytes() == want.tobytes()
+    small = lgbm.pack_model(m)
+    X2 = _X(rng, 4200, small.n_features)  # > 256 workgroups x 16 waves: rows strided
+    got2 = engine.gbdt_predict(torch.from_numpy(X2).to(gpu), small).cpu().numpy()
+    want2 = np.column_stack([lgbm_oracle.booster_predict(b, X2) for b in m.boosters])
+    assert got2.tobytes() == want2.tobytes()
+
+
 def test_learned_weights_match_numpy(gpu):
     from qppfuse import engine
     rng = np.random.default_rng(3)

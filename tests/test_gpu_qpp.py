@@ -115,31 +115,6 @@ def test_normalize_weights_and_rounding(gpu):
         assert (micro[7] == 0).all()
 
 
-def test_weights_only_normalize_equals_full(gpu):
-    """qf_qpp_normalize without norm / micro outputs and qpp_index >= 0 takes the
-    one-column path (the fusion step's weights): the same bits as the full
-    13-column call, min-max and zscore, absent lists and a constant column."""
-    from qppfuse import engine
-    rng = np.random.default_rng(8)
-    Q, R = 700, 5
-    raw = rng.gamma(2, 3, (Q * R, 13))
-    raw[:, 4] = 1.5
-    n = rng.integers(0, 4, Q * R)
-    n[[0, 11, 12]] = 0
-    off = np.zeros(Q * R + 1, np.int64)
-    off[1:] = np.cumsum(n)
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
-    graw, goff = t(raw), t(off)
-    for mode, stats in (("minmax", engine.qpp_colminmax(graw, goff, R)),
-                        ("zscore", engine.qpp_colmeanstd(graw, goff, R))):
-        for idx in (0, 4, 5, 12):
-            full = engine.qpp_normalize(graw, stats, goff, R, mode, idx, want_micro=True)
-            only = engine.qpp_normalize(graw, stats, goff, R, mode, idx, want_micro=False)
-            assert only["micro"] is None
-            assert torch.equal(full["weights"].view(torch.int64),
-                               only["weights"].view(torch.int64)), (mode, idx)
-
-
 def test_compute_qpp_for_res_file(gpu, tmp_path):
     from qppfuse.qpp import compute_qpp_for_res_file
     from qppfuse import textfeat
