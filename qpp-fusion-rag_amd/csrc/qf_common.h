@@ -166,19 +166,6 @@ __host__ __device__ __forceinline__ void kahan_add(Kahan& k, double v) {
   k.s = velvel;
   k.simple += v;
 }
-// kahan_add when p, else nothing — as selects, not a branch: a load feeding it
-// (the serial chains' LDS reads) is then not sunk into a predicated block and
-// waited on at every step.  The same operations as kahan_add when p holds.
-__host__ __device__ __forceinline__ void kahan_add_if(Kahan& k, double v, bool p) {
-  const double tmp = v - k.c;
-  const double sum = k.s;
-  const double velvel = sum + tmp;
-  const double nc = (velvel - sum) - tmp;
-  const double ns = k.simple + v;
-  k.c = p ? nc : k.c;
-  k.s = p ? velvel : k.s;
-  k.simple = p ? ns : k.simple;
-}
 // computeFinalSum in two halves, so that a serial chain can keep the first and
 // leave the second to lane-parallel code: the compensated sum, then the
 // fall-back to the simple sum when it is NaN and the simple sum infinite.

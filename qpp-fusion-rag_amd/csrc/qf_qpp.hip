@@ -114,7 +114,6 @@ constexpr int kQppBlock = 64 * kQppLists;
 constexpr int kChains = 6;   // cum, smv, wig, skew, snqc, uw
 constexpr int kRow = 65;     // padded LDS row (doubles)
 constexpr int kQppK = 50;    // k = min(50, n), QPPBridge.java:141
-constexpr int kPf = 4;       // the serial chains' LDS reads issued this many steps ahead
 
 __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
@@ -164,9 +163,13 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   QPP_STAMP(1);
 
   // ---- B (lane = list): the serial chains that need only rsv, on two waves at once.
-  // The serial loops run to kQppK unrolled, their LDS loads issued unconditionally
-  // (rows are kRow long; values past k unused) and only the arithmetic predicated,
-  // so a chain does not wait one LDS latency per element; every sum keeps its order.
+  // The serial loops run to kQppK unrolled (rows are kRow long; values past k
+  // unused), only the arithmetic predicated; every sum keeps its order.  (The
+  // compiler sinks each LDS read into its predicated step.  Round 4 measured the
+  // chains branch-free with their reads issued four steps ahead, and phase C's x_j
+  // by readlane instead of an LDS broadcast: bit-identical, 65.1 vs 65.2 us for
+  // C2 — the kernel is bound by its VALU issue, not by these latencies — and 12 %
+  // more VALU instructions; not kept.)
   // The chains are the workgroup's critical path (its other six waves wait at the
   // barrier) while the CU's other workgroups keep the SIMD busy: the chain waves run
   // at raised issue priority (s_setprio), so each dependent step issues as soon as
@@ -179,17 +182,11 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const int kl = s_k[lane];
     Kahan kp;
     kahan_init(kp);
-    // the row's values kPf steps ahead in a rotating buffer: each step's LDS read
-    // was issued right before its use and waited on, one latency per element
-    double pf[kPf];
-#pragma unroll
-    for (int t = 0; t < kPf; ++t) pf[t] = s_x[lane][t];
 #pragma unroll
     for (int j = 0; j < kQppK; ++j) {
-      const double v = pf[j % kPf];
-      if (j + kPf < kQppK) pf[j % kPf] = s_x[lane][j + kPf];
-      kahan_add_if(kp, v, j < kl);
+      const double v = s_x[lane][j];
       if (j < kl) {
+        kahan_add(kp, v);
         s_pf[lane][j] = kahan_final_sum(kp);
         s_ps[lane][j] = kp.simple;
       }
@@ -205,14 +202,10 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     if (kl >= 2 && nf >= 2) {
       Kahan kf;
       kahan_init(kf);
-      double pf[kPf];
-#pragma unroll
-      for (int t = 0; t < kPf; ++t) pf[t] = s_x[lane][t];
 #pragma unroll
       for (int j = 0; j < kQppK; ++j) {
-        const double v = pf[j % kPf];
-        if (j + kPf < kQppK) pf[j % kPf] = s_x[lane][j + kPf];
-        kahan_add_if(kf, v, j < kl && ((fm >> j) & 1ull));
+        const double v = s_x[lane][j];
+        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kf, v);
       }
       mf = kahan_final(kf) / (double)nf;
     }
@@ -235,14 +228,11 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   Kahan kv;
   kahan_init(kv);
   double sq = 0.0;
-  const int lim = k - 1 < lane ? k - 1 : lane;  // prefix i = lane: j = 0..i, j < k
 #pragma unroll
   for (int j = 0; j < kQppK; ++j) {
-    // x_j from lane j's register (two v_readlane into SGPRs): the LDS broadcast it
-    // replaces was sunk into the predicated block and waited on every step
-    const double del = readlane_f64(x, j) - mean_i;
+    const double del = s_x[w][j] - mean_i;
     const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
-    if (j <= lim) {
+    if (j < k && j <= lane) {
       sq += d2;
       kahan_add(kv, d2);
     }
@@ -296,14 +286,10 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       const double mf = s_mf[lane];
       Kahan kfv;
       kahan_init(kfv);
-      double pf[kPf];
-#pragma unroll
-      for (int t = 0; t < kPf; ++t) pf[t] = s_x[lane][t];
 #pragma unroll
       for (int j = 0; j < kQppK; ++j) {
-        const double dv = pf[j % kPf] - mf;
-        if (j + kPf < kQppK) pf[j % kPf] = s_x[lane][j + kPf];
-        kahan_add_if(kfv, dv * dv, j < kl && ((fm >> j) & 1ull));
+        const double dv = s_x[lane][j] - mf;
+        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
       }
       sigmax = sqrt(kahan_final(kfv) / (double)nf);
     }
@@ -314,15 +300,11 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const int kl = s_k[ll];
     const int len = c == 5 ? (kl < 20 ? kl : 20) : kl;
     const double* row = s_t[ll][c];
-    double acc = 0.0, pf[kPf];
-#pragma unroll
-    for (int t = 0; t < kPf; ++t) pf[t] = row[t];
+    double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < kQppK; ++j) {
-      const double v = pf[j % kPf];
-      if (j + kPf < kQppK) pf[j % kPf] = row[j + kPf];
-      const double a2 = acc + v;
-      acc = j < len ? a2 : acc;  // a select: the load is not sunk into a branch
+      const double v = row[j];
+      if (j < len) acc += v;
     }
     s_res[ll][c] = acc;
   }
