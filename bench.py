@@ -262,8 +262,8 @@ class Pipeline:
                                 want_micro=learned, want_weights=not learned)
             w = o["weights"]
             if learned:
-                X = e.qpp_features(o["micro"], n, R, self.block_runs)
-                w = e.learned_weights(e.gbdt_predict(X, self.packed), self.run_to_booster)
+                w = e.learned_gbdt_weights(o["micro"], n, R, self.block_runs, self.packed,
+                                           self.run_to_booster)
         out = e.fuse(off, docid, micro, R, self.methods, 60, weights=w, max_entries=R * K)
         return e.fused_topk(out, off, R, a.gather_topk)
 
@@ -316,9 +316,9 @@ class Pipeline:
             o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
                                 want_micro=learned, want_weights=not learned)
             w = o["weights"]
-            if learned:  # the .qpp values as features, GBDT, normalised weights
-                X = e.qpp_features(o["micro"], self.Q, self.R, self.block_runs, out=self.X)
-                w = e.learned_weights(e.gbdt_predict(X, self.packed), self.run_to_booster)
+            if learned:  # the .qpp values as features, GBDT, normalised weights: one launch
+                w = e.learned_gbdt_weights(o["micro"], self.Q, self.R, self.block_runs,
+                                           self.packed, self.run_to_booster)
         if timed:
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0.record()

@@ -304,6 +304,24 @@ int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters
                        void* stream);
 
 /*
+ * qf_qpp_features + qf_gbdt_predict + qf_learned_weights in ONE launch (the step
+ * src/fusion.py:415-440 takes from the .qpp values to the run weights): row q's
+ * features are read from the QPP micro-units as qf_qpp_features lays them out
+ * (run_of_block: HOST array, n_blocks <= 19 so the 13 * n_blocks features fit the
+ * kernel's LDS row), the model walked as qf_gbdt_predict does, and w_out filled as
+ * qf_learned_weights does — the same bits as the three calls.  pred_out
+ * (nullable) receives the raw predictions [n_queries][n_boosters].
+ */
+int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, int32_t n_retrievers,
+                            const int32_t* run_of_block, int32_t n_blocks, int32_t n_boosters,
+                            const int32_t* tree_off, const int32_t* node_off,
+                            const int32_t* leaf_off, const int32_t* feature,
+                            const double* threshold, const int32_t* decision_type,
+                            const int32_t* left, const int32_t* right, const double* leaf_value,
+                            int32_t n_runs, const int32_t* run_to_booster, double* pred_out,
+                            double* w_out, void* stream);
+
+/*
  * FusionMLP learned fusion (src/models/mlp_model.py:254-274 predict, called by
  * src/fusion.py:429 -> replaces `pred_weights = model.predict(X)` for the MLP model
  * and the weights' lookup at :440).  Model input i is X[q*x_cols + in_col[i]]

@@ -350,6 +350,51 @@ int qf_gbdt_predict(int64_t n_rows, const double* X, int32_t n_features, int32_t
   return check(qf::gbdt_predict_launch(p, (hipStream_t)stream), "qf_gbdt_predict");
 }
 
+int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, int32_t n_retrievers,
+                            const int32_t* run_of_block, int32_t n_blocks, int32_t n_boosters,
+                            const int32_t* tree_off, const int32_t* node_off,
+                            const int32_t* leaf_off, const int32_t* feature,
+                            const double* threshold, const int32_t* decision_type,
+                            const int32_t* left, const int32_t* right, const double* leaf_value,
+                            int32_t n_runs, const int32_t* run_to_booster, double* pred_out,
+                            double* w_out, void* stream) {
+  constexpr int kMaxBlocks = 256 / QF_QPP_COLS;  // the row's features staged in LDS
+  if (n_queries < 0 || n_retrievers <= 0 || n_blocks <= 0 || n_blocks > kMaxBlocks ||
+      n_boosters <= 0 || n_boosters > qf::kMaxBoosters || n_runs <= 0 ||
+      n_runs > qf::kMaxLearnedRuns || !run_of_block || !run_to_booster)
+    return fail(QF_EINVAL,
+                "qf_learned_gbdt_weights: bad sizes (n_blocks in [1, %d], n_boosters in [1, %d], "
+                "n_runs in [1, %d])",
+                kMaxBlocks, qf::kMaxBoosters, qf::kMaxLearnedRuns);
+  qf::GbdtFusedParams f{};
+  f.blk.n = n_blocks;
+  for (int j = 0; j < n_blocks; ++j) {
+    if (run_of_block[j] < -1 || run_of_block[j] >= n_retrievers)
+      return fail(QF_EINVAL, "qf_learned_gbdt_weights: run_of_block[%d] = %d out of range", j,
+                  run_of_block[j]);
+    f.blk.run[j] = run_of_block[j];
+  }
+  for (int r = 0; r < n_runs; ++r) {
+    if (run_to_booster[r] < -1 || run_to_booster[r] >= n_boosters)
+      return fail(QF_EINVAL, "qf_learned_gbdt_weights: run_to_booster[%d] out of range", r);
+    f.lw.run_to_booster[r] = run_to_booster[r];
+  }
+  if (n_queries == 0) return QF_OK;
+  if (!micro || !tree_off || !node_off || !leaf_off || !feature || !threshold ||
+      !decision_type || !left || !right || !leaf_value || !w_out)
+    return fail(QF_EINVAL, "qf_learned_gbdt_weights: null buffer");
+  f.gbdt = qf::GbdtParams{n_queries, nullptr, n_blocks * QF_QPP_COLS, n_boosters, tree_off,
+                          node_off, leaf_off, feature, threshold, decision_type, left, right,
+                          leaf_value, pred_out};
+  f.micro = micro;
+  f.R = n_retrievers;
+  f.lw.n_queries = n_queries;
+  f.lw.n_boosters = n_boosters;
+  f.lw.n_runs = n_runs;
+  f.lw.w_out = w_out;
+  return check(qf::learned_gbdt_weights_launch(f, (hipStream_t)stream), "qf_learned_gbdt_weights");
+}
+
 int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters,
                        int32_t n_runs, const int32_t* run_to_booster, double* w_out,
                        void* stream) {

@@ -101,7 +101,24 @@ struct LearnedWeightParams {
   int32_t run_to_booster[kMaxLearnedRuns];
   double* w_out;
 };
+constexpr int kMaxFeatureBlocks = 32;  // model retrievers of a learned-fusion feature matrix
+struct QppBlocks {
+  int32_t n;
+  int32_t run[kMaxFeatureBlocks];
+};
+// qf_learned_gbdt_weights: the feature matrix read from the QPP micro-units as
+// qpp_features_kernel builds it, the GBDT walk, and the weights as
+// learned_weights_kernel computes them, in one launch (gbdt.X unused; gbdt.out
+// nullable: the raw predictions, if wanted).
+struct GbdtFusedParams {
+  GbdtParams gbdt;
+  const int64_t* micro;  // [n_rows * R][13] QPP micro-units (qf_qpp_normalize)
+  int32_t R;
+  QppBlocks blk;
+  LearnedWeightParams lw;  // lw.pred unused; lw.w_out [n_rows][n_runs]
+};
 hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st);
+hipError_t learned_gbdt_weights_launch(const GbdtFusedParams& p, hipStream_t st);
 hipError_t learned_weights_launch(const LearnedWeightParams& p, hipStream_t st);
 
 // FusionMLP inference + weights (qf_mlp_weights): Linear layers (ReLU between,
@@ -147,11 +164,6 @@ hipError_t qpp_colminmax_launch(const double* raw, const int64_t* list_off, int6
                                 double* mm, hipStream_t st);
 hipError_t qpp_colmeanstd_launch(const double* raw, const int64_t* list_off, int64_t Q,
                                  int32_t R, double* st, hipStream_t stm);
-constexpr int kMaxFeatureBlocks = 32;  // model retrievers of a learned-fusion feature matrix
-struct QppBlocks {
-  int32_t n;
-  int32_t run[kMaxFeatureBlocks];
-};
 hipError_t qpp_features_launch(const int64_t* micro, int64_t Q, int32_t R, const QppBlocks& blk,
                                double* X, hipStream_t st);
 hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64_t* list_off,

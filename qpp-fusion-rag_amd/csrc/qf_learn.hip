@@ -37,6 +37,23 @@
 
 namespace qf {
 
+// numpy's pairwise_sum for n < 128 (numpy/_core/src/umath/loops_utils.h.src)
+__device__ __forceinline__ double np_pairwise_sum(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
 // One wave per row: the lanes walk the model's trees in parallel (tree c0 + lane
 // of each 64-tree chunk, the row's features staged in LDS), then lane b adds
 // booster b's leaf values of the chunk in tree order onto its running sum — the
@@ -103,20 +120,57 @@ __device__ __forceinline__ double gbdt_walk(const M& m, const double* x, int t) 
   return m.leaf(lb + leaf);
 }
 
-// The rows of wave wid, strided over the grid: stage the row, walk, sum.
-template <class M>
-__device__ __forceinline__ void gbdt_rows(const GbdtParams& p, const M& m, double* sxw,
-                                          double* sl, int wid, int lane, int T, bool staged) {
+// learned_weights_kernel's arithmetic for one row (lane 0): numpy's clip, the row
+// sum as 0.0 + pairwise_sum, the zero guard, the division, 1 / n for unknown runs.
+__device__ __forceinline__ void learned_row_weights(const LearnedWeightParams& lw, int64_t q,
+                                                    const double* pred) {
+  double c[kMaxBoosters];
+  for (int b = 0; b < lw.n_boosters; ++b) {
+    const double v = pred[b];
+    c[b] = (v > 0.0 || isnan(v)) ? v : 0.0;  // np.clip(pred, 0, None): NaN kept, -0.0 -> +0.0
+  }
+  double s = 0.0 + np_pairwise_sum(c, lw.n_boosters);  // the reduction starts from 0.0
+  if (s == 0.0) s = 1.0;
+  const double dflt = 1.0 / (double)lw.n_boosters;
+  for (int r = 0; r < lw.n_runs; ++r) {
+    const int j = lw.run_to_booster[r];
+    lw.w_out[q * lw.n_runs + r] = j >= 0 ? c[j] / s : dflt;
+  }
+}
+
+// A row's features: the X row (qf_gbdt_predict), or read from the QPP micro-units as
+// qpp_features_kernel lays them out (qf_learned_gbdt_weights: X[q, 13 j + c] =
+// micro[(q R + run[j]) 13 + c] / 1e6, 0.0 for a block without a run).
+struct RowFromX {
+  const GbdtParams& p;
+  __device__ double operator()(int64_t row, int i) const { return p.X[row * p.n_features + i]; }
+};
+struct RowFromMicro {
+  const GbdtFusedParams& f;
+  __device__ double operator()(int64_t row, int i) const {
+    const int j = i / kQppCols, c = i - j * kQppCols;
+    const int r = f.blk.run[j];
+    if (r < 0) return 0.0;
+    const int64_t m = f.micro[(row * f.R + r) * kQppCols + c];
+    return (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m) : (double)m / 1e6;
+  }
+};
+
+// The rows of wave wid, strided over the grid: stage the row, walk, sum; then the
+// raw predictions (p.out) and / or the learned weights (lw, when lw->w_out).
+template <class M, class X>
+__device__ __forceinline__ void gbdt_rows(const GbdtParams& p, const M& m, const X& xrow,
+                                          const LearnedWeightParams* lw, double* sxw, double* sl,
+                                          int wid, int lane, int T, bool staged) {
   const int b = lane < p.n_boosters ? lane : 0;
   for (int64_t row = (int64_t)blockIdx.x * kGbdtWaves + wid; row < p.n_rows;
        row += (int64_t)gridDim.x * kGbdtWaves) {
-    const double* xg = p.X + row * p.n_features;
     if (staged) {
-      for (int i = lane; i < p.n_features; i += 64) sxw[i] = xg[i];
+      for (int i = lane; i < p.n_features; i += 64) sxw[i] = xrow(row, i);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
-    const double* x = staged ? sxw : xg;
+    const double* x = staged ? sxw : p.X + row * p.n_features;
     // lane b < n_boosters: booster b's trees [tb, te) and its running sum
     const int tb = p.tree_off[b], te = p.tree_off[b + 1];
     double s = 0.0;
@@ -132,15 +186,23 @@ __device__ __forceinline__ void gbdt_rows(const GbdtParams& p, const M& m, doubl
       __builtin_amdgcn_wave_barrier();  // every sum read before the next chunk's writes
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
-    if (lane < p.n_boosters) p.out[row * p.n_boosters + lane] = s;
-    __builtin_amdgcn_wave_barrier();  // the row's features read before the next row's
+    if (lane < p.n_boosters) {
+      if (p.out) p.out[row * p.n_boosters + lane] = s;
+      sl[lane] = s;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lw && lane == 0) learned_row_weights(*lw, row, sl);
+    __builtin_amdgcn_wave_barrier();  // the row's features and sums read before the next row's
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
 }
 
-__global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[kGbdtLds];
-  __shared__ double sleaf[kGbdtWaves][64];
+// The model's LDS image (when it fits) and the walk of every row; X is the row source.
+template <class X>
+__device__ __forceinline__ void gbdt_block(const GbdtParams& p, const X& xrow,
+                                           const LearnedWeightParams* lw, unsigned char* lds,
+                                           double (&sleaf)[kGbdtWaves][64]) {
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int T = p.tree_off[p.n_boosters];
   const int NN = p.node_off[T], NL = p.leaf_off[T], nf = p.n_features;
@@ -152,6 +214,7 @@ __global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParam
                        8 * (int64_t)(T + 1);
   const bool fits = need <= kGbdtLds && nf <= (1 << 24);  // uniform; features fit 24 bits
   double* sx = (double*)lds;
+  double* sxw = staged ? sx + (int64_t)wid * nf : nullptr;
   if (fits) {
     double* thr = (double*)(lds + xbytes);
     double* lv = thr + NN;
@@ -176,45 +239,32 @@ __global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParam
     }
     __syncthreads();
     const GbdtLds m{thr, lv, fd, lc, rc, no, lo};
-    gbdt_rows(p, m, sx + (int64_t)wid * nf, sleaf[wid], wid, lane, T, staged);
+    gbdt_rows(p, m, xrow, lw, sxw, sleaf[wid], wid, lane, T, staged);
   } else {
     const GbdtGlobal m{p};
-    gbdt_rows(p, m, staged ? sx + (int64_t)wid * nf : nullptr, sleaf[wid], wid, lane, T, staged);
+    gbdt_rows(p, m, xrow, lw, sxw, sleaf[wid], wid, lane, T, staged);
   }
 }
 
-// numpy's pairwise_sum for n < 128 (numpy/_core/src/umath/loops_utils.h.src)
-__device__ __forceinline__ double np_pairwise_sum(const double* a, int n) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r += a[i];
-    return r;
-  }
-  double r[8];
-  for (int j = 0; j < 8; ++j) r[j] = a[j];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8)
-    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
-  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res += a[i];
-  return res;
+__global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kGbdtLds];
+  __shared__ double sleaf[kGbdtWaves][64];
+  gbdt_block(p, RowFromX{p}, nullptr, lds, sleaf);
+}
+
+// Learned fusion's weights in one launch: features from the QPP micro-units, the
+// walk, learned_weights_kernel's normalisation (src/fusion.py:415-440,
+// src/models/base.py:120-125) — bit for bit the three-launch path.
+__global__ __launch_bounds__(64 * kGbdtWaves) void learned_gbdt_weights_kernel(GbdtFusedParams f) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kGbdtLds];
+  __shared__ double sleaf[kGbdtWaves][64];
+  gbdt_block(f.gbdt, RowFromMicro{f}, &f.lw, lds, sleaf);
 }
 
 __global__ __launch_bounds__(256) void learned_weights_kernel(LearnedWeightParams p) {
   const int64_t q = block_id() * blockDim.x + threadIdx.x;
   if (q >= p.n_queries) return;
-  double c[kMaxBoosters];
-  for (int b = 0; b < p.n_boosters; ++b) {
-    const double v = p.pred[q * p.n_boosters + b];
-    c[b] = (v > 0.0 || isnan(v)) ? v : 0.0;  // np.clip(pred, 0, None): NaN kept, -0.0 -> +0.0
-  }
-  double s = 0.0 + np_pairwise_sum(c, p.n_boosters);  // the reduction starts from 0.0
-  if (s == 0.0) s = 1.0;
-  const double dflt = 1.0 / (double)p.n_boosters;
-  for (int r = 0; r < p.n_runs; ++r) {
-    const int j = p.run_to_booster[r];
-    p.w_out[q * p.n_runs + r] = j >= 0 ? c[j] / s : dflt;
-  }
+  learned_row_weights(p, q, p.pred + q * p.n_boosters);
 }
 
 // numpy's float32 pairwise_sum for n < 128 (float32 accumulators)
@@ -302,6 +352,14 @@ hipError_t gbdt_predict_launch(const GbdtParams& p, hipStream_t st) {
   const int64_t want = (p.n_rows + kGbdtWaves - 1) / kGbdtWaves;
   const unsigned grid = (unsigned)(want < 256 ? want : 256);
   hipLaunchKernelGGL(gbdt_predict_kernel, dim3(grid), dim3(64 * kGbdtWaves), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t learned_gbdt_weights_launch(const GbdtFusedParams& f, hipStream_t st) {
+  if (f.gbdt.n_rows == 0) return hipSuccess;
+  const int64_t want = (f.gbdt.n_rows + kGbdtWaves - 1) / kGbdtWaves;
+  const unsigned grid = (unsigned)(want < 256 ? want : 256);
+  hipLaunchKernelGGL(learned_gbdt_weights_kernel, dim3(grid), dim3(64 * kGbdtWaves), 0, st, f);
   return hipGetLastError();
 }
 

@@ -56,6 +56,8 @@ SIGNATURES = {
     "qf_gbdt_predict": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp]),
     "qf_learned_weights": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "qf_learned_gbdt_weights": (C.c_int, [_i64, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "qf_mlp_weights": (C.c_int, [_i64, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
     "qf_fuse_learned_f32": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, C.c_uint32, _i32,
                                       _vp, _vp, _vp, _vp, _i64, _vp]),

@@ -322,6 +322,31 @@ def gbdt_predict(X: torch.Tensor, packed) -> torch.Tensor:
     return out
 
 
+def learned_gbdt_weights(micro: torch.Tensor, n_queries: int, n_retrievers: int, run_of_block,
+                         packed, run_to_booster, want_pred: bool = False):
+    """qf_learned_gbdt_weights: qpp_features + gbdt_predict + learned_weights in one
+    launch — [Q * R] run weights (and the raw [Q, B] predictions if want_pred).  For
+    models of up to 19 retrievers (13 features each); bit-identical to the three calls."""
+    import numpy as np
+    dev = require_device()
+    Q, R = int(n_queries), int(n_retrievers)
+    blocks = np.ascontiguousarray(run_of_block, dtype=np.int32)
+    rb = np.ascontiguousarray(run_to_booster, dtype=np.int32)
+    if micro.dtype != torch.int64 or micro.numel() != Q * R * _lib.QPP_COLS:
+        raise ValueError(f"micro must be int64 [{Q * R}, {_lib.QPP_COLS}]")
+    if packed.n_features != len(blocks) * _lib.QPP_COLS:
+        raise ValueError("the model's features must be 13 per block of run_of_block")
+    d = packed.to_device(dev)
+    w = torch.empty(Q * len(rb), dtype=torch.float64, device=dev)
+    pred = torch.empty((Q, packed.n_boosters), dtype=torch.float64, device=dev) if want_pred else None
+    _lib.call("qf_learned_gbdt_weights", Q, _ptr(micro.contiguous()), R, blocks.ctypes.data,
+              len(blocks), packed.n_boosters, _ptr(d["tree_off"]), _ptr(d["node_off"]),
+              _ptr(d["leaf_off"]), _ptr(d["feature"]), _ptr(d["threshold"]), _ptr(d["dtype"]),
+              _ptr(d["left"]), _ptr(d["right"]), _ptr(d["leaf_value"]), len(rb), rb.ctypes.data,
+              _ptr(pred), _ptr(w), _stream())
+    return (w, pred) if want_pred else w
+
+
 def learned_weights(pred: torch.Tensor, run_to_booster) -> torch.Tensor:
     """qf_learned_weights: [Q * R] run weights from [Q, B] predictions."""
     import numpy as np

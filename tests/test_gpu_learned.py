@@ -84,6 +84,33 @@ def test_gbdt_model_beyond_lds_walks_global_arrays(gpu):
     assert got2.tobytes() == want2.tobytes()
 
 
+@pytest.mark.parametrize("name", NAMES)
+def test_learned_gbdt_weights_one_launch_equals_three(gpu, name):
+    """qf_learned_gbdt_weights (features from the QPP micro-units, the walk and the
+    weight normalisation in one launch) == qf_qpp_features + qf_gbdt_predict +
+    qf_learned_weights bit for bit: predictions and weights, a model block whose
+    retriever the batch lacks (-1), a run the model does not know (-1), zero and
+    negative micro-units, a row count that is no multiple of the 16 rows in flight."""
+    from qppfuse import engine, lgbm
+    m = _model(name)
+    p = lgbm.pack_model(m)
+    rng = np.random.default_rng(13)
+    Q, R = 1037, 6
+    micro = rng.integers(-200_000, 1_200_000, (Q * R, 13)).astype(np.int64)
+    micro[rng.random(micro.shape) < 0.2] = 0
+    blocks = [3, 0, -1, 5, 1][:len(m.retrievers)]
+    run_to_booster = [1, -1, 0, 3, 4, 2]
+    mt = torch.from_numpy(micro).to(gpu)
+    X = engine.qpp_features(mt, Q, R, blocks)
+    pred3 = engine.gbdt_predict(X, p)
+    w3 = engine.learned_weights(pred3, run_to_booster)
+    w1, pred1 = engine.learned_gbdt_weights(mt, Q, R, blocks, p, run_to_booster, want_pred=True)
+    assert torch.equal(pred1.view(torch.int64), pred3.view(torch.int64))
+    assert torch.equal(w1.view(torch.int64), w3.view(torch.int64))
+    assert torch.equal(engine.learned_gbdt_weights(mt, Q, R, blocks, p, run_to_booster)
+                       .view(torch.int64), w3.view(torch.int64))
+
+
 def test_learned_weights_match_numpy(gpu):
     from qppfuse import engine
     rng = np.random.default_rng(3)

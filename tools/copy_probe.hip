@@ -56,13 +56,21 @@ int main(int argc, char** argv) {
   CK(hipMemset(s, 1, bytes));
   CK(hipMemset(d, 0, bytes));
   const int reps = 20;
-  for (int blocks : {1024, 2048, 4096}) {
-    run<1, false>(d, s, n, blocks, reps);
-    run<4, false>(d, s, n, blocks, reps);
-    run<8, false>(d, s, n, blocks, reps);
-    run<1, true>(d, s, n, blocks, reps);
-    run<4, true>(d, s, n, blocks, reps);
-    run<8, true>(d, s, n, blocks, reps);
+  if (argc > 2) {  // round 4: fewer workgroups per CU, and the one-shot grid (one access per thread)
+    for (int blocks : {256, 512, 768, 1024, 1280, (int)((n + 255) / 256)}) {
+      run<1, false>(d, s, n, blocks, reps);
+      run<1, true>(d, s, n, blocks, reps);
+      run<2, true>(d, s, n, blocks, reps);
+    }
+  } else {
+    for (int blocks : {1024, 2048, 4096}) {
+      run<1, false>(d, s, n, blocks, reps);
+      run<4, false>(d, s, n, blocks, reps);
+      run<8, false>(d, s, n, blocks, reps);
+      run<1, true>(d, s, n, blocks, reps);
+      run<4, true>(d, s, n, blocks, reps);
+      run<8, true>(d, s, n, blocks, reps);
+    }
   }
   CK(hipFree(s));
   CK(hipFree(d));
