@@ -782,7 +782,8 @@ def main():
                          "valu_insts_per_launch": valu,
                          "copy_ceiling_gbs": round(copy_gbs, 1),
                          "copy_ceiling_source": "qf_stream_copy: 16 B/lane non-temporal "
-                                                "streaming copy kernel, 1 GiB, read + write",
+                                                "copy, one access per thread, one-shot grid, "
+                                                "1 GiB, read + write, best of 4 x 10",
                          "copy_blit_gbs": round(copy["blit"], 1),
                          "frac_of_copy_ceiling": round(achieved / copy_gbs, 4)},
             "cpu_baseline": cpu,

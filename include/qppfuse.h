@@ -401,8 +401,8 @@ int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int3
 
 /*
  * Measurement support (bench.py's roofline): a device-to-device streaming copy of
- * nbytes (a multiple of 16; 16-byte aligned pointers), 16 bytes per lane per
- * access, non-temporal.  Its rate (2 * nbytes / time) is the practical HBM
+ * nbytes (a multiple of 16; 16-byte aligned pointers), 16 bytes per lane, one
+ * non-temporal access per thread over a one-shot grid (the fastest shape measured).  Its rate (2 * nbytes / time) is the practical HBM
  * ceiling the roofline object reports next to the 8 TB/s spec peak.  No
  * counterpart in the reference.
  */

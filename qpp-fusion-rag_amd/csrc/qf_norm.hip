@@ -160,25 +160,24 @@ hipError_t synth_launch(int64_t q_begin, int64_t n_queries, int32_t R, int32_t K
 }
 
 // ---- the HBM copy ceiling (measurement support) ------------------------------------
-// A streaming copy, 16 bytes per lane per access, non-temporal, a grid-stride loop
-// over 4 workgroups of 256 threads per CU: the practical read + write rate of HBM
-// the roofline's achieved bytes are compared with.  tools/copy_probe.hip measured
-// the shapes on MI355X (1 GiB, r04): this one 6.15 TB/s; 2 or 4 per CU, or 4 or 8
-// accesses in flight per lane at grid strides, 4.3-5.7 TB/s; plain stores 5.7.
+// A streaming copy, 16 bytes per lane, non-temporal, ONE access per thread over a
+// one-shot grid (n16 / 256 workgroups): the practical read + write rate of HBM the
+// roofline's achieved bytes are compared with.  tools/copy_probe.hip measured the
+// shapes on MI355X (1 GiB): this one 6.57 TB/s (plain accesses 6.21); grid-stride
+// loops over 1-5 workgroups per CU 3.2-5.9 TB/s, 2 / 4 / 8 accesses per lane in
+// flight 4.3-5.8 (profiles/r04_copy_probe.jsonl, r04_copy_probe2.jsonl).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void stream_copy_kernel(u32x4* __restrict__ dst,
                                                           const u32x4* __restrict__ src,
                                                           int64_t n16) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+  const int64_t i = block_id() * 256 + threadIdx.x;
+  if (i < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
 }
 
 hipError_t stream_copy_launch(void* dst, const void* src, int64_t n16, hipStream_t st) {
-  const int64_t want = (n16 + 255) / 256;
-  const int blocks = (int)(want < 1024 ? (want > 0 ? want : 1) : 1024);
-  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, st, (u32x4*)dst,
-                     (const u32x4*)src, n16);
+  if (n16 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(stream_copy_kernel, grid_for((n16 + 255) / 256), dim3(256), 0, st,
+                     (u32x4*)dst, (const u32x4*)src, n16);
   return hipGetLastError();
 }
 
