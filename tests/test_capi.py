@@ -95,6 +95,22 @@ def test_argument_validation_without_device():
                   kind.ctypes.data, cut.ctypes.data, 8, None)
     with pytest.raises(ValueError, match="qpp_index"):
         _lib.call("qf_qpp_normalize", 1, 1, 1, 1, 1, 1, 13, None, None, None, None)
+    # the one-launch learned weights: host-side size and map checks (no device needed)
+    blocks = np.array([0, 1, -1], np.int32)
+    rb = np.array([0, 1, -1], np.int32)
+    args = lambda nb, nboost, rbp, rblk: (5, 8, 3, rblk.ctypes.data, nb, nboost, 8, 8, 8, 8, 8,
+                                         8, 8, 8, 8, 3, rbp.ctypes.data, None, 8, None)
+    with pytest.raises(ValueError, match="bad sizes"):
+        _lib.call("qf_learned_gbdt_weights", *args(20, 3, rb, blocks))  # 20 x 13 > 256 features
+    with pytest.raises(ValueError, match="bad sizes"):
+        _lib.call("qf_learned_gbdt_weights", *args(3, 17, rb, blocks))  # boosters > 16
+    with pytest.raises(ValueError, match="run_of_block"):
+        _lib.call("qf_learned_gbdt_weights", *args(3, 3, rb, np.array([0, 3, 1], np.int32)))
+    with pytest.raises(ValueError, match="run_to_booster"):
+        _lib.call("qf_learned_gbdt_weights", *args(3, 3, np.array([0, 3, 1], np.int32), blocks))
+    with pytest.raises(ValueError, match="null buffer"):
+        _lib.call("qf_learned_gbdt_weights", 5, None, 3, blocks.ctypes.data, 3, 3, 8, 8, 8, 8, 8,
+                  8, 8, 8, 8, 3, rb.ctypes.data, None, 8, None)
 
 
 def test_product_has_no_cpu_fallback(monkeypatch):
