@@ -304,14 +304,17 @@ class Pipeline:
             minmax()
         else:
             e.qpp_raw(self.raw, self.off, self.R, a.qpp_top_k, self.nt, self.tf, out=self.qraw)
-            e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
-            work = None
-            if self.world > 1:  # the path's only exchange: ~1 KB over RCCL/xGMI,
-                from qppfuse.dist import allreduce_minmax  # hidden behind the min-max kernel
+            if self.world > 1:
+                e.qpp_colminmax(self.qraw, self.off, self.R, out=self.mm)
+                # the path's only exchange: ~1 KB over RCCL/xGMI, hidden behind the
+                # min-max kernel
+                from qppfuse.dist import allreduce_minmax
                 work = allreduce_minmax(self.mm, async_op=True)
-            minmax()
-            if work is not None:
+                minmax()
                 work.wait()
+            else:  # every query here: the column extremes and the min-max in one launch
+                e.minmax_colminmax(self.raw, self.off, self.R, self.qraw, micro_out=self.micro,
+                                   mm_out=self.mm)
             learned = "learned" in self.methods
             o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
                                 want_micro=learned, want_weights=not learned)

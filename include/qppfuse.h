@@ -119,6 +119,17 @@ int qf_qpp_colminmax(const double* raw, const int64_t* list_off, int64_t n_queri
                      int32_t n_retrievers, double* mm_out, void* stream);
 
 /*
+ * qf_minmax_per_query (micro-units and / or normalised scores of the n_queries *
+ * n_retrievers lists) and qf_qpp_colminmax (of raw_qpp into mm_out) in ONE launch —
+ * the two independent reductions of an unsharded step; the same bits as the two
+ * calls.  (A sharded step keeps them apart: the column extremes go through the MIN
+ * all-reduce while the min-max kernel runs.)
+ */
+int qf_minmax_colminmax(const double* score, const int64_t* list_off, int64_t n_queries,
+                        int32_t n_retrievers, double* out_norm, int32_t* out_micro,
+                        const double* raw_qpp, double* mm_out, void* stream);
+
+/*
  * zscore statistics (src/qpp.py:358-359): per (retriever, column) numpy's
  * arr.mean() and the scale arr.std() (population; 1.0 when not > 0) over the
  * queries with a non-empty list, in query order.  Bit-identical to numpy: its

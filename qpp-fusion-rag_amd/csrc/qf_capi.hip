@@ -72,6 +72,18 @@ int qf_qpp_colminmax(const double* raw, const int64_t* list_off, int64_t n_queri
                "qf_qpp_colminmax");
 }
 
+int qf_minmax_colminmax(const double* score, const int64_t* list_off, int64_t n_queries,
+                        int32_t n_retrievers, double* out_norm, int32_t* out_micro,
+                        const double* raw_qpp, double* mm_out, void* stream) {
+  if (n_queries < 0 || n_retrievers <= 0 || !list_off || !raw_qpp || !mm_out ||
+      (n_queries > 0 && !score))
+    return fail(QF_EINVAL, "qf_minmax_colminmax: bad arguments");
+  if (!out_norm && !out_micro) return fail(QF_EINVAL, "qf_minmax_colminmax: no output");
+  return check(qf::minmax_colminmax_launch(score, list_off, n_queries, n_retrievers, out_norm,
+                                           out_micro, raw_qpp, mm_out, (hipStream_t)stream),
+               "qf_minmax_colminmax");
+}
+
 int qf_qpp_colmeanstd(const double* raw, const int64_t* list_off, int64_t n_queries,
                       int32_t n_retrievers, double* st_out, void* stream) {
   if (n_queries < 0 || n_retrievers <= 0 || !raw || !list_off || !st_out)

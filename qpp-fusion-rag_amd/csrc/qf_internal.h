@@ -170,6 +170,9 @@ hipError_t qpp_normalize_launch(const double* raw, const double* mm, const int64
                                 int64_t Q, int32_t R, int32_t mode, int32_t qpp_index,
                                 double* norm_out, int64_t* micro_out, double* w_out,
                                 hipStream_t st);
+hipError_t minmax_colminmax_launch(const double* score, const int64_t* list_off, int64_t Q,
+                                   int32_t R, double* out_norm, int32_t* out_micro,
+                                   const double* raw, double* mm, hipStream_t st);
 hipError_t minmax_launch(const double* score, const int64_t* list_off, int64_t n_lists,
                          double* out_norm, int32_t* out_micro, hipStream_t st);
 hipError_t stream_copy_launch(void* dst, const void* src, int64_t n16, hipStream_t st);

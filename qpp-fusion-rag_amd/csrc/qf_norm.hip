@@ -6,71 +6,34 @@
 // reduction, then (s - min) / range with range = 1.0 when max == min.
 #include "qf_common.h"
 #include "qf_internal.h"
+#include "qf_lists.h"
 
 namespace qf {
 
 __global__ __launch_bounds__(256) void minmax_per_query_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     double* __restrict__ out_norm, int32_t* __restrict__ out_micro) {
-  const int lane = threadIdx.x & 63;
   const int64_t l = block_id() * 4 + (threadIdx.x >> 6);
   if (l >= n_lists) return;
-  const int64_t a = list_off[l], b = list_off[l + 1];
-  constexpr int kRegRows = 16;  // lists of <= 1024 entries: one HBM read, held in registers
-  if (b - a <= 64 * kRegRows) {
-    double v[kRegRows];
-    double mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < kRegRows; ++j) {  // every load in flight before the first use
-      const int64_t i = a + j * 64 + lane;
-#ifdef QF_MINMAX_NT  // development A/B: the raw scores read once, non-temporal
-      v[j] = i < b ? __builtin_nontemporal_load(&score[i]) : 0.0;
-#else
-      v[j] = i < b ? score[i] : 0.0;
-#endif
-    }
-#pragma unroll
-    for (int j = 0; j < kRegRows; ++j)
-      if (a + j * 64 + lane < b) {
-        mn = fmin(mn, v[j]);
-        mx = fmax(mx, v[j]);
-      }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    const double range = mx > mn ? mx - mn : 1.0;
-    const double y = 1.0 / range;  // one IEEE division per list
-    const bool fast = range >= 0x1p-900 && range <= 0x1p900;
-#pragma unroll
-    for (int j = 0; j < kRegRows; ++j) {
-      const int64_t i = a + j * 64 + lane;
-      if (i < b) {
-        const double d = v[j] - mn;
-        const double x = (fast && d >= 0x1p-900 && d <= 0x1p900) ? div_by_recip(d, range, y)
-                                                                 : d / range;
-        if (out_norm) out_norm[i] = x;
-        if (out_micro) out_micro[i] = (int32_t)round6(x);
-      }
-    }
+  minmax_list(score, list_off, l, out_norm, out_micro);
+}
+
+// The unsharded step's two independent reductions in one launch: the QPP column
+// min / max workgroups first (latency-bound, R * 13 of them), then the per-list
+// min-max ones — the column pass runs beside the streaming one instead of as a
+// launch of its own (qf_minmax_colminmax; the same bits as the two kernels).
+__global__ __launch_bounds__(256) void minmax_colminmax_kernel(
+    const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t Q, int32_t R,
+    double* __restrict__ out_norm, int32_t* __restrict__ out_micro,
+    const double* __restrict__ raw, double* __restrict__ mm) {
+  const int64_t bid = block_id(), ncol = (int64_t)R * kQppCols;
+  if (bid < ncol) {
+    qpp_colminmax_block(raw, list_off, Q, R, mm, (int)bid);
     return;
   }
-  double mn = INFINITY, mx = -INFINITY;
-  for (int64_t i = a + lane; i < b; i += 64) {
-    const double s = score[i];
-    mn = fmin(mn, s);
-    mx = fmax(mx, s);
-  }
-  mn = wave_min(mn);
-  mx = wave_max(mx);
-  const double range = mx > mn ? mx - mn : 1.0;
-  const double y = 1.0 / range;
-  const bool fast = range >= 0x1p-900 && range <= 0x1p900;
-  for (int64_t i = a + lane; i < b; i += 64) {
-    const double d = score[i] - mn;
-    const double v = (fast && d >= 0x1p-900 && d <= 0x1p900) ? div_by_recip(d, range, y)
-                                                             : d / range;
-    if (out_norm) out_norm[i] = v;
-    if (out_micro) out_micro[i] = (int32_t)round6(v);
-  }
+  const int64_t l = (bid - ncol) * 4 + (threadIdx.x >> 6);
+  if (l >= Q * R) return;
+  minmax_list(score, list_off, l, out_norm, out_micro);
 }
 
 hipError_t minmax_launch(const double* score, const int64_t* list_off, int64_t n_lists,
@@ -78,6 +41,16 @@ hipError_t minmax_launch(const double* score, const int64_t* list_off, int64_t n
   if (n_lists == 0) return hipSuccess;
   hipLaunchKernelGGL(minmax_per_query_kernel, grid_for((n_lists + 3) / 4), dim3(256), 0,
                      st, score, list_off, n_lists, out_norm, out_micro);
+  return hipGetLastError();
+}
+
+hipError_t minmax_colminmax_launch(const double* score, const int64_t* list_off, int64_t Q,
+                                   int32_t R, double* out_norm, int32_t* out_micro,
+                                   const double* raw, double* mm, hipStream_t st) {
+  if (Q * R == 0) return hipSuccess;
+  const int64_t blocks = (int64_t)R * kQppCols + (Q * R + 3) / 4;
+  hipLaunchKernelGGL(minmax_colminmax_kernel, grid_for(blocks), dim3(256), 0, st, score, list_off,
+                     Q, R, out_norm, out_micro, raw, mm);
   return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 // off them.
 #include "qf_common.h"
 #include "qf_internal.h"
+#include "qf_lists.h"
 
 namespace qf {
 
@@ -348,42 +349,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
 __global__ __launch_bounds__(256) void qpp_colminmax_kernel(
     const double* __restrict__ raw, const int64_t* __restrict__ list_off, int64_t Q, int32_t R,
     double* __restrict__ mm) {
-  __shared__ double smin[4], smax[4];
-  const int rc = blockIdx.x;  // r * 13 + c
-  const int r = rc / kQppCols, c = rc % kQppCols;
-  double vmin = INFINITY, vmax = -INFINITY;
-  // 8 queries per thread per step, their loads in flight together
-  constexpr int kU = 8;
-  for (int64_t q0 = threadIdx.x; q0 < Q; q0 += (int64_t)blockDim.x * kU) {
-    double v[kU];
-    bool pr[kU];
-#pragma unroll
-    for (int t = 0; t < kU; ++t) {
-      const int64_t q = q0 + (int64_t)t * blockDim.x;
-      const int64_t l = q * R + r;
-      pr[t] = q < Q && list_off[l + 1] > list_off[l];
-      v[t] = q < Q ? raw[l * kQppCols + c] : 0.0;
-    }
-#pragma unroll
-    for (int t = 0; t < kU; ++t)
-      if (pr[t]) {
-        vmin = fmin(vmin, v[t]);
-        vmax = fmax(vmax, v[t]);
-      }
-  }
-  vmin = wave_min(vmin);
-  vmax = wave_max(vmax);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) { smin[wid] = vmin; smax[wid] = vmax; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)(blockDim.x / 64); ++w) {
-      vmin = fmin(vmin, smin[w]);
-      vmax = fmax(vmax, smax[w]);
-    }
-    mm[rc] = vmin;
-    mm[R * kQppCols + rc] = -vmax;
-  }
+  qpp_colminmax_block(raw, list_off, Q, R, mm, (int)blockIdx.x);
 }
 
 // ---- zscore statistics: numpy's mean / std of each column --------------------

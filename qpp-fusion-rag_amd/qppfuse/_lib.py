@@ -42,6 +42,7 @@ SIGNATURES = {
     "qf_minmax_per_query": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "qf_qpp_raw": (C.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_qpp_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "qf_minmax_colminmax": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "qf_qpp_colmeanstd": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "qf_qpp_normalize": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "qf_qpp_features": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),

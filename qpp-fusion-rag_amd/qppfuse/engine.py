@@ -198,6 +198,28 @@ def minmax_per_query(score: torch.Tensor, list_off: torch.Tensor, want_norm=True
     return norm, micro
 
 
+def minmax_colminmax(score: torch.Tensor, list_off: torch.Tensor, n_retrievers: int,
+                     raw_qpp: torch.Tensor, want_norm=False, want_micro=True,
+                     micro_out: Optional[torch.Tensor] = None,
+                     mm_out: Optional[torch.Tensor] = None):
+    """minmax_per_query + qpp_colminmax in one launch (an unsharded batch): returns
+    (norm, micro, mm) — the same values as the two calls."""
+    require_device()
+    R = int(n_retrievers)
+    Q = (list_off.numel() - 1) // R
+    dev = score.device
+    norm = torch.empty_like(score) if want_norm else None
+    micro = None
+    if want_micro:
+        micro = micro_out if micro_out is not None else torch.empty(score.shape, dtype=torch.int32,
+                                                                    device=dev)
+    mm = mm_out if mm_out is not None else torch.empty(2 * R * _lib.QPP_COLS,
+                                                       dtype=torch.float64, device=dev)
+    _lib.call("qf_minmax_colminmax", _ptr(score), _ptr(list_off), Q, R, _ptr(norm), _ptr(micro),
+              _ptr(raw_qpp), _ptr(mm), _stream())
+    return norm, micro, mm
+
+
 def qpp_raw(score: torch.Tensor, list_off: torch.Tensor, n_retrievers: int, top_k: int,
             num_terms: torch.Tensor, text_feat: torch.Tensor,
             out: Optional[torch.Tensor] = None) -> torch.Tensor:

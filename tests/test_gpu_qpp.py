@@ -115,6 +115,34 @@ def test_normalize_weights_and_rounding(gpu):
         assert (micro[7] == 0).all()
 
 
+@pytest.mark.parametrize("Q", [7, 3452])
+def test_minmax_colminmax_one_launch_equals_two(gpu, Q):
+    """qf_minmax_colminmax == qf_minmax_per_query + qf_qpp_colminmax bit for bit:
+    micro-units, normalised scores and the column [min, -max], with empty lists,
+    constant lists and signed zeros."""
+    from qppfuse import engine
+    rng = np.random.default_rng(Q)
+    R = 5
+    lens = rng.integers(0, 1100, Q * R)
+    lens[::9] = 0
+    lists = [np.sort(rng.gamma(2, 3, n))[::-1] for n in lens]
+    lists[3] = np.full(len(lists[3]), 0.5)
+    off = np.zeros(Q * R + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    flat = np.concatenate(lists) if off[-1] else np.zeros(1)
+    raw = rng.gamma(2, 3, (Q * R, 13))
+    raw[::4, 2] = -0.0
+    raw[1::4, 2] = 0.0
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    gs, go, gq = t(flat), t(off), t(raw)
+    norm2, micro2 = engine.minmax_per_query(gs, go)
+    mm2 = engine.qpp_colminmax(gq, go, R)
+    norm1, micro1, mm1 = engine.minmax_colminmax(gs, go, R, gq, want_norm=True)
+    assert torch.equal(micro1, micro2)
+    assert torch.equal(norm1.view(torch.int64), norm2.view(torch.int64))
+    assert torch.equal(mm1.view(torch.int64), mm2.view(torch.int64))
+
+
 def test_compute_qpp_for_res_file(gpu, tmp_path):
     from qppfuse.qpp import compute_qpp_for_res_file
     from qppfuse import textfeat
