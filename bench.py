@@ -251,20 +251,20 @@ class Pipeline:
         e, a, R, K = self.engine, self.args, self.R, self.K
         off, docid, raw = e.synth_runs(q_begin + start, n, R, K, seed=SEED)
         _, micro = e.minmax_per_query(raw, off, want_norm=False)
-        w = None
+        w, qppw = None, None
         if a.wl["qpp"]:
             nt, tf = self.text_arrays(q_begin, Q_shard)
             nt = torch.from_numpy(np.ascontiguousarray(nt[start:start + n])).to(self.dev)
             tf = torch.from_numpy(np.ascontiguousarray(tf[start:start + n])).to(self.dev)
             qraw = e.qpp_raw(raw, off, R, a.qpp_top_k, nt, tf)
-            learned = "learned" in self.methods
-            o = e.qpp_normalize(qraw, self.mm, off, R, "minmax", a.qpp_index,
-                                want_micro=learned, want_weights=not learned)
-            w = o["weights"]
-            if learned:
-                w = e.learned_gbdt_weights(o["micro"], n, R, self.block_runs, self.packed,
-                                           self.run_to_booster)
-        out = e.fuse(off, docid, micro, R, self.methods, 60, weights=w, max_entries=R * K)
+            if "learned" in self.methods:
+                w = e.learned_gbdt_weights(None, n, R, self.block_runs, self.packed,
+                                           self.run_to_booster, raw_qpp=qraw, mm=self.mm,
+                                           list_off=off)
+            else:
+                qppw = (qraw, self.mm, "minmax", a.qpp_index)
+        out = e.fuse(off, docid, micro, R, self.methods, 60, weights=w, max_entries=R * K,
+                     qpp=qppw)
         return e.fused_topk(out, off, R, a.gather_topk)
 
     def gather_parity(self, per_block: int = 4):
@@ -299,7 +299,7 @@ class Pipeline:
         minmax = lambda: _lib.call("qf_minmax_per_query", self.raw.data_ptr(),
                                    self.off.data_ptr(), self.Q * self.R, None,
                                    self.micro.data_ptr(), s)
-        w = None
+        w, qppw = None, None
         if not a.wl["qpp"]:
             minmax()
         else:
@@ -315,18 +315,19 @@ class Pipeline:
             else:  # every query here: the column extremes and the min-max in one launch
                 e.minmax_colminmax(self.raw, self.off, self.R, self.qraw, micro_out=self.micro,
                                    mm_out=self.mm)
-            learned = "learned" in self.methods
-            o = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax", a.qpp_index,
-                                want_micro=learned, want_weights=not learned)
-            w = o["weights"]
-            if learned:  # the .qpp values as features, GBDT, normalised weights: one launch
-                w = e.learned_gbdt_weights(o["micro"], self.Q, self.R, self.block_runs,
-                                           self.packed, self.run_to_booster)
+            if "learned" in self.methods:
+                # the .qpp values as features (normalised on the fly from the raw
+                # predictors and the column statistics), GBDT, weights: one launch
+                w = e.learned_gbdt_weights(None, self.Q, self.R, self.block_runs, self.packed,
+                                           self.run_to_booster, raw_qpp=self.qraw, mm=self.mm,
+                                           list_off=self.off)
+            else:  # the W-* weights are computed inside the fusion (qf_fuse_qpp)
+                qppw = (self.qraw, self.mm, "minmax", a.qpp_index)
         if timed:
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0.record()
         e.fuse(self.off, self.docid, self.micro, self.R, self.methods, 60, weights=w,
-               max_entries=self.R * self.K, out=self.out)
+               max_entries=self.R * self.K, out=self.out, qpp=qppw)
         if timed:
             t1.record()
             self.ev.append((t0, t1))
@@ -423,13 +424,20 @@ def ndcg_delta(p: Pipeline, dev_vals, nq: int):
 
 
 def host_sample(p: Pipeline, nq: int):
-    """Copy the first nq queries' inputs + device outputs to host numpy."""
+    """Copy the first nq queries' inputs + device outputs to host numpy.  When the
+    step's fusion took its W-* weights from the QPP predictors (qf_fuse_qpp), `w` is
+    what qf_qpp_normalize gives for the same predictors and column statistics — the
+    oracle then fuses with those, so the check covers the in-kernel weights too."""
     R, K = p.R, p.K
     n = nq * R * K
     off = p.off[: nq * R + 1].cpu().numpy()
+    w = p.w
+    if w is None and p.args.wl["qpp"] and "learned" not in p.methods:
+        w = p.engine.qpp_normalize(p.qraw, p.mm, p.off, R, "minmax", p.args.qpp_index,
+                                   want_micro=False)["weights"]
     return dict(off=off, docid=p.docid[:n].cpu().numpy().view(np.uint32),
                 raw=p.raw[:n].cpu().numpy(), micro=p.micro[:n].cpu().numpy(),
-                w=None if p.w is None else p.w[: nq * R].cpu().numpy(),
+                w=None if w is None else w[: nq * R].cpu().numpy(),
                 nt=p.nt[:nq].cpu().numpy(),
                 tf=p.tf[:nq].cpu().numpy(), qraw=p.qraw[: nq * R].cpu().numpy())
 

@@ -210,6 +210,23 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             uint16_t* perm, double* fused, int64_t out_stride, void* stream);
 
 /*
+ * qf_fuse with the W-* weights taken from the QPP predictors themselves: the raw
+ * predictors qpp_raw [n_queries * n_retrievers][13] and their column statistics
+ * qpp_stats (qf_qpp_colminmax's [min, -max] for QF_NORM_MINMAX, qf_qpp_colmeanstd's
+ * [mean, scale] for QF_NORM_ZSCORE; unused for QF_NORM_NONE), column qpp_index
+ * (-1: the mean of the 13) — the weights qf_qpp_normalize's w_out would hold, bit
+ * for bit, computed inside the fusion (src/qpp.py:356-372 + the .qpp round trip of
+ * get_qpp_weight, src/fusion.py:116-158): one launch fewer per batch.  Not with
+ * QF_LEARNED.
+ */
+int qf_fuse_qpp(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
+                const double* qpp_raw, const double* qpp_stats, int32_t qpp_mode,
+                int32_t qpp_index, int32_t methods, int32_t rrf_k, int32_t max_entries,
+                uint32_t* union_docid, int32_t* union_count, uint16_t* perm, double* fused,
+                int64_t out_stride, void* stream);
+
+/*
  * The explicit workspace of qf_fuse (the library allocates only in
  * an explicit workspace).  qf_fuse_workspace_bytes: the bytes a call with these
  * sizes would allocate stream-ordered for its workspace kernel (queries above
@@ -317,13 +334,17 @@ int qf_learned_weights(int64_t n_queries, const double* pred, int32_t n_boosters
 /*
  * qf_qpp_features + qf_gbdt_predict + qf_learned_weights in ONE launch (the step
  * src/fusion.py:415-440 takes from the .qpp values to the run weights): row q's
- * features are read from the QPP micro-units as qf_qpp_features lays them out
+ * features are the QPP micro-units laid out as qf_qpp_features lays them out
  * (run_of_block: HOST array, n_blocks <= 19 so the 13 * n_blocks features fit the
- * kernel's LDS row), the model walked as qf_gbdt_predict does, and w_out filled as
- * qf_learned_weights does — the same bits as the three calls.  pred_out
- * (nullable) receives the raw predictions [n_queries][n_boosters].
+ * kernel's LDS row) — read from `micro`, or, when micro is NULL, normalised on the
+ * fly from raw_qpp with the column statistics mm (norm_mode QF_NORM_*; list_off
+ * marks absent lists) exactly as qf_qpp_normalize would — the model walked as
+ * qf_gbdt_predict does, and w_out filled as qf_learned_weights does: the same bits
+ * as the separate calls.  pred_out (nullable): the raw predictions [n_queries][B].
  */
-int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, int32_t n_retrievers,
+int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, const double* raw_qpp,
+                            const double* mm, const int64_t* list_off, int32_t norm_mode,
+                            int32_t n_retrievers,
                             const int32_t* run_of_block, int32_t n_blocks, int32_t n_boosters,
                             const int32_t* tree_off, const int32_t* node_off,
                             const int32_t* leaf_off, const int32_t* feature,

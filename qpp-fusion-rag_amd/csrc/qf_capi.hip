@@ -134,14 +134,25 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
                        int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
                        void* perm, int perm32, double* fused, int64_t out_stride,
                        void* stream, const char* fn, uint32_t learned_f32 = 0u,
-                       void* ws = nullptr, size_t ws_bytes = 0) {
+                       void* ws = nullptr, size_t ws_bytes = 0,
+                       const double* qpp_raw = nullptr, const double* qpp_stats = nullptr,
+                       int32_t qpp_mode = 0, int32_t qpp_index = -1) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "%s: n_retrievers must be in [1, %d]", fn, kMaxR);
   if (methods <= 0 ||
       (methods & ~(QF_ALL_METHODS | QF_LEARNED | QF_PROBFUSE | QF_WRRF_MUL)))
     return fail(QF_EINVAL, "%s: bad method mask 0x%x", fn, methods);
-  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_LEARNED | QF_WRRF_MUL)) && !weights)
+  if ((methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_LEARNED | QF_WRRF_MUL)) && !weights &&
+      !qpp_raw)
     return fail(QF_EINVAL, "%s: weighted method requested without weights", fn);
+  if (qpp_raw && (methods & QF_LEARNED))
+    return fail(QF_EINVAL, "%s: QF_LEARNED takes its learned weights, not QPP ones", fn);
+  if (qpp_raw && (qpp_index < -1 || qpp_index >= QF_QPP_COLS ||
+                  (qpp_mode != QF_NORM_NONE && qpp_mode != QF_NORM_MINMAX &&
+                   qpp_mode != QF_NORM_ZSCORE) ||
+                  (qpp_mode != QF_NORM_NONE && !qpp_stats)))
+    return fail(QF_EINVAL, "%s: bad QPP weight arguments (index %d, mode %d)", fn, qpp_index,
+                qpp_mode);
   if ((methods & QF_LEARNED) && (methods & (QF_WCOMBSUM | QF_WCOMBMNZ | QF_WRRF | QF_WRRF_MUL)))
     return fail(QF_EINVAL, "%s: QF_LEARNED and the W-* methods need different weights", fn);
   if ((methods & QF_PROBFUSE) && (!seg_prob || n_seg <= 0 || seg_len <= 0))
@@ -160,6 +171,10 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
                    weights,   methods,      rrf_k,       union_docid, union_count,
                    perm,      fused,        out_stride,  seg_prob,    n_seg, seg_len};
   p.perm32 = perm32;
+  p.qpp_raw = qpp_raw;
+  p.qpp_stats = qpp_stats;
+  p.qpp_mode = qpp_mode;
+  p.qpp_index = qpp_index;
   if (learned_f32) {
     const uint32_t all = n_retrievers == 32 ? 0xFFFFFFFFu : (1u << n_retrievers) - 1u;
     p.learned_f32 = learned_f32 & all;
@@ -187,6 +202,21 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
   return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, weights,
                      methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
                      0, fused, out_stride, stream, "qf_fuse");
+}
+
+int qf_fuse_qpp(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
+                const double* qpp_raw, const double* qpp_stats, int32_t qpp_mode,
+                int32_t qpp_index, int32_t methods, int32_t rrf_k, int32_t max_entries,
+                uint32_t* union_docid, int32_t* union_count, uint16_t* perm, double* fused,
+                int64_t out_stride, void* stream) {
+  if (methods & QF_PROBFUSE)
+    return fail(QF_EINVAL, "qf_fuse_qpp: QF_PROBFUSE needs qf_fuse_probfuse (segment table)");
+  if (n_queries > 0 && !qpp_raw) return fail(QF_EINVAL, "qf_fuse_qpp: null buffer");
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, nullptr,
+                     methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
+                     0, fused, out_stride, stream, "qf_fuse_qpp", 0u, nullptr, 0, qpp_raw,
+                     qpp_stats, qpp_mode, qpp_index);
 }
 
 int64_t qf_fuse_workspace_bytes(int64_t n_queries, int32_t n_retrievers, int32_t max_entries,
@@ -362,7 +392,9 @@ int qf_gbdt_predict(int64_t n_rows, const double* X, int32_t n_features, int32_t
   return check(qf::gbdt_predict_launch(p, (hipStream_t)stream), "qf_gbdt_predict");
 }
 
-int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, int32_t n_retrievers,
+int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, const double* raw_qpp,
+                            const double* mm, const int64_t* list_off, int32_t norm_mode,
+                            int32_t n_retrievers,
                             const int32_t* run_of_block, int32_t n_blocks, int32_t n_boosters,
                             const int32_t* tree_off, const int32_t* node_off,
                             const int32_t* leaf_off, const int32_t* feature,
@@ -392,13 +424,21 @@ int qf_learned_gbdt_weights(int64_t n_queries, const int64_t* micro, int32_t n_r
     f.lw.run_to_booster[r] = run_to_booster[r];
   }
   if (n_queries == 0) return QF_OK;
-  if (!micro || !tree_off || !node_off || !leaf_off || !feature || !threshold ||
-      !decision_type || !left || !right || !leaf_value || !w_out)
+  if (!(micro || (raw_qpp && list_off && (norm_mode == QF_NORM_NONE || mm))) || !tree_off ||
+      !node_off || !leaf_off || !feature || !threshold || !decision_type || !left || !right ||
+      !leaf_value || !w_out)
     return fail(QF_EINVAL, "qf_learned_gbdt_weights: null buffer");
+  if (!micro && norm_mode != QF_NORM_NONE && norm_mode != QF_NORM_MINMAX &&
+      norm_mode != QF_NORM_ZSCORE)
+    return fail(QF_EINVAL, "qf_learned_gbdt_weights: unsupported norm_mode %d", norm_mode);
   f.gbdt = qf::GbdtParams{n_queries, nullptr, n_blocks * QF_QPP_COLS, n_boosters, tree_off,
                           node_off, leaf_off, feature, threshold, decision_type, left, right,
                           leaf_value, pred_out};
   f.micro = micro;
+  f.raw_qpp = raw_qpp;
+  f.mm = mm;
+  f.list_off = list_off;
+  f.norm_mode = norm_mode;
   f.R = n_retrievers;
   f.lw.n_queries = n_queries;
   f.lw.n_boosters = n_boosters;

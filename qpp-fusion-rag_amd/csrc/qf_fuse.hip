@@ -28,6 +28,7 @@
 #include "../../include/qppfuse.h"
 #include "qf_common.h"
 #include "qf_internal.h"
+#include "qf_lists.h"
 
 namespace qf {
 
@@ -74,6 +75,29 @@ struct ScoreIn<1> {
   static __device__ __forceinline__ double val(raw_t r) { return micro_to_f64(r); }
   static __device__ __forceinline__ double load(const void* p, int64_t i) { return val(raw(p, i)); }
 };
+
+// The weight of list (q, r): p.weights, or (qf_fuse_qpp) the .qpp round trip of the
+// raw predictors normalised with the column statistics — qpp_normalize_kernel's
+// w_out bit for bit (src/qpp.py:356-372, src/fusion.py:150-158), computed by the
+// join's per-list threads while the entries' loads are in flight.
+__device__ __forceinline__ double list_weight(const FuseParams& p, int64_t q, int r,
+                                              bool present) {
+  if (!p.qpp_raw) return p.weights ? p.weights[q * p.R + r] : 1.0;
+  const int64_t l = q * p.R + r;
+  const int mode = p.qpp_mode;
+  const double* x = p.qpp_raw + l * kQppCols;
+  const double* m0 = p.qpp_stats + (int64_t)r * kQppCols;
+  const double* m1 = p.qpp_stats + ((int64_t)p.R + r) * kQppCols;
+  auto back = [&](int c) {
+    return micro_back(round6(qpp_norm_value(x[c], mode != 0 ? m0[c] : 0.0,
+                                            mode != 0 ? m1[c] : 0.0, mode, present)));
+  };
+  if (p.qpp_index >= 0) return back(p.qpp_index);
+  double wsum = 0.0;  // Python sum(): left to right
+#pragma unroll
+  for (int c = 0; c < kQppCols; ++c) wsum += back(c);
+  return wsum / (double)kQppCols;
+}
 
 // ---- block-level helpers ------------------------------------------------------
 
@@ -623,7 +647,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     // ranx min-max (norm="min-max", the fuse() default); lists are sorted
     // descending (checked below), so max / min are the end points.  The three
     // loads are issued together (one latency)
-    const double wv = p.weights ? p.weights[q * R + tid] : 1.0;
+    const double wv = list_weight(p, q, tid, b > a);
     double mx = 0.0, mn = 0.0;
     if (b > a) {
       mx = ScoreIn<KIND>::load(p.score, a);
@@ -2416,7 +2440,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   const int N = (int)(s_off[R] - base);  // JoinXL::kNMax < N <= kXlNMax (the lister's test)
   if (tid < R) {  // as the LDS join
     const int64_t a = s_off[tid], b = s_off[tid + 1];
-    s_w[tid] = p.weights ? p.weights[q * R + tid] : 1.0;
+    s_w[tid] = list_weight(p, q, tid, b > a);
     double mx = 0.0, mn = 0.0;
     if (b > a) {
       mx = ScoreIn<KIND>::load(p.score, a);

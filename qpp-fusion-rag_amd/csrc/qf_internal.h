@@ -38,6 +38,12 @@ struct FuseParams {
   uint32_t learned_f32;
   int32_t learned_sum_f32;
   int32_t perm32;  // perm holds uint32 entries (unions above 65,535 documents)
+  // qf_fuse_qpp: the W-* weights from the raw QPP predictors [Q*R][13] and their
+  // column statistics [2][R][13] (QF_NORM_* qpp_mode), column qpp_index (-1: the
+  // mean of the 13) — qf_qpp_normalize's w_out computed in the join; NULL: weights
+  const double* qpp_raw;
+  const double* qpp_stats;
+  int32_t qpp_mode, qpp_index;
 };
 // perm element i (m * out_stride + base + rank): every kernel writes perm through
 // these, so one flag switches a call between the uint16 and uint32 layouts
@@ -112,7 +118,11 @@ struct QppBlocks {
 // nullable: the raw predictions, if wanted).
 struct GbdtFusedParams {
   GbdtParams gbdt;
-  const int64_t* micro;  // [n_rows * R][13] QPP micro-units (qf_qpp_normalize)
+  const int64_t* micro;  // [n_rows * R][13] QPP micro-units (qf_qpp_normalize), or NULL:
+  const double* raw_qpp;   // [n_rows * R][13] raw predictors, normalised on the fly with
+  const double* mm;        // the column statistics (qf_qpp_colminmax / colmeanstd)
+  const int64_t* list_off;  // (absent lists: 0.0)
+  int32_t norm_mode;       // QF_NORM_*
   int32_t R;
   QppBlocks blk;
   LearnedWeightParams lw;  // lw.pred unused; lw.w_out [n_rows][n_runs]

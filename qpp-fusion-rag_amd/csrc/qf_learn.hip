@@ -34,6 +34,7 @@
 #include "../../include/qppfuse.h"
 #include "qf_common.h"
 #include "qf_internal.h"
+#include "qf_lists.h"
 
 namespace qf {
 
@@ -151,8 +152,23 @@ struct RowFromMicro {
     const int j = i / kQppCols, c = i - j * kQppCols;
     const int r = f.blk.run[j];
     if (r < 0) return 0.0;
-    const int64_t m = f.micro[(row * f.R + r) * kQppCols + c];
-    return (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m) : (double)m / 1e6;
+    return micro_back(f.micro[(row * f.R + r) * kQppCols + c]);
+  }
+};
+// ... or normalised from the raw predictors on the fly, as qpp_normalize_kernel
+// does before its micro-units (no normalisation launch in between).
+struct RowFromRaw {
+  const GbdtFusedParams& f;
+  __device__ double operator()(int64_t row, int i) const {
+    const int j = i / kQppCols, c = i - j * kQppCols;
+    const int r = f.blk.run[j];
+    if (r < 0) return 0.0;
+    const int64_t l = row * f.R + r;
+    const bool present = f.list_off[l + 1] > f.list_off[l];
+    const double m0 = f.norm_mode != 0 ? f.mm[r * kQppCols + c] : 0.0;
+    const double m1 = f.norm_mode != 0 ? f.mm[f.R * kQppCols + r * kQppCols + c] : 0.0;
+    return micro_back(round6(qpp_norm_value(f.raw_qpp[l * kQppCols + c], m0, m1, f.norm_mode,
+                                            present)));
   }
 };
 
@@ -258,7 +274,10 @@ __global__ __launch_bounds__(64 * kGbdtWaves) void gbdt_predict_kernel(GbdtParam
 __global__ __launch_bounds__(64 * kGbdtWaves) void learned_gbdt_weights_kernel(GbdtFusedParams f) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[kGbdtLds];
   __shared__ double sleaf[kGbdtWaves][64];
-  gbdt_block(f.gbdt, RowFromMicro{f}, &f.lw, lds, sleaf);
+  if (f.micro)
+    gbdt_block(f.gbdt, RowFromMicro{f}, &f.lw, lds, sleaf);
+  else
+    gbdt_block(f.gbdt, RowFromRaw{f}, &f.lw, lds, sleaf);
 }
 
 __global__ __launch_bounds__(256) void learned_weights_kernel(LearnedWeightParams p) {

@@ -110,4 +110,25 @@ __device__ __forceinline__ void qpp_colminmax_block(const double* __restrict__ r
   }
 }
 
+// One raw QPP value normalised as src/qpp.py:356-372 does — mode 1 (minmax: m0 =
+// the column min, m1 = minus its max), 2 (zscore: m0 = mean, m1 = scale), 0 (none)
+// — and 0.0 for a query whose list is absent (src/qpp.py:321).
+__device__ __forceinline__ double qpp_norm_value(double x, double m0, double m1, int mode,
+                                                 bool present) {
+  double v = x;
+  if (mode == 1) {
+    const double vmin = m0;
+    const double vmax = -m1;
+    const double scale = vmax > vmin ? vmax - vmin : 1.0;
+    v = scale > 0.0 ? (x - vmin) / scale : 0.0;
+  } else if (mode == 2) {  // zscore: mm = [mean, scale] (qpp_colmeanstd)
+    v = (x - m0) / m1;
+  }
+  return present ? v : 0.0;
+}
+// float("%.6f") of the written text: m / 1e6 (division-free where checked exact).
+__device__ __forceinline__ double micro_back(long long m) {
+  return (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m) : (double)m / 1e6;
+}
+
 }  // namespace qf

@@ -535,23 +535,11 @@ __global__ __launch_bounds__(256) void qpp_normalize_kernel(
   double wsum = 0.0, wsel = 0.0;
 #pragma unroll
   for (int c = 0; c < kQppCols; ++c) {
-    const double x = xs[c];
-    double v = x;
-    if (mode == 1) {
-      const double vmin = m0[c];
-      const double vmax = -m1[c];
-      const double scale = vmax > vmin ? vmax - vmin : 1.0;
-      v = scale > 0.0 ? (x - vmin) / scale : 0.0;
-    } else if (mode == 2) {  // zscore: mm = [mean, scale] (qpp_colmeanstd)
-      v = (x - m0[c]) / m1[c];
-    }
-    if (!present) v = 0.0;
+    const double v = qpp_norm_value(xs[c], m0[c], m1[c], mode, present);
     const long long m = round6(v);
     if (norm_out) norm_out[l * kQppCols + c] = v;
     if (micro_out) micro_out[l * kQppCols + c] = m;
-    // float("%.6f") of the written text: m / 1e6 (division-free where checked exact)
-    const double back = (m > -0x7FFFFFFFll && m < 0x7FFFFFFFll) ? micro_to_f64((int32_t)m)
-                                                               : (double)m / 1e6;
+    const double back = micro_back(m);     // the .qpp text read back
     wsum += back;                          // Python sum(): left to right
     if (c == qpp_index) wsel = back;
   }

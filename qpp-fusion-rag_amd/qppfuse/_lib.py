@@ -48,6 +48,8 @@ SIGNATURES = {
     "qf_qpp_features": (C.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "qf_fuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,
                           _vp, _vp, _vp, _vp, _i64, _vp]),
+    "qf_fuse_qpp": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32,
+                              _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_fuse_probfuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp,
                                    _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_fused_topk": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp,
@@ -57,7 +59,8 @@ SIGNATURES = {
     "qf_gbdt_predict": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp]),
     "qf_learned_weights": (C.c_int, [_i64, _vp, _i32, _i32, _vp, _vp, _vp]),
-    "qf_learned_gbdt_weights": (C.c_int, [_i64, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+    "qf_learned_gbdt_weights": (C.c_int, [_i64, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _i32, _i32,
+                                          _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "qf_mlp_weights": (C.c_int, [_i64, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
     "qf_fuse_learned_f32": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, C.c_uint32, _i32,

@@ -114,7 +114,7 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
          out: Optional[FuseOut] = None, seg_prob: Optional[torch.Tensor] = None,
          n_segments: int = 0, seg_len: int = 0,
          learned_f32: Optional[int] = None,
-         workspace: Optional[torch.Tensor] = None) -> FuseOut:
+         workspace: Optional[torch.Tensor] = None, qpp=None) -> FuseOut:
     """qf_fuse over every query of a packed run set (see include/qppfuse.h); with
     "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table;
     methods == ["learned"] with learned_f32 (run bitmask: float32 model weights,
@@ -122,7 +122,11 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
     (65,535) entries takes the _wide entry points (uint32 perm): `out` is then
     allocated wide (alloc_fuse_out(..., wide=True)).  `workspace`: a caller-owned
     device byte buffer for the workspace kernel (qf_fuse_ws; workspace_bytes() sizes
-    it) instead of the library's stream-ordered allocation."""
+    it) instead of the library's stream-ordered allocation.  `qpp` = (raw, stats,
+    mode, qpp_index): the W-* weights from the raw QPP predictors and their column
+    statistics, computed inside the fusion (qf_fuse_qpp — the weights qpp_normalize
+    would give, one launch fewer); for the uint16-perm path without a workspace
+    (other calls normalise first and pass `weights`)."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
@@ -162,6 +166,20 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
                   _ptr(weights), int(learned_f32) & 0xFFFFFFFF, int(max_entries),
                   _ptr(out.union_docid), _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused),
                   out.fused.shape[1], _stream())
+        return out
+    if qpp is not None:
+        raw_qpp, stats, mode, qidx = qpp
+        mode_id = {"none": _lib.NORM_NONE, "minmax": _lib.NORM_MINMAX,
+                   "zscore": _lib.NORM_ZSCORE}[mode]
+        if wide or workspace is not None or weights is not None or mask & _lib.LEARNED:
+            raise ValueError("qpp weights: the uint16-perm fusion without weights / workspace "
+                             "/ learned fusion")
+        if raw_qpp.dtype != torch.float64 or raw_qpp.numel() != Q * R * _lib.QPP_COLS:
+            raise ValueError(f"qpp raw must be float64 [{Q * R}, {_lib.QPP_COLS}]")
+        _lib.call("qf_fuse_qpp", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
+                  _ptr(rank), _ptr(raw_qpp), _ptr(stats), mode_id, int(qidx), mask, int(rrf_k),
+                  int(max_entries), _ptr(out.union_docid), _ptr(out.union_count),
+                  _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], _stream())
         return out
     if workspace is not None:
         if workspace.device != out.fused.device or not workspace.is_contiguous():
@@ -344,24 +362,37 @@ def gbdt_predict(X: torch.Tensor, packed) -> torch.Tensor:
     return out
 
 
-def learned_gbdt_weights(micro: torch.Tensor, n_queries: int, n_retrievers: int, run_of_block,
-                         packed, run_to_booster, want_pred: bool = False):
+def learned_gbdt_weights(micro: Optional[torch.Tensor], n_queries: int, n_retrievers: int,
+                         run_of_block, packed, run_to_booster, want_pred: bool = False,
+                         raw_qpp: Optional[torch.Tensor] = None, mm: Optional[torch.Tensor] = None,
+                         list_off: Optional[torch.Tensor] = None, mode: str = "minmax"):
     """qf_learned_gbdt_weights: qpp_features + gbdt_predict + learned_weights in one
-    launch — [Q * R] run weights (and the raw [Q, B] predictions if want_pred).  For
-    models of up to 19 retrievers (13 features each); bit-identical to the three calls."""
+    launch — [Q * R] run weights (and the raw [Q, B] predictions if want_pred).  The
+    features come from `micro` (qpp_normalize's micro-units) or, with micro None,
+    from raw_qpp normalised on the fly with mm (qpp_colminmax / qpp_colmeanstd) —
+    the normalisation launch folded in.  For models of up to 19 retrievers (13
+    features each); bit-identical to the separate calls."""
     import numpy as np
     dev = require_device()
     Q, R = int(n_queries), int(n_retrievers)
     blocks = np.ascontiguousarray(run_of_block, dtype=np.int32)
     rb = np.ascontiguousarray(run_to_booster, dtype=np.int32)
-    if micro.dtype != torch.int64 or micro.numel() != Q * R * _lib.QPP_COLS:
+    mode_id = {"none": _lib.NORM_NONE, "minmax": _lib.NORM_MINMAX,
+               "zscore": _lib.NORM_ZSCORE}[mode]
+    if micro is None:
+        if raw_qpp is None or list_off is None or (mode_id != _lib.NORM_NONE and mm is None):
+            raise ValueError("raw_qpp, list_off (and mm) are needed without micro")
+        if raw_qpp.dtype != torch.float64 or raw_qpp.numel() != Q * R * _lib.QPP_COLS:
+            raise ValueError(f"raw_qpp must be float64 [{Q * R}, {_lib.QPP_COLS}]")
+    elif micro.dtype != torch.int64 or micro.numel() != Q * R * _lib.QPP_COLS:
         raise ValueError(f"micro must be int64 [{Q * R}, {_lib.QPP_COLS}]")
     if packed.n_features != len(blocks) * _lib.QPP_COLS:
         raise ValueError("the model's features must be 13 per block of run_of_block")
     d = packed.to_device(dev)
     w = torch.empty(Q * len(rb), dtype=torch.float64, device=dev)
     pred = torch.empty((Q, packed.n_boosters), dtype=torch.float64, device=dev) if want_pred else None
-    _lib.call("qf_learned_gbdt_weights", Q, _ptr(micro.contiguous()), R, blocks.ctypes.data,
+    _lib.call("qf_learned_gbdt_weights", Q, _ptr(None if micro is None else micro.contiguous()),
+              _ptr(raw_qpp), _ptr(mm), _ptr(list_off), mode_id, R, blocks.ctypes.data,
               len(blocks), packed.n_boosters, _ptr(d["tree_off"]), _ptr(d["node_off"]),
               _ptr(d["leaf_off"]), _ptr(d["feature"]), _ptr(d["threshold"]), _ptr(d["dtype"]),
               _ptr(d["left"]), _ptr(d["right"]), _ptr(d["leaf_value"]), len(rb), rb.ctypes.data,

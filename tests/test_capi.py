@@ -95,11 +95,26 @@ def test_argument_validation_without_device():
                   kind.ctypes.data, cut.ctypes.data, 8, None)
     with pytest.raises(ValueError, match="qpp_index"):
         _lib.call("qf_qpp_normalize", 1, 1, 1, 1, 1, 1, 13, None, None, None, None)
+    # qf_fuse_qpp's QPP-weight arguments (checked before any device work)
+    W, L = 1 << 3, 1 << 6  # QF_WCOMBSUM, QF_LEARNED
+    fq = lambda raw, stats, mode, idx, methods: (2, 3, 8, 8, 8, 1, None, raw, stats, mode, idx,
+                                                methods, 60, 10, 8, 8, 8, 8, 10, None)
+    with pytest.raises(ValueError, match="QPP weight"):
+        _lib.call("qf_fuse_qpp", *fq(8, 8, 1, 13, W))
+    with pytest.raises(ValueError, match="QPP weight"):
+        _lib.call("qf_fuse_qpp", *fq(8, None, 1, 5, W))   # min-max needs the statistics
+    with pytest.raises(ValueError, match="QPP weight"):
+        _lib.call("qf_fuse_qpp", *fq(8, 8, 7, 5, W))
+    with pytest.raises(ValueError, match="learned"):
+        _lib.call("qf_fuse_qpp", *fq(8, 8, 1, 5, L))
+    with pytest.raises(ValueError, match="null buffer"):
+        _lib.call("qf_fuse_qpp", *fq(None, 8, 1, 5, W))
     # the one-launch learned weights: host-side size and map checks (no device needed)
     blocks = np.array([0, 1, -1], np.int32)
     rb = np.array([0, 1, -1], np.int32)
-    args = lambda nb, nboost, rbp, rblk: (5, 8, 3, rblk.ctypes.data, nb, nboost, 8, 8, 8, 8, 8,
-                                         8, 8, 8, 8, 3, rbp.ctypes.data, None, 8, None)
+    args = lambda nb, nboost, rbp, rblk: (5, 8, None, None, None, 0, 3, rblk.ctypes.data, nb,
+                                         nboost, 8, 8, 8, 8, 8, 8, 8, 8, 8, 3, rbp.ctypes.data,
+                                         None, 8, None)
     with pytest.raises(ValueError, match="bad sizes"):
         _lib.call("qf_learned_gbdt_weights", *args(20, 3, rb, blocks))  # 20 x 13 > 256 features
     with pytest.raises(ValueError, match="bad sizes"):
@@ -109,8 +124,8 @@ def test_argument_validation_without_device():
     with pytest.raises(ValueError, match="run_to_booster"):
         _lib.call("qf_learned_gbdt_weights", *args(3, 3, np.array([0, 3, 1], np.int32), blocks))
     with pytest.raises(ValueError, match="null buffer"):
-        _lib.call("qf_learned_gbdt_weights", 5, None, 3, blocks.ctypes.data, 3, 3, 8, 8, 8, 8, 8,
-                  8, 8, 8, 8, 3, rb.ctypes.data, None, 8, None)
+        _lib.call("qf_learned_gbdt_weights", 5, None, 8, None, None, 1, 3, blocks.ctypes.data, 3,
+                  3, 8, 8, 8, 8, 8, 8, 8, 8, 8, 3, rb.ctypes.data, None, 8, None)
 
 
 def test_product_has_no_cpu_fallback(monkeypatch):

@@ -794,3 +794,46 @@ def test_caller_owned_workspace(gpu, share):
             b, n = off[q * R], uc[q]
             np.testing.assert_array_equal(perm[m, b:b + n], o_perm[b:b + n], err_msg=name)
             assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
+
+
+@pytest.mark.parametrize("mode,qidx", [("minmax", 5), ("minmax", -1), ("minmax", 0),
+                                       ("zscore", 5), ("zscore", -1)])
+def test_fuse_qpp_weights_in_kernel_equal_normalize_then_fuse(gpu, mode, qidx):
+    """qf_fuse_qpp (the W-* weights computed in the join from the raw QPP predictors
+    and their column statistics) == qf_qpp_normalize's weights fed to qf_fuse, bit
+    for bit: union sizes, every method's fused scores and perm; absent lists (weight
+    from a 0.0 value), a constant QPP column."""
+    from qppfuse import engine
+    Q, R, K = 300, 5, 400
+    off, docid, raw = engine.synth_runs(11, Q, R, K)
+    lens = torch.diff(off).cpu().numpy()
+    # empty some lists: rebuild the run set without their entries
+    drop = np.zeros(Q * R, bool)
+    drop[[3, 17, 18, 250]] = True
+    keep = np.repeat(~drop, lens)
+    off_h = off.cpu().numpy()
+    n2 = np.where(drop, 0, lens)
+    off2 = torch.from_numpy(np.concatenate([[0], np.cumsum(n2)]).astype(np.int64)).to(gpu)
+    kt = torch.from_numpy(keep).to(gpu)
+    docid2, raw2 = docid[kt].contiguous(), raw[kt].contiguous()
+    _, micro = engine.minmax_per_query(raw2, off2, want_norm=False)
+    nt = torch.full((Q,), 3, dtype=torch.int32, device=gpu)
+    tf = torch.rand((Q, 2), dtype=torch.float64, device=gpu,
+                    generator=torch.Generator(gpu).manual_seed(2))
+    qraw = engine.qpp_raw(raw2, off2, R, 100, nt, tf)
+    qraw[:, 7] = 0.75  # a constant column
+    stats = (engine.qpp_colminmax if mode == "minmax" else engine.qpp_colmeanstd)(qraw, off2, R)
+    w = engine.qpp_normalize(qraw, stats, off2, R, mode, qidx, want_micro=False)["weights"]
+    M = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
+    a = engine.fuse(off2, docid2, micro, R, M, 60, weights=w, max_entries=R * K)
+    b = engine.fuse(off2, docid2, micro, R, M, 60, max_entries=R * K,
+                    qpp=(qraw, stats, mode, qidx))
+    assert torch.equal(a.union_count, b.union_count)
+    uc = a.union_count.cpu().numpy()
+    fa, fb = a.fused.cpu().numpy(), b.fused.cpu().numpy()
+    pa, pb = a.perm.cpu().numpy(), b.perm.cpu().numpy()
+    lo = off2.cpu().numpy()
+    for q in range(Q):
+        s, u = int(lo[q * R]), int(uc[q])
+        assert fa[:, s:s + u].tobytes() == fb[:, s:s + u].tobytes(), q
+        assert np.array_equal(pa[:, s:s + u], pb[:, s:s + u]), q

@@ -111,6 +111,35 @@ def test_learned_gbdt_weights_one_launch_equals_three(gpu, name):
                        .view(torch.int64), w3.view(torch.int64))
 
 
+@pytest.mark.parametrize("mode", ["minmax", "zscore"])
+def test_learned_gbdt_weights_from_raw_qpp(gpu, mode):
+    """The one-launch learned weights fed the RAW predictors + column statistics
+    (the normalisation folded in) == qpp_normalize's micro-units -> features ->
+    GBDT -> weights, bit for bit; absent lists normalise to 0.0."""
+    from qppfuse import engine, lgbm
+    m = _model("fusion_multioutput")
+    p = lgbm.pack_model(m)
+    rng = np.random.default_rng(17)
+    Q, R = 613, 5
+    raw = rng.gamma(2, 3, (Q * R, 13))
+    raw[:, 6] = 2.5                              # a constant column
+    n = rng.integers(0, 4, Q * R)
+    n[[1, 2, 40]] = 0                            # absent lists
+    off = np.zeros(Q * R + 1, np.int64)
+    off[1:] = np.cumsum(n)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    graw, goff = t(raw), t(off)
+    stats = (engine.qpp_colminmax if mode == "minmax" else engine.qpp_colmeanstd)(graw, goff, R)
+    micro = engine.qpp_normalize(graw, stats, goff, R, mode, 5, want_micro=True,
+                                 want_weights=False)["micro"]
+    blocks = list(range(len(m.retrievers)))
+    rb = [0, 1, 2, 3, 4]
+    want = engine.learned_gbdt_weights(micro, Q, R, blocks, p, rb)
+    got = engine.learned_gbdt_weights(None, Q, R, blocks, p, rb, raw_qpp=graw, mm=stats,
+                                      list_off=goff, mode=mode)
+    assert torch.equal(got.view(torch.int64), want.view(torch.int64))
+
+
 def test_learned_weights_match_numpy(gpu):
     from qppfuse import engine
     rng = np.random.default_rng(3)
