@@ -217,7 +217,9 @@ int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
  * (-1: the mean of the 13) — the weights qf_qpp_normalize's w_out would hold, bit
  * for bit, computed inside the fusion (src/qpp.py:356-372 + the .qpp round trip of
  * get_qpp_weight, src/fusion.py:116-158): one launch fewer per batch.  Not with
- * QF_LEARNED.
+ * QF_LEARNED.  Meant for one column: qpp_index -1 puts 13 normalisations per list
+ * on the start of every query's workgroup (C4: slower than qf_qpp_normalize +
+ * qf_fuse).
  */
 int qf_fuse_qpp(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
                 const uint32_t* docid, const void* score, int32_t score_kind, const int32_t* rank,
