@@ -165,7 +165,7 @@ def _copy(res):
     return [(d.numpy().copy(), s.numpy().copy()) for d, s in res]
 
 
-@pytest.mark.parametrize("world,total", [(4, 11157), (2, 10)])
+@pytest.mark.parametrize("world,total", [(4, 11157), (2, 10), (8, 1000)])
 def test_topk_gather_preallocated_unequal_shards(world, total):
     """dist.TopkGather (bench.py's allocation-free N > 1 gather) with C4's unequal
     shard_range(11157, 4, r) shards (2790, 2789, 2789, 2789) on gloo, world 4:
