@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
         const double v = s_x[lane][j];
         if (j < kl && ((fm >> j) & 1ull)) kahan_add(kf, v);
       }
-      mf = kahan_final(kf) / (double)nf;
+      mf = div_int(kahan_final(kf), nf);
     }
     s_mf[lane] = mf;
   }
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
         const double dv = s_x[lane][j] - mf;
         if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
       }
-      sigmax = sqrt(kahan_final(kfv) / (double)nf);
+      sigmax = sqrt(div_int(kahan_final(kfv), nf));
     }
     s_sigmax[lane] = sigmax;
   }
@@ -322,19 +322,19 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   const double cum = s_res[w][0], smv = s_res[w][1], wig = s_res[w][2], skew = s_res[w][3];
   const double snqc = s_res[w][4], util = s_res[w][5];
   const double sigmax = s_sigmax[w];
-  const double cumnqc = k < 2 ? 0.0 : cum / (double)(k - 1);
+  const double cumnqc = k < 2 ? 0.0 : div_int(cum, k - 1);
   double res[kQppCols];
   res[0] = nqc;
-  res[1] = smv / (double)k;
-  res[2] = wig / (double)(numTerms * k);
+  res[1] = div_int(smv, k);
+  res[2] = div_int(wig, numTerms * k);
   res[3] = sigmamax;
   res[4] = sigmax;
-  res[5] = (k < 3 || std_full < 1e-10) ? 0.0 : skew / (double)k;
+  res[5] = (k < 3 || std_full < 1e-10) ? 0.0 : div_int(skew, k);
   res[6] = util / wsum;
   res[7] = tf0;
   res[8] = tf1;
   res[9] = cumnqc;
-  res[10] = mu <= 0.0 ? 0.0 : snqc / (double)k;
+  res[10] = mu <= 0.0 ? 0.0 : div_int(snqc, k);
   const double range = mx - mn;
   res[11] = (k < 2 || !(range > 0.0)) ? 0.0 : log(1.0 + 1.0 / range);
   res[12] = res[11];
