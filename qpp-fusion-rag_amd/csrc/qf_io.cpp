@@ -266,9 +266,14 @@ struct Cols {
 };
 
 // Parse [begin, end) of a mapped file (whole lines) into rows o, o+1, ...;
-// returns the number of rows whose score is not an exact 6-decimal number.
+// micro_bad_out: the number of rows whose score is not an exact 6-decimal number.
+// The count is kept in a local and stored once: the per-chunk counters sit side by
+// side in one vector, and a per-row store to them (the compiler must store it, the
+// row columns may alias a size_t) made the threads fight over those cache lines —
+// the parse ran 1.6x faster on 8 threads than on 1 (4x after the fix).
 bool parse_chunk(const char* p, const char* end, const char* map_end, Cols& c, Heads& h,
-                 size_t o, size_t& micro_bad, std::string& err) {
+                 size_t o, size_t& micro_bad_out, std::string& err) {
+  size_t micro_bad = 0;
   std::string_view pq, pit, ptag;  // the previous row's (a chunk's first row is a head)
   bool first = true;
   while (p < end) {
@@ -341,6 +346,7 @@ bool parse_chunk(const char* p, const char* end, const char* map_end, Cols& c, H
     micro_bad += !mok;
     ++o;
   }
+  micro_bad_out = micro_bad;
   return true;
 }
 
@@ -354,16 +360,24 @@ struct Key {
   uint64_t k1, k2;
   uint32_t u;
 };
-inline Key make_key(std::string_view v, uint32_t u) {
+inline void key16(std::string_view v, uint64_t& k1, uint64_t& k2) {
   unsigned char b[16] = {0};
   memcpy(b, v.data(), std::min<size_t>(16, v.size()));
-  uint64_t k1 = 0, k2 = 0;
-  for (int i = 0; i < 8; ++i) {
-    k1 = (k1 << 8) | b[i];
-    k2 = (k2 << 8) | b[8 + i];
-  }
-  return Key{k1, k2, u};
+  uint64_t w1, w2;
+  memcpy(&w1, b, 8);
+  memcpy(&w2, b + 8, 8);
+  k1 = __builtin_bswap64(w1);
+  k2 = __builtin_bswap64(w2);
 }
+// a row on its way to the dedupe, and a distinct string found there
+struct PartEnt {
+  uint64_t h;
+  uint32_t row, len;
+};
+struct Rep {
+  uint64_t h, k1, k2;
+  uint32_t len, row;
+};
 
 // hs_in: the strings' hash_sv values when the caller has them (the parse's)
 template <class Views>
@@ -397,16 +411,21 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     size_t o = start[b];
     for (int t = 0; t < T; ++t) { at[t][b] = o; o += cnt[t][b]; }
   }
-  RawArray<uint32_t> rows;  // uninitialised: the scatter writes every element
-  rows.resize(n);
+  // Each row goes to its partition as (hash, row, length): the dedupe then streams
+  // its partition's hashes instead of fetching them at random, and keeps, per
+  // distinct string, its hash, length and first 16 bytes (the sort key) beside the
+  // probe table — a repeat of a string of <= 16 bytes is recognised from those
+  // alone, without touching the first occurrence's row or text.  (Was: row indices
+  // only, and every probe hit compared the strings through both rows' views.)
+  RawArray<PartEnt> ents;  // uninitialised: the scatter writes every element
+  ents.resize(n);
 #pragma omp parallel for schedule(static)
   for (int t = 0; t < T; ++t)
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) rows[at[t][hs[i] >> 56]++] = (uint32_t)i;
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i)
+      ents[at[t][hs[i] >> 56]++] = PartEnt{hs[i], (uint32_t)i, (uint32_t)sv(views[i]).size()};
   tm.mark("  hash+partition");
-  // per partition: open-addressing table of first rows -> local unique index; each
-  // new distinct string's sort key is made while its bytes are in cache
-  std::vector<std::vector<uint32_t>> ufirst(P);  // first row of each distinct string
-  std::vector<std::vector<Key>> ukey(P);
+  // per partition: open-addressing table -> local unique index
+  std::vector<std::vector<Rep>> urep(P);
   RawArray<uint32_t> local;
   local.resize(n);
 #pragma omp parallel for schedule(dynamic, 4)
@@ -416,38 +435,42 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     size_t cap = 16;
     while (cap < 2 * m) cap <<= 1;
     std::vector<uint32_t> tab(cap, 0xFFFFFFFFu);
-    auto& uf = ufirst[b];
-    auto& uk = ukey[b];
-    uf.reserve(m);  // at most m distinct: no regrowth copies
-    uk.reserve(m);
+    // built locally and moved in at the end (the vector headers in urep share
+    // cache lines with the neighbouring partitions')
+    std::vector<Rep> rep;
+    rep.reserve(m);  // at most m distinct: no regrowth copies
     for (size_t k = a0; k < a1; ++k) {
-      // the partition's rows are scattered over the columns and the text: their
-      // hash and view prefetched 16 rows ahead, the text 8 rows ahead
-      if (k + 16 < a1) {
-        __builtin_prefetch(&hs[rows[k + 16]]);
-        __builtin_prefetch(&views[rows[k + 16]]);
-      }
-      if (k + 8 < a1) __builtin_prefetch(sv(views[rows[k + 8]]).data());
-      const uint32_t i = rows[k];
-      size_t h = (size_t)hs[i] & (cap - 1);
+      // the rows' views and text are scattered: the view prefetched 16 entries
+      // ahead, the text 8 ahead
+      if (k + 16 < a1) __builtin_prefetch(&views[ents[k + 16].row]);
+      if (k + 8 < a1) __builtin_prefetch(sv(views[ents[k + 8].row]).data());
+      const PartEnt e = ents[k];
+      const std::string_view v = sv(views[e.row]);
+      uint64_t k1, k2;
+      key16(v, k1, k2);
+      size_t h = (size_t)e.h & (cap - 1);
       while (true) {
         const uint32_t u = tab[h];
         if (u == 0xFFFFFFFFu) {
-          tab[h] = (uint32_t)uf.size();
-          local[i] = (uint32_t)uf.size();
-          uk.push_back(make_key(sv(views[i]), (uint32_t)uf.size()));  // u: local for now
-          uf.push_back(i);
+          tab[h] = (uint32_t)rep.size();
+          local[e.row] = (uint32_t)rep.size();
+          rep.push_back(Rep{e.h, k1, k2, e.len, e.row});
           break;
         }
-        const uint32_t r = uf[u];
-        if (hs[r] == hs[i] && sv(views[r]) == sv(views[i])) { local[i] = u; break; }
+        const Rep& r = rep[u];
+        if (r.h == e.h && r.len == e.len && r.k1 == k1 && r.k2 == k2 &&
+            (e.len <= 16 || memcmp(sv(views[r.row]).data() + 16, v.data() + 16, e.len - 16) == 0)) {
+          local[e.row] = u;
+          break;
+        }
         h = (h + 1) & (cap - 1);
       }
     }
+    urep[b] = std::move(rep);
   }
   tm.mark("  dedupe");
   std::vector<size_t> ubase(P + 1, 0);
-  for (int b = 0; b < P; ++b) ubase[b + 1] = ubase[b] + ufirst[b].size();
+  for (int b = 0; b < P; ++b) ubase[b + 1] = ubase[b] + urep[b].size();
   const size_t U = ubase[P];
   RawArray<uint32_t> reps;  // row of each distinct string
   RawArray<Key> keys;
@@ -456,11 +479,10 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   // Sort the distinct strings by byte order (== Python's str order for UTF-8).
 #pragma omp parallel for schedule(dynamic, 4)
   for (int b = 0; b < P; ++b) {
-    std::copy(ufirst[b].begin(), ufirst[b].end(), reps.data() + ubase[b]);
-    Key* kd = keys.data() + ubase[b];
-    for (size_t j = 0; j < ukey[b].size(); ++j) {
-      kd[j] = ukey[b][j];
-      kd[j].u += (uint32_t)ubase[b];
+    const std::vector<Rep>& rep = urep[b];
+    for (size_t j = 0; j < rep.size(); ++j) {
+      reps[ubase[b] + j] = rep[j].row;
+      keys[ubase[b] + j] = Key{rep[j].k1, rep[j].k2, (uint32_t)(ubase[b] + j)};
     }
   }
   auto less = [&](const Key& a, const Key& b) {
@@ -1227,7 +1249,7 @@ int qfio_read_score_lists(const char* path, int32_t top_k, int32_t n_threads,
   std::vector<Chunk> ch((size_t)T);
 #pragma omp parallel for schedule(static, 1)
   for (int t = 0; t < T; ++t) {
-    Chunk& c = ch[(size_t)t];
+    Chunk c;  // local, moved into ch[t] at the end: the Chunk headers share cache lines
     c.score.reserve((size_t)(cut[t + 1] - cut[t]) / 32 + 16);
     const char* p = cut[t];
     const char* end = cut[t + 1];
@@ -1272,6 +1294,7 @@ int qfio_read_score_lists(const char* path, int32_t top_k, int32_t n_threads,
       ++c.run_len.back();
       c.score.push_back(v);
     }
+    ch[(size_t)t] = std::move(c);
   }
   for (int t = 0; t < T; ++t) {  // the first failing chunk in file order decides
     if (ch[(size_t)t].code == 1) return fail(QFIO_EPARSE, ch[(size_t)t].err);

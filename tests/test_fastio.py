@@ -96,6 +96,37 @@ def test_threads_do_not_change_the_result(tmp_path):
     np.testing.assert_array_equal(a.list_off, b.list_off)
 
 
+@pytest.mark.parametrize("threads", [1, 5])
+def test_docnos_sharing_their_first_16_bytes(tmp_path, threads):
+    """The interning recognises a repeat from (hash, length, first 16 bytes) and
+    compares only the bytes past 16 for longer strings: docnos of 15-40 bytes that
+    share 16-byte prefixes, differ in one late byte or only in length, and repeat
+    across runs and queries must intern exactly as pack_frames does."""
+    rng = np.random.default_rng(7)
+    pre = ["abcdefghijklmnop", "abcdefghijklmnoq", "abcdefghijklmno"]
+    pool = []
+    for a in pre:
+        pool += [a, a + "x", a + "xy", a + "y"]
+        pool += [a + f"-{i:020d}" for i in range(40)]
+        pool += [a + f"-{i:020d}z" for i in range(0, 40, 3)]
+    names, paths = [], []
+    for r in range(3):
+        lines = []
+        for q in range(25):
+            docs = rng.choice(len(pool), size=int(rng.integers(1, 60)), replace=False)
+            for i, d in enumerate(docs):
+                lines.append(f"q{q} Q0 {pool[d]} {i + 1} {1.0 - i / 100:.6f} t{r}\n")
+        pth = tmp_path / f"R{r}.norm.res"
+        pth.write_text("".join(lines))
+        names.append(f"R{r}")
+        paths.append(str(pth))
+    rs, _ = fastio.parse_runs(paths, names, n_threads=threads)
+    ref = pack_frames(_pandas_frames(paths, names))
+    assert list(rs.docnos) == list(ref.docnos)
+    np.testing.assert_array_equal(rs.docid, ref.docid)
+    np.testing.assert_array_equal(rs.list_off, ref.list_off)
+
+
 def test_parse_errors(tmp_path):
     p = tmp_path / "bad.res"
     p.write_text("q1 Q0 d1 1 0.5 t\nq1 Q0 d2 2 t\n")
