@@ -116,12 +116,36 @@ struct RawArray {
     a = (T*)malloc(bytes);
     if (!a) throw std::bad_alloc();
   }
+  // hands a mapped buffer to `bin` (to be unmapped later), frees a small one now
+  void release_to(std::vector<std::pair<void*, size_t>>& bin) {
+    if (a && mapped) bin.emplace_back((void*)a, bytes);
+    else free(a);
+    a = nullptr;
+    n = bytes = 0;
+    mapped = false;
+  }
   size_t size() const { return n; }
   T& operator[](size_t i) { return a[i]; }
   const T& operator[](size_t i) const { return a[i]; }
   T* data() { return a; }
   const T* data() const { return a; }
 };
+
+// Gives back the buffers of large temporaries on a thread of its own: freeing a few
+// hundred MB of touched pages costs tens of ms that need not be on the caller's
+// path.  The pages go first (madvise takes the address-space lock shared, so the
+// caller's page faults proceed meanwhile); the munmap, which takes it exclusively,
+// then has nothing left to free.
+template <class... A>
+void release_async(A&... arrays) {
+  auto* bin = new std::vector<std::pair<void*, size_t>>();
+  (arrays.release_to(*bin), ...);
+  std::thread([bin] {
+    for (auto& m : *bin) madvise(m.first, m.second, MADV_DONTNEED);
+    for (auto& m : *bin) munmap(m.first, m.second);
+    delete bin;
+  }).detach();
+}
 
 // A string view that is trivially constructible (rows of the column buffers).
 struct SV {
@@ -385,7 +409,10 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
             const uint64_t* hs_in = nullptr) {
   PhaseTimer tm;
   const size_t n = views.size();
-  constexpr int P = 256;
+  // hash partitions: 4,096 for large sets (a partition's probe table and distinct
+  // strings — ~4 K rows, ~2 K strings for C2's 17 M docnos — stay in the core's
+  // cache during its dedupe), 256 for small ones (the run heads)
+  const int PB = n >= ((size_t)1 << 22) ? 12 : 8, P = 1 << PB, PS = 64 - PB;
   RawArray<uint64_t> hs_own;
   const uint64_t* hs = hs_in;
   if (!hs) {
@@ -399,7 +426,7 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   std::vector<std::vector<uint32_t>> cnt(T, std::vector<uint32_t>(P, 0));
 #pragma omp parallel for schedule(static)
   for (int t = 0; t < T; ++t)
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) ++cnt[t][hs[i] >> 56];
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) ++cnt[t][hs[i] >> PS];
   std::vector<size_t> start(P + 1, 0);
   for (int b = 0; b < P; ++b) {
     size_t s = 0;
@@ -422,7 +449,7 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
 #pragma omp parallel for schedule(static)
   for (int t = 0; t < T; ++t)
     for (size_t i = n * t / T; i < n * (t + 1) / T; ++i)
-      ents[at[t][hs[i] >> 56]++] = PartEnt{hs[i], (uint32_t)i, (uint32_t)sv(views[i]).size()};
+      ents[at[t][hs[i] >> PS]++] = PartEnt{hs[i], (uint32_t)i, (uint32_t)sv(views[i]).size()};
   tm.mark("  hash+partition");
   // per partition: open-addressing table -> local unique index
   std::vector<std::vector<Rep>> urep(P);
@@ -508,10 +535,11 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   id.resize(n);
 #pragma omp parallel for schedule(static)
   for (size_t i = 0; i < n; ++i) {
-    if (i + 16 < n) __builtin_prefetch(&rank[ubase[hs[i + 16] >> 56] + local[i + 16]]);
-    id[i] = rank[ubase[hs[i] >> 56] + local[i]];
+    if (i + 16 < n) __builtin_prefetch(&rank[ubase[hs[i + 16] >> PS] + local[i + 16]]);
+    id[i] = rank[ubase[hs[i] >> PS] + local[i]];
   }
   tm.mark("  ranks");
+  release_async(hs_own, ents, local, reps, keys, rank);
 }
 
 // intern() for columns made of long runs of one value (qid, Q0, tag): only the
@@ -745,6 +773,7 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   // the per-row views (~1 GB for C2) are released on a thread of their own:
   // unmapping them is not on the caller's path
   std::thread([c = new Cols(std::move(cols))] { delete c; }).detach();
+  release_async(row_micro);
   tm.mark("release columns");
   *out = rs;
   return QFIO_OK;
