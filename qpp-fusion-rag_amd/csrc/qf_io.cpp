@@ -395,7 +395,7 @@ inline void key16(std::string_view v, uint64_t& k1, uint64_t& k2) {
 }
 // a row on its way to the dedupe, and a distinct string found there
 struct PartEnt {
-  uint64_t h;
+  uint64_t h, k1, k2;
   uint32_t row, len;
 };
 struct Rep {
@@ -438,18 +438,22 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     size_t o = start[b];
     for (int t = 0; t < T; ++t) { at[t][b] = o; o += cnt[t][b]; }
   }
-  // Each row goes to its partition as (hash, row, length): the dedupe then streams
-  // its partition's hashes instead of fetching them at random, and keeps, per
-  // distinct string, its hash, length and first 16 bytes (the sort key) beside the
-  // probe table — a repeat of a string of <= 16 bytes is recognised from those
-  // alone, without touching the first occurrence's row or text.  (Was: row indices
-  // only, and every probe hit compared the strings through both rows' views.)
+  // Each row goes to its partition as (hash, first 16 bytes, row, length), read
+  // here in row order (the text sequentially): the dedupe then streams its
+  // partition and keeps, per distinct string, the same fields beside the probe
+  // table — a string of <= 16 bytes is recognised from them alone, without
+  // touching any row's view or text at random.  (Was: row indices only; every probe
+  // fetched the row's hash, view and text, and every hit the first occurrence's.)
   RawArray<PartEnt> ents;  // uninitialised: the scatter writes every element
   ents.resize(n);
 #pragma omp parallel for schedule(static)
   for (int t = 0; t < T; ++t)
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i)
-      ents[at[t][hs[i] >> PS]++] = PartEnt{hs[i], (uint32_t)i, (uint32_t)sv(views[i]).size()};
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+      const std::string_view v = sv(views[i]);
+      uint64_t k1, k2;
+      key16(v, k1, k2);
+      ents[at[t][hs[i] >> PS]++] = PartEnt{hs[i], k1, k2, (uint32_t)i, (uint32_t)v.size()};
+    }
   tm.mark("  hash+partition");
   // per partition: open-addressing table -> local unique index
   std::vector<std::vector<Rep>> urep(P);
@@ -467,26 +471,20 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
     std::vector<Rep> rep;
     rep.reserve(m);  // at most m distinct: no regrowth copies
     for (size_t k = a0; k < a1; ++k) {
-      // the rows' views and text are scattered: the view prefetched 16 entries
-      // ahead, the text 8 ahead
-      if (k + 16 < a1) __builtin_prefetch(&views[ents[k + 16].row]);
-      if (k + 8 < a1) __builtin_prefetch(sv(views[ents[k + 8].row]).data());
       const PartEnt e = ents[k];
-      const std::string_view v = sv(views[e.row]);
-      uint64_t k1, k2;
-      key16(v, k1, k2);
       size_t h = (size_t)e.h & (cap - 1);
       while (true) {
         const uint32_t u = tab[h];
         if (u == 0xFFFFFFFFu) {
           tab[h] = (uint32_t)rep.size();
           local[e.row] = (uint32_t)rep.size();
-          rep.push_back(Rep{e.h, k1, k2, e.len, e.row});
+          rep.push_back(Rep{e.h, e.k1, e.k2, e.len, e.row});
           break;
         }
         const Rep& r = rep[u];
-        if (r.h == e.h && r.len == e.len && r.k1 == k1 && r.k2 == k2 &&
-            (e.len <= 16 || memcmp(sv(views[r.row]).data() + 16, v.data() + 16, e.len - 16) == 0)) {
+        if (r.h == e.h && r.len == e.len && r.k1 == e.k1 && r.k2 == e.k2 &&
+            (e.len <= 16 || memcmp(sv(views[r.row]).data() + 16, sv(views[e.row]).data() + 16,
+                                   e.len - 16) == 0)) {
           local[e.row] = u;
           break;
         }
@@ -770,10 +768,8 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
   rs->canonical = not_canon == 0;
   rs->has_dups = dups != 0;
   tm.mark("csr");
-  // the per-row views (~1 GB for C2) are released on a thread of their own:
-  // unmapping them is not on the caller's path
-  std::thread([c = new Cols(std::move(cols))] { delete c; }).detach();
-  release_async(row_micro);
+  // the per-row views and hashes (~0.4 GB for C2) go on a thread of their own
+  release_async(cols.d, cols.dh, cols.rank, cols.score, cols.micro, row_micro);
   tm.mark("release columns");
   *out = rs;
   return QFIO_OK;
