@@ -125,6 +125,8 @@ struct RawArray {
     mapped = false;
   }
   size_t size() const { return n; }
+  const T* begin() const { return a; }
+  const T* end() const { return a + n; }
   T& operator[](size_t i) { return a[i]; }
   const T& operator[](size_t i) const { return a[i]; }
   T* data() { return a; }
@@ -405,7 +407,7 @@ struct Rep {
 
 // hs_in: the strings' hash_sv values when the caller has them (the parse's)
 template <class Views>
-void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<uint32_t>& id,
+void intern(const Views& views, RawArray<SV>& uniq, RawArray<uint32_t>& id,
             const uint64_t* hs_in = nullptr) {
   PhaseTimer tm;
   const size_t n = views.size();
@@ -528,7 +530,8 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
   for (size_t k = 0; k < U; ++k) {
     if (k + 16 < U) __builtin_prefetch(&views[reps[keys[k + 16].u]]);
     rank[keys[k].u] = (uint32_t)k;
-    uniq[k] = sv(views[reps[keys[k].u]]);
+    const std::string_view v = sv(views[reps[keys[k].u]]);
+    uniq[k] = SV{v.data(), v.size()};
   }
   id.resize(n);
 #pragma omp parallel for schedule(static)
@@ -545,7 +548,7 @@ void intern(const Views& views, std::vector<std::string_view>& uniq, RawArray<ui
 // costs one more string), then every row takes its run's id.
 // head_rows / head_ids (optional): the runs (first row, id), in row order.
 void intern_runs(const std::vector<Heads>& heads, std::vector<Head> Heads::*which, size_t n,
-                 std::vector<std::string_view>& uniq, RawArray<uint32_t>& id,
+                 RawArray<SV>& uniq, RawArray<uint32_t>& id,
                  std::vector<size_t>* head_rows = nullptr, RawArray<uint32_t>* head_ids = nullptr) {
   std::vector<size_t> hix;
   std::vector<std::string_view> hv;
@@ -575,7 +578,9 @@ void intern_runs(const std::vector<Heads>& heads, std::vector<Head> Heads::*whic
 struct qfio_runset {
   std::vector<Mapped*> maps;
   int32_t n_files = 0;
-  std::vector<std::string_view> qids, docnos, iters, tags;
+  // the distinct strings in byte order (views into the mapped files; RawArrays:
+  // no serial zero-fill of C2's 8.6 M docno views)
+  RawArray<SV> qids, docnos, iters, tags;
   // CSR (query-major, run-minor), rows in file order
   std::vector<int64_t> list_off;
   RawArray<uint32_t> docid;
@@ -777,10 +782,10 @@ int qfio_load_runs(const char* const* paths, int32_t n_files, int32_t n_threads,
 
 void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes /* [8] */) {
   int64_t qb = 0, db = 0, ib = 0, tb = 0;
-  for (auto& s : rs->qids) qb += (int64_t)s.size();
-  for (auto& s : rs->docnos) db += (int64_t)s.size();
-  for (auto& s : rs->iters) ib += (int64_t)s.size();
-  for (auto& s : rs->tags) tb += (int64_t)s.size();
+  for (auto& s : rs->qids) qb += (int64_t)s.n;
+  for (auto& s : rs->docnos) db += (int64_t)s.n;
+  for (auto& s : rs->iters) ib += (int64_t)s.n;
+  for (auto& s : rs->tags) tb += (int64_t)s.n;
   sizes[0] = (int64_t)rs->qids.size();
   sizes[1] = (int64_t)rs->docnos.size();
   sizes[2] = (int64_t)rs->docid.size();
@@ -792,18 +797,18 @@ void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes /* [8] */) {
   sizes[7] = ib | (tb << 32);
 }
 
-static void copy_strings(const std::vector<std::string_view>& v, int64_t* off, char* chars) {
+static void copy_strings(const RawArray<SV>& v, int64_t* off, char* chars) {
   int64_t o = 0;
   off[0] = 0;
   for (size_t i = 0; i < v.size(); ++i) {
-    o += (int64_t)v[i].size();
+    o += (int64_t)v[i].n;
     off[i + 1] = o;
   }
   // the bytes in parallel: the views point all over the mapped files
 #pragma omp parallel for schedule(static, 4096)
   for (int64_t i = 0; i < (int64_t)v.size(); ++i) {
-    if (i + 8 < (int64_t)v.size()) __builtin_prefetch(v[i + 8].data());
-    memcpy(chars + off[i], v[i].data(), v[i].size());
+    if (i + 8 < (int64_t)v.size()) __builtin_prefetch(v[i + 8].p);
+    memcpy(chars + off[i], v[i].p, v[i].n);
   }
 }
 
@@ -852,10 +857,10 @@ int qfio_runset_rows(const qfio_runset* rs, int64_t* file_off, uint32_t* qid, ui
 }
 
 void qfio_runset_drop_text(qfio_runset* rs) {
-  std::vector<std::string_view>().swap(rs->qids);
-  std::vector<std::string_view>().swap(rs->docnos);
-  std::vector<std::string_view>().swap(rs->iters);
-  std::vector<std::string_view>().swap(rs->tags);
+  rs->qids.release();
+  rs->docnos.release();
+  rs->iters.release();
+  rs->tags.release();
   for (auto* m : rs->maps) delete m;
   rs->maps.clear();
 }
