@@ -798,11 +798,26 @@ void qfio_runset_sizes(const qfio_runset* rs, int64_t* sizes /* [8] */) {
 }
 
 static void copy_strings(const RawArray<SV>& v, int64_t* off, char* chars) {
-  int64_t o = 0;
+  // offsets: a blocked parallel scan (the 69 MB of C2's docno offsets are fresh pages)
+  const int64_t n = (int64_t)v.size();
   off[0] = 0;
-  for (size_t i = 0; i < v.size(); ++i) {
-    o += (int64_t)v[i].n;
-    off[i + 1] = o;
+  const int T = std::max(1, omp_get_max_threads());
+  std::vector<int64_t> part((size_t)T + 1, 0);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+    const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+    int64_t o = 0;
+    for (int64_t i = a; i < b; ++i) {
+      o += (int64_t)v[(size_t)i].n;
+      off[i + 1] = o;
+    }
+    part[(size_t)t + 1] = o;
+#pragma omp barrier
+#pragma omp single
+    for (int k = 0; k < nt; ++k) part[(size_t)k + 1] += part[(size_t)k];
+    const int64_t add = part[(size_t)t];
+    for (int64_t i = a; i < b; ++i) off[i + 1] += add;
   }
   // the bytes in parallel: the views point all over the mapped files
 #pragma omp parallel for schedule(static, 4096)
