@@ -2713,10 +2713,12 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
 }
 
 // ---- launch -----------------------------------------------------------------
+using JoinT = JoinCfg<128, 3, 10, 4>; // N <= 384: two waves per query (C1)
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
 using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
 using JoinXL = JoinCfg<1024, 10, 14>; // N <= 10240 (e.g. 10 runs x top-1000; 143 KB LDS)
+using SortT = SortCfg<64, 5, 8>;      // U <= 320: one wave per (query, method) (C1)
 using SortS = SortCfg<256, 4, 4>;     // U <= 1024
 using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
@@ -2852,6 +2854,8 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     // more runs than the LDS join's masks hold: every query takes the workspace join
     e = launch_xl(p, kind, max_entries < 1 ? 1 : max_entries, -1, SortXL::kUMax, st, &ws,
                   ws_user, ws_bytes);
+  } else if (max_entries <= JoinT::kNMax) {
+    launch_join<JoinT>(p, kind, st);
   } else if (max_entries <= JoinS::kNMax) {
     launch_join<JoinS>(p, kind, st);
   } else {
@@ -2863,7 +2867,9 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
                     ws_bytes);
   }
   if (e == hipSuccess) {
-    if (max_entries <= SortS::kUMax) {
+    if (max_entries <= SortT::kUMax) {
+      launch_sort<SortT>(p, 0, st);
+    } else if (max_entries <= SortS::kUMax) {
       launch_sort<SortS>(p, 0, st);
     } else {
       launch_sort<SortM>(p, 0, st);
