@@ -2713,7 +2713,7 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
 }
 
 // ---- launch -----------------------------------------------------------------
-using JoinT = JoinCfg<128, 3, 10, 4>; // N <= 384: two waves per query (C1)
+using JoinT = JoinCfg<64, 5, 10, 6>;  // N <= 320: one wave per query (C1)
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
 using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
