@@ -28,6 +28,26 @@ def test_minmax_bit_exact_and_micro_is_python_format(gpu):
     assert got == fmt
 
 
+@pytest.mark.parametrize("n_lists", [1, 7, 32768, 32769])
+def test_minmax_batch_sizes_and_list_lengths(gpu, n_lists):
+    """One to 32,769 lists of 0-1,100 entries (the register path up to 1,024, the
+    loop beyond), odd counts: bit-exact, and the micro-units are "%.6f"."""
+    from qppfuse import engine
+    rng = np.random.default_rng(n_lists)
+    lens = rng.integers(0, 80, n_lists)
+    lens[rng.random(n_lists) < 0.05] = 512
+    lens[rng.random(n_lists) < 0.02] = 513
+    lens[rng.random(n_lists) < 0.01] = 1100
+    off = np.cumsum(np.concatenate([[0], lens])).astype(np.int64)
+    flat = np.repeat(rng.normal(0, 5, n_lists), lens) + rng.random(int(off[-1]))
+    norm, micro = engine.minmax_per_query(torch.from_numpy(flat).to(gpu),
+                                          torch.from_numpy(off).to(gpu))
+    want = coracle.minmax_per_query(flat, off)
+    assert norm.cpu().numpy().tobytes() == want.tobytes()
+    m = micro.cpu().numpy()
+    assert [f"{x // 10**6}.{x % 10**6:06d}" for x in m] == [f"{v:.6f}" for v in want]
+
+
 def test_round6_half_even_and_hard_cases(gpu):
     """Values next to 6th-decimal ties: the exact binary value decides (CPython)."""
     from qppfuse import engine
