@@ -1465,13 +1465,17 @@ struct BsShared {
   BsKey key;  // wave 0's key constants for the first count
 };
 
-// LDS bytes of bsort_core's area (region A + region BC; BYDOC's docids after it).
-template <int BITS, bool BYDOC>
+// LDS bytes of bsort_core's area (region A + region BC; BYDOC's docids after it):
+// region BC holds the words by position (u32 [UMAX]) and, before them, BYDOC's docid
+// partials (u32 [2 * BLOCK]) and then the bucket starts (u16 [NB + 8], at kStart).
+template <int BITS, bool BYDOC, int UMAX = kJsUMax, int BLOCK = 512>
 struct BsLds {
   static constexpr int kNB = 1 << BITS;
-  static constexpr int kBcBytes = 6144 + 2 * (kNB + 8);
-  static constexpr int kSd = 8 * kJsUMax + kBcBytes;  // BYDOC: docid by position
-  static constexpr int kBytes = kSd + (BYDOC ? 4 * kJsUMax : 0);
+  static constexpr int kStart = UMAX == kJsUMax ? 6144 : 8 * BLOCK;
+  static constexpr int kBcBytes = (4 * UMAX > kStart + 2 * (kNB + 8)) ? 4 * UMAX
+                                                                      : kStart + 2 * (kNB + 8);
+  static constexpr int kSd = 8 * UMAX + kBcBytes;  // BYDOC: docid by position
+  static constexpr int kBytes = kSd + (BYDOC ? 4 * UMAX : 0);
 };
 
 // The bucket sort of one (query, method slot) pair whose U scores are in
@@ -1480,28 +1484,29 @@ struct BsLds {
 // lane), v[j] its score, d[j] its docid (BYDOC).  lds: BsLds<BITS, BYDOC>::kBytes
 // of LDS no one else uses until the call returns.  Writes perm[po + i] (or marks
 // perm[po] for the fallback pass).  Every thread of the block calls it.
-template <int BLOCK, int BITS, bool BYDOC>
-__device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* lds,
+// Returns whether it marked the pair (block-uniform).
+template <int BLOCK, int BITS, bool BYDOC, int UMAX = kJsUMax>
+__device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* lds,
                                            BsShared<BLOCK / 64>& sm,
-                                           double (&v)[(kJsUMax + BLOCK - 1) / BLOCK],
-                                           uint32_t (&d)[BYDOC ? (kJsUMax + BLOCK - 1) / BLOCK : 1],
+                                           double (&v)[(UMAX + BLOCK - 1) / BLOCK],
+                                           uint32_t (&d)[BYDOC ? (UMAX + BLOCK - 1) / BLOCK : 1],
                                            int U, int ub0, int ustep, int64_t po) {
-  constexpr int WAVES = BLOCK / 64, ROWS = (kJsUMax + BLOCK - 1) / BLOCK, NB = 1 << BITS;
+  constexpr int WAVES = BLOCK / 64, ROWS = (UMAX + BLOCK - 1) / BLOCK, NB = 1 << BITS;
   constexpr int MINSUB = NB / 16, MINBASE = NB - MINSUB;
-  static_assert(2 * BLOCK * 8 + 4 * NB <= 8 * kJsUMax, "partials + counters overlay the scores");
+  static_assert(2 * BLOCK * 8 + 4 * NB <= 8 * UMAX, "partials + counters overlay the scores");
   // One LDS array: region A = the scores by position (f64 [kJsUMax]; until the
   // scatter: the range partials [0, 8 KB) and the u32 counters [8 KB, 24 KB));
   // region BC after it = the u | size | arrival words by position (u32 [kJsUMax],
   // from the scatter on), before that the bucket starts (u16, at BC + 6 KB), the
   // spare counter cnt[NB] (BC[0]) and BYDOC's docid partials (BC[0, 4 KB)).
-  constexpr int kBcBytes = BsLds<BITS, BYDOC>::kBcBytes;
-  static_assert(kBcBytes >= 4 * kJsUMax && 6144 >= 8 * BLOCK, "region BC layout");
+  using LD = BsLds<BITS, BYDOC, UMAX, BLOCK>;
+  static_assert(LD::kBcBytes >= 4 * UMAX && LD::kStart >= 8 * BLOCK, "region BC layout");
   double* sval = (double*)lds;                                   // region A
   uint64_t* skey = (uint64_t*)lds;  // region A from the scatter on: bs_rank_key by position
-  uint32_t* sw = (uint32_t*)(lds + 8 * kJsUMax);                 // region BC: u << 20 | size << 8 | at
-  uint16_t* bk = (uint16_t*)(lds + 8 * kJsUMax + 6144);          // bucket starts [NB + 8]
+  uint32_t* sw = (uint32_t*)(lds + 8 * UMAX);                    // region BC: u << 20 | size << 8 | at
+  uint16_t* bk = (uint16_t*)(lds + 8 * UMAX + LD::kStart);       // bucket starts [NB + 8]
   uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                 // [NB + 1] u32
-  uint32_t* sd = (uint32_t*)(lds + BsLds<BITS, BYDOC>::kSd);     // docid by position (BYDOC)
+  uint32_t* sd = (uint32_t*)(lds + LD::kSd);                     // docid by position (BYDOC)
   const int tid = threadIdx.x, lane = tid & 63,
             wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rows = (U + BLOCK - 1) / BLOCK;
@@ -1588,7 +1593,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) acc += (uint32_t)__double2loint(v[j]);
     if (acc == 12345u) perm_put(p, po, acc);
-    return;
+    return false;
   }
 #endif
   const bool nan = sm.nan != 0;
@@ -1598,7 +1603,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
       const int u = ub0 + j * ustep + lane;
       if (j < rows && u < U) perm_put(p, po + u, (uint32_t)u);
     }
-    return;
+    return false;
   }
   const double smax = sm.mx, smin = sm.mn;
   int ush = 0;  // U - 1 >> ush < MINSUB
@@ -1609,7 +1614,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     while (((sm.dmx - dmin) >> dsh) >= (uint32_t)MINSUB) ++dsh;
   // the minimum's sub-bucket of row j: MINBASE + (ub0 + ustep j + lane) >> ush, with
   // 64-aligned row bases and ush <= 6 (U <= kJsUMax): a per-lane part + a row part
-  static_assert(((kJsUMax - 1) >> 6) < MINSUB, "ush <= 6");
+  static_assert(((UMAX - 1) >> 6) < MINSUB, "ush <= 6");
   const uint32_t lane_sub = (uint32_t)lane >> ush;
   uint32_t ws[ROWS];  // bucket | arrival index << 16
   // count with delta = range / 2^shift: -1 = a range the key cannot take (the
@@ -1679,7 +1684,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
   }
   if (cs != 0) {  // uniform: a range the key cannot take, or a bucket still too big
     if (tid == 0) perm_put(p, po, kJsUnsorted);
-    return;
+    return true;
   }
 #if defined(QF_BS_STOP) && QF_BS_STOP == 2  // development: the phases before it only
   {
@@ -1687,7 +1692,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) acc += ws[j];
     if (acc == 12345u) perm_put(p, po, acc);
-    return;
+    return false;
   }
 #endif
 
@@ -1723,7 +1728,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) acc += ws[j] + bk[j];
     if (acc == 12345u) perm_put(p, po, acc);
-    return;
+    return false;
   }
 #endif
 
@@ -1762,7 +1767,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) acc += pa[j] + sw[j];
     if (acc == 12345u) perm_put(p, po, acc);
-    return;
+    return false;
   }
 #endif
 
@@ -1809,7 +1814,7 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) acc += P[j] + uo[j];
     if (acc == 12345u) perm_put(p, po, acc);
-    return;
+    return false;
   }
 #endif
   // ---- outputs (every row's position before any store) ----------------------------------
@@ -1818,12 +1823,20 @@ __device__ __forceinline__ void bsort_core(const FuseParams& p, unsigned char* l
     const int i = pbase + j * 64 + lane;
     if (j < rows && i < U) perm_put(p, po + P[j], uo[j]);
   }
+  return false;
 }
 
-template <int BLOCK, int BITS, bool BYDOC>
-__global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams p) {
-  constexpr int WAVES = BLOCK / 64, ROWS = (kJsUMax + BLOCK - 1) / BLOCK;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[BsLds<BITS, BYDOC>::kBytes];
+// UMAX < kJsUMax with INLINE_FB (small unions, one wave: C1): a pair the bucket sort
+// cannot order is sorted by the LSD window sort in the same workgroup (sort_one over
+// the same LDS), so no fallback pass follows the launch.
+template <int BLOCK, int BITS, bool BYDOC, int UMAX = kJsUMax, bool INLINE_FB = false>
+__global__ __launch_bounds__(BLOCK, BYDOC || INLINE_FB ? 6 : 8) void bsort_kernel(FuseParams p) {
+  constexpr int WAVES = BLOCK / 64, ROWS = (UMAX + BLOCK - 1) / BLOCK;
+  using FbC = SortCfg<BLOCK, ROWS, 8>;
+  constexpr int kBs = BsLds<BITS, BYDOC, UMAX, BLOCK>::kBytes;
+  constexpr int kLds = INLINE_FB && (int)sizeof(SortShared<FbC>) > kBs ? (int)sizeof(SortShared<FbC>)
+                                                                        : kBs;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kLds];
   __shared__ BsShared<WAVES> sm;
   // wid is wave-uniform: readfirstlane puts it (and every row base derived from
   // it) in SGPRs, so the per-row address arithmetic is scalar
@@ -1853,7 +1866,7 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
   if (q >= p.n_queries) return;
   const int U = p.union_count[q];
   const int64_t base = p.list_off[q * p.R];
-  if (U < 1 || U > kJsUMax) return;  // error / fuse_large_kernel's
+  if (U < 1 || U > UMAX) return;  // error / fuse_large_kernel's
   double* io = p.fused + (int64_t)ms * p.out_stride + base;
   const int64_t po = (int64_t)ms * p.out_stride + base;  // perm of this pair
   const int rows = (U + BLOCK - 1) / BLOCK;
@@ -1870,7 +1883,13 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : 8) void bsort_kernel(FuseParams 
     v[j] = __builtin_nontemporal_load(&io[uc]);
     if (BYDOC) d[j] = p.union_docid[base + uc];
   }
-  bsort_core<BLOCK, BITS, BYDOC>(p, lds, sm, v, d, U, wbase, 64, po);
+  const bool marked = bsort_core<BLOCK, BITS, BYDOC, UMAX>(p, lds, sm, v, d, U, wbase, 64, po);
+  if constexpr (INLINE_FB) {
+    if (marked) {  // uniform
+      __syncthreads();
+      sort_one<FbC>(p, *reinterpret_cast<SortShared<FbC>*>(lds), ms, U, base, false);
+    }
+  }
 }
 
 // ============================================================================
@@ -2719,6 +2738,7 @@ using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit s
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
 using JoinXL = JoinCfg<1024, 10, 14>; // N <= 10240 (e.g. 10 runs x top-1000; 143 KB LDS)
 using SortT = SortCfg<64, 5, 8>;      // U <= 320: one wave per (query, method) (C1)
+constexpr int kBsSmallUMax = 384;     // the one-wave bucket sort (C1's unions)
 using SortS = SortCfg<256, 4, 4>;     // U <= 1024
 using SortM = SortCfg<512, 6, 8>;     // U <= 3072
 using SortL = SortCfg<768, 10, 3>;    // U <= 7680
@@ -2867,7 +2887,11 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
                     ws_bytes);
   }
   if (e == hipSuccess) {
-    if (max_entries <= SortT::kUMax) {
+    if (max_entries <= kBsSmallUMax && !(p.methods & QF_LEARNED)) {
+      const int M = __builtin_popcount((unsigned)p.methods);
+      hipLaunchKernelGGL((bsort_kernel<64, 9, false, kBsSmallUMax, true>),
+                         grid_for((p.n_queries + 7) / 8 * 8 * M), dim3(64), 0, st, p);
+    } else if (max_entries <= SortT::kUMax) {
       launch_sort<SortT>(p, 0, st);
     } else if (max_entries <= SortS::kUMax) {
       launch_sort<SortS>(p, 0, st);

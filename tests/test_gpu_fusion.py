@@ -276,6 +276,9 @@ def _sort_case(kind, n, rng):
     elif kind == "huge_and_inf":  # score range overflows: the raw-key window path
         s = rng.uniform(-1, 1, n)
         s[: n // 10] = rng.choice([1.7e308, -1.7e308, np.inf, -np.inf, 0.0], n // 10)
+    elif kind == "heavy_tie":  # > 128 equal scores above the minimum: a bucket overflows
+        s = np.full(n, 0.5)
+        s[: max(1, n // 20)] = rng.uniform(-1, 1, max(1, n // 20))
     elif kind == "zeros_and_ties":
         s = rng.choice([0.0, -0.0, 1.0, 0.5, 0.5 + 2.0 ** -40, -2.0 ** -1074], n)
     else:  # uniform
@@ -284,16 +287,17 @@ def _sort_case(kind, n, rng):
     return s
 
 
-@pytest.mark.parametrize("n", [700, 2560, 2561, 2900, 3072, 3073, 7000, 7681, 10240, 10241,
-                               40000, 70000])
+@pytest.mark.parametrize("n", [1, 2, 63, 65, 300, 320, 321, 384, 385, 700, 2560, 2561, 2900,
+                               3072, 3073, 7000, 7681, 10240, 10241, 40000, 70000])
 @pytest.mark.parametrize("kind", ["wide_then_clustered", "pairs", "zeros_and_ties", "uniform",
-                                  "huge_and_inf"])
+                                  "huge_and_inf", "heavy_tie"])
 def test_sort_is_stable_descending_on_adversarial_keys(gpu, kind, n):
     """One retriever, W-CombSUM with weight 1: the fused scores are the inputs, so the
     kernel's sort (LSD window + run fix-up + full-LSD fallback; above 10,240 the
     workspace bucket sort and its bitonic fallback, above 65,535 with the uint32 perm)
     is checked against a stable descending sort with -0.0 == +0.0 (Python's sorted(),
-    src/fusion.py:488)."""
+    src/fusion.py:488).  Up to 384 entries: the one-wave bucket sort, whose marked
+    pairs (ties beyond a bucket, non-finite ranges) take the LSD sort in-workgroup."""
     from qppfuse import engine
     rng = np.random.default_rng(hash((kind, n)) & 0xFFFF)
     s = _sort_case(kind, n, rng)
