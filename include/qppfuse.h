@@ -235,8 +235,10 @@ int qf_fuse_qpp(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off
  * 10,240 entries, or more than 16 runs); 0 when the call needs none.
  * qf_fuse_ws = qf_fuse (wide = 0: uint16 perm) or qf_fuse_wide (wide = 1: uint32
  * perm) with a caller-owned device workspace: ws = NULL keeps the stream-ordered
- * allocation; otherwise ws_bytes must hold at least one workgroup's share (the
- * call fails with QF_EINVAL naming it), and a workspace smaller than
+ * allocation; otherwise ws must be 256-byte aligned (its workgroup shares hold
+ * u32 atomicCAS targets and u64 sort words; a misaligned ws fails with
+ * QF_EINVAL) and ws_bytes must hold at least one workgroup's share (the call
+ * fails with QF_EINVAL naming it), and a workspace smaller than
  * qf_fuse_workspace_bytes runs the workspace kernel with fewer workgroups (same
  * results).  The workspace needs no initialisation and may be reused by the next
  * call on the same stream; the library never frees it.

@@ -181,6 +181,10 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
     p.learned_sum_f32 = (learned_f32 & all) == all;
   }
   if (ws) {
+    // each workgroup's share (a multiple of 256 bytes) holds the hash table's u32
+    // atomicCAS targets and u64 sort words: the base must be 256-byte aligned
+    if ((uintptr_t)ws % 256u != 0u)
+      return fail(QF_EINVAL, "%s: workspace %p is not 256-byte aligned", fn, ws);
     int64_t min_bytes = 0;
     qf::fuse_workspace_bytes(n_queries, n_retrievers, max_entries, perm32, &min_bytes);
     if ((int64_t)ws_bytes < min_bytes)

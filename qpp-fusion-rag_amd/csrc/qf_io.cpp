@@ -99,6 +99,7 @@ struct RawArray {
     else free(a);
     a = nullptr;
     n = bytes = 0;
+    mapped = false;  // a later small resize() mallocs: never munmap that
   }
   void resize(size_t m) {  // contents undefined
     release();
@@ -1041,6 +1042,70 @@ size_t qfio_format_score(double x, char* out) { return fmt6(x, out); }
 
 }  // extern "C"
 
+// write_run's output file (see there): a temporary file renamed over a regular
+// target, or the target itself opened in place.
+struct AtomicTarget {
+  std::string final_path, tmp_path;  // tmp_path empty: written in place
+  bool seekable = true;
+  static mode_t process_umask() {  // without umask()'s process-wide set-and-restore
+    FILE* f = fopen("/proc/self/status", "r");
+    unsigned m = 022;
+    if (f) {
+      char line[256];
+      while (fgets(line, sizeof line, f))
+        if (sscanf(line, "Umask: %o", &m) == 1) break;
+      fclose(f);
+    }
+    return (mode_t)m;
+  }
+  int open_for(const char* path) {
+    struct stat st;
+    const bool exists = stat(path, &st) == 0;  // follows a symlink to its target
+    if (!exists || S_ISREG(st.st_mode)) {
+      char* rp = exists ? realpath(path, nullptr) : nullptr;
+      final_path = rp ? rp : path;
+      free(rp);
+      const size_t slash = final_path.rfind('/');
+      const std::string dir = slash == std::string::npos ? "." : final_path.substr(0, slash + 1);
+      const std::string base = slash == std::string::npos ? final_path : final_path.substr(slash + 1);
+      std::string tmpl = (slash == std::string::npos ? std::string() : dir) + "." + base +
+                         ".qfio-XXXXXX";
+      std::vector<char> buf(tmpl.begin(), tmpl.end());
+      buf.push_back('\0');
+      const int fd = mkstemp(buf.data());
+      if (fd >= 0) {
+        const mode_t mode = exists ? (st.st_mode & 07777) : (0666 & ~process_umask());
+        if (fchmod(fd, mode) == 0) {
+          tmp_path = buf.data();
+          return fd;
+        }
+        close(fd);
+        unlink(buf.data());
+      }
+    }
+    // in place, as open(path, "w"): a device, a FIFO, or no room for a temporary
+    final_path = path;
+    tmp_path.clear();
+    const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (fd >= 0) {
+      struct stat fs;
+      seekable = fstat(fd, &fs) == 0 && S_ISREG(fs.st_mode);
+    }
+    return fd;
+  }
+  void abandon() {
+    if (!tmp_path.empty()) unlink(tmp_path.c_str());
+  }
+  bool commit() {
+    if (tmp_path.empty()) return true;
+    if (rename(tmp_path.c_str(), final_path.c_str()) == 0) return true;
+    const int e = errno;
+    unlink(tmp_path.c_str());
+    errno = e;
+    return false;
+  }
+};
+
 // write_runfile for one fused run (include/qfio.h), either perm width
 template <class Perm>
 static int write_run(const char* path, int64_t n_out, const int64_t* order, const int64_t* qbase,
@@ -1056,12 +1121,19 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
   const size_t tl = strlen(tag);
   const int T = std::max(1, omp_get_max_threads());
   const int64_t chunks = std::min<int64_t>(std::max<int64_t>(n_out, 1), (int64_t)T * 8);
-  // Written to a temporary file beside the target and renamed over it on success,
-  // so a failure part way (out of memory, a short write) leaves an existing run file
-  // as it was, as the reference's buffered write would until its first flush.
-  const std::string tmp_path = std::string(path) + ".qfio-tmp." + std::to_string((long)getpid());
-  const int fd = open(tmp_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  // A regular (or absent) target in a writable directory is written to a temporary
+  // file beside it (mkstemp in the directory of its real path, the existing file's
+  // mode copied, else 0666 & ~umask as open(path, "w") gives) and renamed over it on
+  // success, so a failure part way (out of memory, a short write) leaves an existing
+  // run file as it was, as the reference's buffered write would until its first
+  // flush; a symlink is written through (its target replaced).  Anything else —
+  // /dev/null, a FIFO or /dev/stdout, a file in a directory we cannot create in — is
+  // written in place like the reference's open(path, "w"), chunks strictly in order
+  // (a pipe cannot seek).
+  AtomicTarget tgt;
+  const int fd = tgt.open_for(path);
   if (fd < 0) return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(errno));
+  const bool seq = !tgt.seekable;
   // Each chunk of queries is formatted into a raw buffer sized by an upper bound
   // (no per-field string appends, no snprintf for the rank) and written at its
   // offset as soon as the chunk before it has published its end: the writes (one
@@ -1140,25 +1212,27 @@ static int write_run(const char* path, int64_t n_out, const int64_t* order, cons
     // this chunk's offset: the previous chunk's end, published once it is formatted
     int64_t off;
     while ((off = at[(size_t)c].load(std::memory_order_acquire)) < 0) std::this_thread::yield();
-    at[(size_t)c + 1].store(off + (int64_t)used, std::memory_order_release);
+    if (!seq) at[(size_t)c + 1].store(off + (int64_t)used, std::memory_order_release);
     size_t done = 0;
     while (o && done < used) {
-      const ssize_t r = pwrite(fd, o + done, used - done, (off_t)(off + (int64_t)done));
+      const ssize_t r = seq ? write(fd, o + done, used - done)
+                            : pwrite(fd, o + done, used - done, (off_t)(off + (int64_t)done));
       if (r <= 0) { werr |= 1; break; }
       done += (size_t)r;
     }
+    // in place on a stream: the next chunk writes only once this one is written
+    if (seq) at[(size_t)c + 1].store(off + (int64_t)used, std::memory_order_release);
     free(o);
   }
   tm.mark("write: format + pwrite");
   const bool closed = close(fd) == 0;
   if (!closed || werr || err) {
-    unlink(tmp_path.c_str());
+    tgt.abandon();
     if (err) return fail(QFIO_EIO, "qfio_write_run: out of memory");
     return fail(QFIO_EIO, std::string("short write to ") + path);
   }
-  if (rename(tmp_path.c_str(), path) != 0) {
+  if (!tgt.commit()) {
     const int e = errno;
-    unlink(tmp_path.c_str());
     return fail(QFIO_EIO, std::string("cannot write ") + path + ": " + strerror(e));
   }
   tm.mark("write: close");

@@ -7,6 +7,7 @@ to the GPU box with the repository snapshot.
 from __future__ import annotations
 
 import os
+import re
 import shutil
 import subprocess
 from pathlib import Path
@@ -18,7 +19,6 @@ LIB_PATH = PKG_DIR / "libqppfuse.so"
 IO_LIB_PATH = PKG_DIR / "libqfio.so"  # host run-file I/O (C++ / OpenMP)
 IO_SOURCES = ["qf_io.cpp"]
 SOURCES = ["qf_fuse.hip", "qf_qpp.hip", "qf_norm.hip", "qf_eval.hip", "qf_learn.hip", "qf_capi.hip"]
-HEADERS = ["qf_common.h", "qf_internal.h", "qf_log2_table.h"]
 ARCH = os.environ.get("QPPFUSE_ARCH", "gfx950")
 # -ffp-contract=off: the reference's arithmetic is sequential IEEE double; an
 # FMA contraction would change bits (fusion sums, Java's Kahan sums).
@@ -32,19 +32,39 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: install ROCm or set HIPCC")
 
 
-def _stale() -> bool:
-    if not LIB_PATH.exists():
+_INCLUDE = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def deps(sources, base: Path = CSRC) -> list:
+    """Every file the sources pull in through `#include "..."`, transitively (resolved
+    against the including file's directory), with the sources themselves: a header
+    edit must mark the library stale (a hand-kept list missed
+    qf_lists.h)."""
+    seen, todo = {}, [(base / s).resolve() for s in sources]
+    while todo:
+        f = todo.pop()
+        if f in seen or not f.exists():
+            continue
+        seen[f] = True
+        for inc in _INCLUDE.findall(f.read_text(errors="replace")):
+            todo.append((f.parent / inc).resolve())
+    return sorted(seen)
+
+
+def _stale_against(lib: Path, sources, base: Path = CSRC) -> bool:
+    if not lib.exists():
         return True
-    t = LIB_PATH.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT.parent / "include" / "qppfuse.h"]
-    return any(d.exists() and d.stat().st_mtime > t for d in deps)
+    t = lib.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps(sources, base))
+
+
+def _stale() -> bool:
+    return _stale_against(LIB_PATH, SOURCES)
 
 
 def build_io(force: bool = False, verbose: bool = True) -> Path:
     """Compile the host I/O library qppfuse/libqfio.so (g++, OpenMP)."""
-    deps = [CSRC / s for s in IO_SOURCES] + [ROOT.parent / "include" / "qfio.h"]
-    if not force and IO_LIB_PATH.exists() and all(
-            d.stat().st_mtime <= IO_LIB_PATH.stat().st_mtime for d in deps if d.exists()):
+    if not force and not _stale_against(IO_LIB_PATH, IO_SOURCES):
         return IO_LIB_PATH
     cxx = os.environ.get("CXX", shutil.which("g++") or "g++")
     tmp = IO_LIB_PATH.with_suffix(".so.tmp")

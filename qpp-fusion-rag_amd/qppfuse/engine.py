@@ -184,6 +184,9 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
     if workspace is not None:
         if workspace.device != out.fused.device or not workspace.is_contiguous():
             raise ValueError("workspace must be a contiguous buffer on the fusion's device")
+        if workspace.data_ptr() % 256:
+            raise ValueError("workspace must be 256-byte aligned (a slice such as ws[1:] is "
+                             "not): its workgroup shares hold atomicCAS targets")
         _lib.call("qf_fuse_ws", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind, _ptr(rank),
                   _ptr(weights), mask, int(rrf_k), int(max_entries), _ptr(out.union_docid),
                   _ptr(out.union_count), _ptr(out.perm), 1 if wide else 0, _ptr(out.fused),

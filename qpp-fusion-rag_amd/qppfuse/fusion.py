@@ -19,6 +19,7 @@ groupby, src/fusion.py:443-446).
 from __future__ import annotations
 
 import os
+import threading
 import weakref
 from collections.abc import Mapping
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -340,13 +341,19 @@ def _launch(rs: RunSet, methods: Sequence[str], rrf_k: int, weights: Optional[np
 
 
 # Page-locked bytes held by live FusedRuns (their numpy views keep the host tensors
-# alive).  A FusedRun's arrays are pinned while the total stays under the cap
-# (QPPFUSE_PINNED_CAP_MB, default 4096): pinned pages cannot be swapped, and torch's
-# caching host allocator keeps freed pinned blocks for reuse rather than returning
-# them, so workflows that keep many runs alive (argmax_runs' 13 QPP-column runs,
-# experiment) would otherwise grow page-locked memory without bound.  Beyond the
-# cap the copy-back lands in pageable memory (~5x slower, same bytes).
+# alive).  A FusedRun's arrays are pinned while the live total stays under the cap
+# (QPPFUSE_PINNED_CAP_MB, default 4096): pinned pages cannot be swapped, and
+# workflows that keep many runs alive (argmax_runs' 13 QPP-column runs, experiment)
+# would otherwise grow page-locked memory without bound.  Beyond the cap the
+# copy-back lands in pageable memory (~5x slower, same bytes).  The cap counts LIVE
+# bytes; torch's caching host allocator also keeps FREED pinned blocks for reuse, so
+# when a copy-back would cross the cap that cache is emptied first
+# (torch._C._host_emptyCache: blocks no live tensor holds go back to the OS) — the
+# page-locked total then stays within the cap plus what the allocator caches between
+# two such crossings.  The counter is updated under a lock (FusedRuns may be built
+# and dropped on several threads).
 _PINNED = {"live": 0}
+_PINNED_LOCK = threading.Lock()
 
 
 def _pinned_cap() -> int:
@@ -354,21 +361,31 @@ def _pinned_cap() -> int:
 
 
 def _release_pinned(nbytes: int) -> None:
-    _PINNED["live"] -= nbytes
+    with _PINNED_LOCK:
+        _PINNED["live"] -= nbytes
 
 
 def _host_copy(t) -> np.ndarray:
-    """t's bytes queued for a copy into host memory (valid after a stream
-    synchronisation), as a numpy array — the object the FusedRun's views keep
+    """Device tensor -> host numpy array (pinned when under the cap: ~5x faster
+    copy-back); a finalizer returns the pinned bytes when the array is no longer
     alive (a tensor's .numpy() holds its storage, not the tensor)."""
     import torch
     nbytes = t.numel() * t.element_size()
-    pinned = _PINNED["live"] + nbytes <= _pinned_cap()
-    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pinned)
+    with _PINNED_LOCK:
+        pinned = _PINNED["live"] + nbytes <= _pinned_cap()
+        if pinned:
+            _PINNED["live"] += nbytes
+        elif hasattr(torch._C, "_host_emptyCache"):
+            torch._C._host_emptyCache()  # the cached, freed pinned blocks
+    try:
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pinned)
+    except BaseException:
+        if pinned:
+            _release_pinned(nbytes)
+        raise
     h.copy_(t, non_blocking=True)  # pageable: the runtime stages it
     a = h.numpy()
     if pinned:
-        _PINNED["live"] += nbytes
         weakref.finalize(a, _release_pinned, nbytes)
     return a
 

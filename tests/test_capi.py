@@ -198,4 +198,46 @@ def test_fuse_ws_rejects_a_short_workspace():
     need = engine.workspace_bytes(1, 5, 100_000, ["rrf"])
     with pytest.raises(ValueError, match="workspace"):
         _lib.call("qf_fuse_ws", 1, 5, 8, 8, 8, 0, None, None, _lib.RRF, 60, 100_000, 8, 8, 8, 1,
-                  8, 16, 8, need - 1, None)
+                  8, 16, 256, need - 1, None)
+
+
+def test_fuse_ws_rejects_a_misaligned_workspace():
+    """Each workgroup's share of the workspace holds u32 atomicCAS targets and u64
+    sort words, so the base must be 256-byte aligned: a slice such as
+    ws[1:] of a torch buffer fails with EINVAL before any device work."""
+    from qppfuse import _lib, engine
+    need = engine.workspace_bytes(1, 5, 100_000, ["rrf"])
+    for base in (8, 256 + 16, 4096 + 1):
+        with pytest.raises(ValueError, match="256-byte aligned"):
+            _lib.call("qf_fuse_ws", 1, 5, 8, 8, 8, 0, None, None, _lib.RRF, 60, 100_000, 8, 8, 8,
+                      1, 8, 16, base, need, None)
+
+
+def test_build_deps_follow_includes(tmp_path):
+    """_build's dependency list comes from an #include scan of the sources, so touching
+    ANY header a source includes (qf_lists.h among them) marks the library stale."""
+    import os
+    from qppfuse import _build
+    names = {p.name for p in _build.deps(_build.SOURCES)}
+    assert {"qf_lists.h", "qf_common.h", "qf_internal.h", "qf_log2_table.h", "qppfuse.h"} <= names
+    assert {"qf_io.cpp", "qfio.h"} <= {p.name for p in _build.deps(_build.IO_SOURCES)}
+    # a private tree: lib newer than every dependency, then one header touched
+    src = tmp_path / "csrc"
+    (src / "sub").mkdir(parents=True)
+    (src / "a.hip").write_text('#include "h1.h"\n#include "sub/h2.h"\n')
+    (src / "h1.h").write_text("#pragma once\n")
+    (src / "sub" / "h2.h").write_text('#include "../h3.h"\n')
+    (src / "h3.h").write_text("// leaf\n")
+    lib = tmp_path / "lib.so"
+    lib.write_bytes(b"")
+    assert sorted(p.name for p in _build.deps(["a.hip"], src)) == ["a.hip", "h1.h", "h2.h", "h3.h"]
+    for p in _build.deps(["a.hip"], src):
+        os.utime(p, (1_000_000, 1_000_000))
+    os.utime(lib, (2_000_000, 2_000_000))
+    assert not _build._stale_against(lib, ["a.hip"], src)
+    os.utime(src / "h3.h", (3_000_000, 3_000_000))  # a header two includes deep
+    assert _build._stale_against(lib, ["a.hip"], src)
+    # and the real library: every in-tree dependency is at most as new as the .so
+    if _build.LIB_PATH.exists() and not _build._stale():
+        t = _build.LIB_PATH.stat().st_mtime
+        assert all(d.stat().st_mtime <= t for d in _build.deps(_build.SOURCES))

@@ -17,6 +17,8 @@ from qppfuse import fastio
 from qppfuse.runset import pack_frames
 
 
+ROOT = Path(__file__).resolve().parents[1]
+
 def _write_runs(tmp_path, rng, n_runs=4, n_q=30, k=50, text_fmt="%.6f"):
     names, paths = [], []
     for r in range(n_runs):
@@ -207,6 +209,79 @@ def test_write_run_failure_leaves_existing_file(tmp_path):
                          np.ones(1), rs, "t")
     assert (target / "keep").read_text() == "old"
     assert sorted(p.name for p in tmp_path.iterdir()) == ["busy"]
+
+
+def test_write_run_target_kinds(tmp_path):
+    """The writer behaves like open(path, "w") for every kind of target:
+    a symlink is written through (the link stays, its target gets the rows), an
+    existing file keeps its mode, a new file gets 0666 & ~umask, /dev/null and a FIFO
+    are written in place (the FIFO in order, read by another thread), and a writable
+    file in a read-only directory is written in place; no temporary file is left."""
+    import stat
+    import threading
+    from qppfuse.runset import RunSet
+    rng = np.random.default_rng(11)
+    Q, U = 40, 30
+    qids = [f"test{i}" for i in range(Q)]
+    docnos = np.array(sorted(f"d{i}" for i in range(200)), dtype=object)
+    counts = np.full(Q, U, np.int32)
+    qbase = np.arange(Q, dtype=np.int64) * U
+    ud = np.concatenate([rng.choice(200, U, replace=False) for _ in range(Q)]).astype(np.uint32)
+    perm = np.tile(np.arange(U, dtype=np.uint16), Q)
+    fused = np.concatenate([np.sort(rng.random(U))[::-1] for _ in range(Q)])
+    rs = RunSet(qids=qids, rankers=["a"], docnos=docnos, list_off=np.zeros(2, np.int64),
+                docid=np.zeros(0, np.uint32), score=np.zeros(0), rank=np.zeros(0, np.int64))
+    order = np.arange(Q, dtype=np.int64)
+    want = "".join(f"{qids[q]} Q0 {docnos[ud[qbase[q] + k]]} {k + 1} {fused[qbase[q] + k]:.6f} t\n"
+                   for q in range(Q) for k in range(U))
+    write = lambda path, threads=4: fastio.write_run(str(path), order, qbase, counts, ud, perm,
+                                                     fused, rs, "t", n_threads=threads)
+    d = tmp_path / "d"
+    d.mkdir()
+    # a symlink: written through
+    real = d / "real.res"
+    real.write_text("old")
+    link = d / "link.res"
+    link.symlink_to(real)
+    write(link)
+    assert link.is_symlink() and real.read_text() == want
+    # an existing file keeps its mode
+    os.chmod(real, 0o640)
+    write(real)
+    assert stat.S_IMODE(real.stat().st_mode) == 0o640 and real.read_text() == want
+    # a new file: 0666 & ~umask
+    old = os.umask(0o027)
+    try:
+        write(d / "new.res")
+    finally:
+        os.umask(old)
+    assert stat.S_IMODE((d / "new.res").stat().st_mode) == 0o640
+    # /dev/null: no error, nothing replaced
+    write("/dev/null")
+    assert os.path.exists("/dev/null") and not os.path.isfile("/dev/null")
+    # a FIFO: in order, in place
+    fifo = d / "pipe"
+    os.mkfifo(fifo)
+    got = []
+    reader = threading.Thread(target=lambda: got.append(open(fifo).read()))
+    reader.start()
+    write(fifo, threads=8)
+    reader.join(60)
+    assert got == [want] and stat.S_ISFIFO(os.stat(fifo).st_mode)
+    # a writable file in a directory we cannot create files in: in place
+    ro = tmp_path / "ro"
+    ro.mkdir()
+    f = ro / "x.res"
+    f.write_text("old")
+    os.chmod(ro, 0o555)
+    try:
+        write(f)  # (as root the mode is not enforced: then the rename path runs)
+        assert f.read_text() == want
+    finally:
+        os.chmod(ro, 0o755)
+    leftovers = [p.name for p in d.iterdir() if "qfio" in p.name] + \
+        [p.name for p in ro.iterdir() if "qfio" in p.name]
+    assert leftovers == []
 
 
 @pytest.mark.parametrize("dtype,n", [(np.int32, 4 * 2**20 // 4 + 3), (np.int8, 4 * 2**20 + 9),
@@ -448,3 +523,39 @@ def test_read_score_lists_errors_like_float(tmp_path):
     e.write_text("")
     got = fastio.read_score_lists(str(e), 100)
     assert got[0] == [] and got[1].tolist() == [0]
+
+
+def test_rawarray_large_then_small_resize(tmp_path):
+    """qf_io.cpp's RawArray mmaps buffers >= 4 MB and mallocs smaller ones; release()
+    must forget the mapping, or a later small resize() would munmap a malloc'd
+    pointer.  A C++ harness including the translation unit (g++, no
+    GPU) resizes large -> small -> large -> small and frees each through the same
+    release path; it runs under glibc's heap checks (MALLOC_CHECK_=3)."""
+    import os
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    src = tmp_path / "rawarray.cpp"
+    src.write_text(
+        '#include "%s"\n'
+        "int main() {\n"
+        "  RawArray<double> a;\n"
+        "  for (int r = 0; r < 3; ++r) {\n"
+        "    a.resize((8u << 20) / sizeof(double));  // mmap'd\n"
+        "    if (!a.mapped) return 2;\n"
+        "    a[0] = 1.0;\n"
+        "    a.resize(16);                            // malloc'd\n"
+        "    if (a.mapped) return 3;\n"
+        "    a[15] = 2.0;\n"
+        "  }\n"
+        "  a.release();\n"
+        "  if (a.mapped || a.data() != nullptr) return 4;\n"
+        "  return 0;\n"
+        "}\n" % (ROOT / "qpp-fusion-rag_amd" / "csrc" / "qf_io.cpp"))
+    exe = tmp_path / "rawarray"
+    subprocess.run([gxx, "-O1", "-std=c++17", "-fopenmp", "-o", str(exe), str(src)], check=True,
+                   timeout=300)
+    r = subprocess.run([str(exe)], env=dict(os.environ, MALLOC_CHECK_="3"), timeout=60)
+    assert r.returncode == 0
