@@ -8,9 +8,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Development stop points: QF_STOP(phase, acc, action...) marks where a development
+// build (tools/dev/qf_dev_hooks.h, force-included by qppfuse._build.build_variant
+// only) returns early to time the phases before it; in the library it expands to
+// nothing — no branch, no computation of `acc`.
+#ifndef QF_STOP
+#define QF_STOP(phase, acc, ...) \
+  do {                            \
+  } while (0)
+#endif
+
 namespace qf {
 
 constexpr int kWave = 64;
+constexpr int kBufNT = 2;  // buffer load / store cache policy: non-temporal (gfx950 "nt")
 constexpr int kQppCols = 13;
 
 // ---- wave-level primitives ------------------------------------------------

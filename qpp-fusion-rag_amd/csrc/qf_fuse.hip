@@ -37,22 +37,6 @@ constexpr int kRMaxXl = 32;  // in the workspace kernel (u32 masks)
 constexpr int kNMethods = 9;  // method bits QF_COMBSUM .. QF_WRRF_MUL
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-#ifdef QF_STAMPS
-// Diagnostic build only (tools/): per-block phase cycle counts of block 0..kStampBlocks-1.
-constexpr int kStampBlocks = 32768, kStampSlots = 16;
-__device__ unsigned long long g_stamps[kStampBlocks * kStampSlots];
-#define QF_STAMP_INIT() unsigned long long _st_prev = __builtin_amdgcn_s_memtime()
-#define QF_STAMP(slot)                                                          \
-  do {                                                                          \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();                 \
-    if (threadIdx.x == 0 && block_id() < kStampBlocks)                          \
-      g_stamps[block_id() * kStampSlots + (slot)] += _t - _st_prev;              \
-    _st_prev = _t;                                                              \
-  } while (0)
-#else
-#define QF_STAMP_INIT()
-#define QF_STAMP(slot)
-#endif
 
 // Score as stored: int32 micro-units (exact "%.6f" text) or double.
 template <int KIND>
@@ -112,6 +96,26 @@ __device__ __forceinline__ double shl1_lane(double v) {
   const int32_t hi = __builtin_amdgcn_update_dpp((int32_t)(b >> 32), (int32_t)(b >> 32), 0x130,
                                                  0xf, 0xf, false);
   return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
+// Raw v_min_f64 / v_max_f64, without fmin / fmax's NaN canonicalisation (three
+// more instructions per call): the callers flag NaNs themselves and discard the
+// range when one is present.
+__device__ __forceinline__ double raw_min_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double raw_max_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// min(a, -b) in one instruction (the negation is a source modifier)
+__device__ __forceinline__ double raw_min_neg_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, -%2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 // MIN / MAX of a 64-bit key over the block (s_min / s_max pre-initialised; a
@@ -200,7 +204,6 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
   // wave's leaders hit distinct banks); counts and offsets stay below 2^16
   uint32_t* hist = sx.hist;
   uint16_t* hist16 = (uint16_t*)sx.hist;
-  QF_STAMP_INIT();
   for (int k = lane; k < kBuckets / 2; k += 64) hist[wid * (kBuckets / 2) + k] = 0u;
   // Rank of every item among its wave's items with the same digit, in item
   // order (see above).  Round 3 took it from one ds_add_rtn per item, which is
@@ -228,9 +231,7 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
       if (act) rank_in[j] = ((old >> hs) & 0xFFFFu) + below;
     }
   }
-  QF_STAMP(8);
   __syncthreads();
-  QF_STAMP(9);
   // block-wide exclusive scan of the kBuckets*WAVES counters in [digit][wave]
   // order, kPer per thread (16-bit loads and stores: no word is shared)
   {
@@ -257,7 +258,6 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
     }
   }
   __syncthreads();
-  QF_STAMP(10);
   asm volatile("" : "+s"(rp));
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -265,9 +265,7 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
     if (j < rp && i < sx.U)
       sx.sitem[hist16[wid * kBuckets + digit(item[j])] + rank_in[j]] = item[j];
   }
-  QF_STAMP(11);
   __syncthreads();
-  QF_STAMP(12);
   if (readback) {
     asm volatile("" : "+s"(rp));
 #pragma unroll
@@ -276,7 +274,6 @@ __device__ __forceinline__ void count_scatter(const SortCtx<ITEMS, WAVES>& sx,
       if (j < rp && i < sx.U) item[j] = sx.sitem[i];
     }
   }
-  QF_STAMP(13);
 }
 
 // Lane l gets lane l-1's value (DPP wave_shr:1; lane 0 gets its own back).
@@ -324,7 +321,6 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
     sh += kDigit;
     if (sh < (fallback ? hb_full : nb)) continue;
     if (fallback || exact) return;
-    QF_STAMP_INIT();
     // -- A: find the runs to fix (read-only) ----------------------------------------
     // First every row's predecessor window and, where the windows tie, both scores
     // are loaded (all rows' loads in flight at once), then compared: one memory
@@ -384,9 +380,7 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
       }
       if (any) atomicOr(&sx.flag[0], 2);
     }
-    QF_STAMP(5);
     __syncthreads();
-    QF_STAMP(6);
     const int f = sx.flag[0];  // block-uniform
     if (f == 0) return;        // no bad item: already in full-key order
     if (!(f & 1)) {
@@ -411,7 +405,6 @@ __device__ void sort_desc(const SortCtx<ITEMS, WAVES>& sx, uint32_t (&item)[ITEM
       }
       __syncthreads();
     }
-    QF_STAMP(7);
     if (sx.flag[0] & 1) {  // a run too long: finish with full LSD passes
       fallback = true;
       sh = 0;
@@ -591,6 +584,7 @@ struct JoinShared {
   int cnt[C::kItems * C::kWaves], gof[C::kItems * C::kWaves];
   // lane 0's score of every (row, wave): lane 63's successor for the sort check
   typename ScoreIn<KIND>::raw_t first[C::kItems * C::kWaves + 1];
+  double wres[12][C::kWaves];  // pair_info: every wave's reduced slot ranges
   int U, status;
   int slow;  // bit 0: a non-empty list is not [0, 1]-normalised; bit 1: a weight needs IEEE division
 };
@@ -615,7 +609,6 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   };
   const int tid = threadIdx.x, lane = tid & 63,
             wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR
-  QF_STAMP_INIT();
   const int R = p.R;
   if (tid <= R) sh.off[tid] = p.list_off[q * R + tid];
   if (tid == 0) {
@@ -669,17 +662,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   for (int i = tid * 4; i < TS / 2; i += BLOCK * 4)
     *(uint4*)&tmask2[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
-  QF_STAMP(3);
-#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 1  // development: phase VALU
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
-    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
-    return -1;
-  }
-#endif
+  QF_STOP(11, [&] { uint32_t a = 0u; for (int j = 0; j < ITEMS; ++j) a += dk[j] + (uint32_t)sc[j]; return a; },
+          if (_qf_acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0; return -1;);
   // ---- insert: entry e = j*BLOCK + tid of list r(e) --------------------------
   int status = 0;
   uint32_t rj[ITEMS];
@@ -735,17 +719,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       if (((defer >> j) & 1u) && sh.first[j * WAVES + wid + 1] > sc[j]) st = QF_QSTATUS_UNSORTED;
     if (st) atomicMin(&sh.status, st);  // read after the barriers that follow
   }
-  QF_STAMP(4);
-#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 2  // development: phase VALU
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
-    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
-    return -1;
-  }
-#endif
+  QF_STOP(12, [&] { uint32_t a = 0u; for (int j = 0; j < ITEMS; ++j) a += dk[j] + (uint32_t)sc[j]; return a; },
+          if (_qf_acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0; return -1;);
   // ---- number distinct documents in first-seen order; size their groups ------
   uint32_t repm = 0u;
 #pragma unroll
@@ -793,17 +768,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
-  QF_STAMP(5);
-#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 3  // development: phase VALU
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
-    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
-    return -1;
-  }
-#endif
+  QF_STOP(13, [&] { uint32_t a = 0u; for (int j = 0; j < ITEMS; ++j) a += dk[j] + (uint32_t)sc[j]; return a; },
+          if (_qf_acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0; return -1;);
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const bool rep = (repm >> j) & 1u;
@@ -832,17 +798,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     }
   }
   __syncthreads();  // the hash table is dead; its LDS becomes the groups
-  QF_STAMP(6);
-#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 4  // development: phase VALU
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
-    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
-    return -1;
-  }
-#endif
+  QF_STOP(14, [&] { uint32_t a = 0u; for (int j = 0; j < ITEMS; ++j) a += dk[j] + (uint32_t)sc[j]; return a; },
+          if (_qf_acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0; return -1;);
   raw_t* gsc = (raw_t*)(smem + L::kGscOff);
   uint32_t* gpr = (uint32_t*)(smem + L::kGprOff);
   uint16_t* ugo = (uint16_t*)(smem + L::kGoOff);
@@ -857,17 +814,8 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
     }
   }
   __syncthreads();
-  QF_STAMP(7);
-#if defined(QF_JOIN_STOP) && QF_JOIN_STOP == 5  // development: phase VALU
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) acc += dk[j] + (uint32_t)sc[j];
-    // union_count = 0 (thread 0 always): the sort kernels after it skip the query
-    if (acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0;
-    return -1;
-  }
-#endif
+  QF_STOP(15, [&] { uint32_t a = 0u; for (int j = 0; j < ITEMS; ++j) a += dk[j] + (uint32_t)sc[j]; return a; },
+          if (_qf_acc == 12345u || threadIdx.x == 0) p.union_count[q] = 0; return -1;);
   return N;
 }
 
@@ -888,11 +836,29 @@ struct RecipTable {
 };
 __device__ constexpr RecipTable kRecip60{};
 
+// Each method slot's range over the query's documents, kept by the join's sums loop
+// for the bucket sort (round 5, pair_info below): every thread's running min and
+// min of the negated values (= -max), one v_min_f64 each per document and slot.
+// Tracked for the compile-time method sets of fast_sums (<= 6 slots).
+constexpr int kRangeSlots = 6;
+struct SlotRange {
+  double mn[kRangeSlots], nmx[kRangeSlots];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int s = 0; s < kRangeSlots; ++s) mn[s] = nmx[s] = INFINITY;
+  }
+  __device__ __forceinline__ void add(int s, double v) {
+    mn[s] = raw_min_f64(mn[s], v);
+    nmx[s] = raw_min_neg_f64(nmx[s], v);
+  }
+};
+
 // The fast path of store_unsorted_sums: MS = the method set when known at compile
-// time (0: read it from p.methods); TAB: rrf_k == 60, reciprocals from kRecip60.
+// time (0: read it from p.methods; no ranges kept); TAB: rrf_k == 60, reciprocals
+// from kRecip60.
 template <int MS, bool TAB, class C, int KIND, int EXTRA>
 __device__ __forceinline__ void fast_sums(const FuseParams& p, JoinShared<C, KIND, EXTRA>& sh,
-                                          int N, const int (&slot)[kNMethods]) {
+                                          int N, const int (&slot)[kNMethods], SlotRange& rg) {
   static_assert(C::kNMax <= kRecipN, "positions beyond the table");
   constexpr int BLOCK = C::kBlock;
   using L = JoinLds<C, KIND>;
@@ -926,12 +892,19 @@ __device__ __forceinline__ void fast_sums(const FuseParams& p, JoinShared<C, KIN
     const double cnt = (double)(ge - gs);
     double* out = p.fused + base + u;
     const int64_t st = p.out_stride;
-    if (methods & QF_COMBSUM) out[slot[0] * st] = a0;
-    if (methods & QF_COMBMNZ) out[slot[1] * st] = a0 * cnt;
-    if (methods & QF_RRF) out[slot[2] * st] = a1;
-    if (methods & QF_WCOMBSUM) out[slot[3] * st] = a2;
-    if (methods & QF_WCOMBMNZ) out[slot[4] * st] = a2 * cnt;
-    if (methods & QF_WRRF) out[slot[5] * st] = a5;
+    // each value stored at its slot and, for a compile-time set (slot k = the
+    // constant count of requested methods below it), kept in the slot's range
+    int k = 0;
+    auto put = [&](int t, double x) {
+      out[slot[t] * st] = x;
+      if (MS != 0) rg.add(k++, x);
+    };
+    if (methods & QF_COMBSUM) put(0, a0);
+    if (methods & QF_COMBMNZ) put(1, a0 * cnt);
+    if (methods & QF_RRF) put(2, a1);
+    if (methods & QF_WCOMBSUM) put(3, a2);
+    if (methods & QF_WCOMBMNZ) put(4, a2 * cnt);
+    if (methods & QF_WRRF) put(5, a5);
   };
   // (Measured, not kept: the documents in one list taken first and those in
   // several after them, through a two-class permutation, so that a wave of
@@ -943,9 +916,12 @@ __device__ __forceinline__ void fast_sums(const FuseParams& p, JoinShared<C, KIN
 // Every document's fused score for every requested method, from the groups the
 // join left in LDS, stored unsorted at fused[slot][base + u] (the sort kernels
 // read them back): one thread per document, strided.
+// Returns whether `rg` holds every slot's range (a compile-time method set of the
+// fast path).
 template <class C, int KIND, int EXTRA>
-__device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
-                                                    JoinShared<C, KIND, EXTRA>& sh, int N) {
+__device__ __forceinline__ bool store_unsorted_sums(const FuseParams& p,
+                                                    JoinShared<C, KIND, EXTRA>& sh, int N,
+                                                    SlotRange& rg) {
   constexpr int BLOCK = C::kBlock;
   using L = JoinLds<C, KIND>;
   using raw_t = typename L::raw_t;
@@ -977,7 +953,7 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
       }
       p.fused[base + u] = a6;  // the one method slot
     }
-    return;
+    return false;
   }
   const bool fast = KIND == 1 && sh.slow == 0 && !p.rank && (methods & ~kFastSumMethods) == 0 &&
                     rrf_k >= 0 && rrf_k + N + 1 <= (1 << 24);
@@ -988,18 +964,18 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
     const bool tab = rrf_k == kRecipK;
     switch (methods) {
       case kFastSumMethods:
-        if (tab) fast_sums<kFastSumMethods, true>(p, sh, N, slot);
-        else fast_sums<kFastSumMethods, false>(p, sh, N, slot);
-        return;
+        if (tab) fast_sums<kFastSumMethods, true>(p, sh, N, slot, rg);
+        else fast_sums<kFastSumMethods, false>(p, sh, N, slot, rg);
+        return true;
       case QF_COMBSUM | QF_RRF:
-        if (tab) fast_sums<QF_COMBSUM | QF_RRF, true>(p, sh, N, slot);
-        else fast_sums<QF_COMBSUM | QF_RRF, false>(p, sh, N, slot);
-        return;
-      case QF_WCOMBSUM: fast_sums<QF_WCOMBSUM, false>(p, sh, N, slot); return;
-      case QF_COMBSUM: fast_sums<QF_COMBSUM, false>(p, sh, N, slot); return;
-      case QF_RRF: fast_sums<QF_RRF, false>(p, sh, N, slot); return;
-      case QF_WRRF: fast_sums<QF_WRRF, false>(p, sh, N, slot); return;
-      default: fast_sums<0, false>(p, sh, N, slot); return;
+        if (tab) fast_sums<QF_COMBSUM | QF_RRF, true>(p, sh, N, slot, rg);
+        else fast_sums<QF_COMBSUM | QF_RRF, false>(p, sh, N, slot, rg);
+        return true;
+      case QF_WCOMBSUM: fast_sums<QF_WCOMBSUM, false>(p, sh, N, slot, rg); return true;
+      case QF_COMBSUM: fast_sums<QF_COMBSUM, false>(p, sh, N, slot, rg); return true;
+      case QF_RRF: fast_sums<QF_RRF, false>(p, sh, N, slot, rg); return true;
+      case QF_WRRF: fast_sums<QF_WRRF, false>(p, sh, N, slot, rg); return true;
+      default: fast_sums<0, false>(p, sh, N, slot, rg); return false;
     }
   }
   for (int u = tid; u < U; u += BLOCK) {
@@ -1057,6 +1033,154 @@ __device__ __forceinline__ void store_unsorted_sums(const FuseParams& p,
     if (methods & QF_PROBFUSE) out[slot[7] * st] = a7;
     if (methods & QF_WRRF_MUL) out[slot[8] * st] = a8;
   }
+  return false;
+}
+
+// ---- the bucket sort's key constants, from the join ----------------------------
+// bsort_fast_kernel buckets a (query, method slot) pair's scores by a key whose
+// constants depend only on the pair's min and max.  The join holds every score in a
+// register once (the sums loop), so it keeps each slot's range (SlotRange) and
+// leaves the constants at fused[slot][base + U .. + kPairInfo) — slots [U, N) of a
+// query's rows are scratch (include/qppfuse.h) — when N - U >= kPairInfo:
+//   [0] min, [1] max (-0.0 folded into +0.0), [2] c: the key's x = v + c when cform,
+//   else x = (v - min) + c, [3] top | cform << 31 | scale << 32 (bs_key2), or
+//   kPairMark (a range the key cannot take: the fallback pass sorts the pair), or 0:
+//   no constants (the sort computes them itself).
+// The sort then needs no range phase (round 4: 1.9 x 10^7 VALU and 2.8 x 10^7 SALU
+// of the C2 launch, a block reduction and a serial wave-0 section per pair).
+constexpr int kPairInfo = 4;
+constexpr uint64_t kPairMark = ~0ull;
+struct BsKey2 {
+  double c;
+  uint32_t top, scale;
+  int cform, ok;
+};
+// delta = (max - min) / 2^shift; x = v + (delta - min) when that keeps every x >=
+// delta / 2 > 0 (monotone rounding), else (v - min) + delta; bucket = mul_hi(top -
+// hi32(x), scale) with top = hi32(x(max)) and scale = floor(MINBASE * 2^32 / span) -
+// 1: non-increasing in v (larger scores first), < MINBASE, equal scores together.
+template <int MINBASE>
+__device__ __forceinline__ BsKey2 bs_key2(double smin, double smax, bool nan, int shift) {
+  BsKey2 k{};
+  const double rng = smax - smin;
+  const double delta = ldexp(rng, -shift);
+  if (!(isfinite(rng) && delta > 0.0) || nan) return k;
+  const double c = delta - smin;
+  k.cform = isfinite(c) && (smin + c) >= 0.5 * delta;
+  const double xmin = k.cform ? smin + c : delta;
+  const double xmax = k.cform ? smax + c : rng + delta;
+  if (!isfinite(xmax)) return k;
+  const uint32_t b0 = (uint32_t)((uint64_t)__double_as_longlong(xmin) >> 32);
+  k.top = (uint32_t)((uint64_t)__double_as_longlong(xmax) >> 32);
+  const uint32_t span = k.top - b0 + 1u;
+  k.scale = span <= (uint32_t)MINBASE
+                ? 0xFFFFFFFFu
+                : (uint32_t)((double)MINBASE * 4294967296.0 / (double)span) - 1u;
+  k.c = k.cform ? c : delta;
+  k.ok = 1;
+  return k;
+}
+__device__ __forceinline__ uint64_t bs_key2_word(const BsKey2& k) {
+  return k.ok ? ((uint64_t)k.scale << 32) | ((uint64_t)k.cform << 31) | k.top : kPairMark;
+}
+constexpr int kFastBits = 12, kFastNB = 1 << kFastBits, kFastMinBase = kFastNB - kFastNB / 16;
+constexpr int kFastDeltaShift = 8;   // delta = range / 2^8 (tools/bsort_sim.py, round 3)
+constexpr int kFastRetryShift = 20;  // the recount after a bucket overflow
+
+// Quad min of a double (DPP quad_perm; result in every lane of the quad).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double quad_min_f64(double x) {
+  x = raw_min_f64(x, dpp_f64<0xB1>(x));  // quad_perm [1,0,3,2]
+  x = raw_min_f64(x, dpp_f64<0x4E>(x));  // quad_perm [2,3,0,1]
+  return x;
+}
+
+// min(a, b) of the value pair the half-exchange v_permlane32_swap (SIXTEEN: the
+// row exchange v_permlane16_swap) leaves in this lane: lanes of the lower half
+// (row) keep value a, min'd with the partner lane's a; the upper half keeps b.
+template <bool SIXTEEN>
+__device__ __forceinline__ double swap_min_f64(double a, double b) {
+  const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+  const auto lo = SIXTEEN ? __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false)
+                          : __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = SIXTEEN
+                      ? __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32),
+                                                         false, false)
+                      : __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32),
+                                                         false, false);
+  const double x = __longlong_as_double((int64_t)(((uint64_t)hi[0] << 32) | lo[0]));
+  const double y = __longlong_as_double((int64_t)(((uint64_t)hi[1] << 32) | lo[1]));
+  return raw_min_f64(x, y);
+}
+
+// Every slot's range reduced over the block and its key constants stored (see
+// above).  All threads call it after the sums; `ranged`: rg holds the ranges.
+// The 12 running values (6 minima, 6 negated maxima) are reduced in registers:
+// two half-exchanges leave each lane 3 values, min'd over 4 lanes (v_permlane32 /
+// 16_swap: lanes 0-31 keep values 0-5, lanes 32-63 values 6-11, then even 16-lane
+// rows the first 3 of those, odd rows the last 3), a DPP butterfly reduces them over
+// each row (row r then holds values 3r .. 3r + 2), one lane per row stores them, and
+// wave 0 reduces the waves' results — no LDS transposition (round 5's first form,
+// whose transposed reads hit one bank per lane quad: join +48 us).
+template <class C, int KIND, int EXTRA>
+__device__ __forceinline__ void pair_info(const FuseParams& p, JoinShared<C, KIND, EXTRA>& sh,
+                                          int N, bool ranged, const SlotRange& rg) {
+  constexpr int WAVES = C::kWaves, NV = 2 * kRangeSlots;
+  static_assert(NV == 12, "three values per 16-lane row after the two exchanges");
+  const int U = sh.U;
+  if (sh.status || N - U < kPairInfo) return;  // uniform
+  const int M = __popc(p.methods);
+  const int64_t at = sh.off[0] + U;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (!ranged || M > kRangeSlots) {  // uniform: "no constants" (w3 = 0)
+    if (tid < M) ((uint64_t*)p.fused)[tid * p.out_stride + at + 3] = 0ull;
+    return;
+  }
+  double y[6], z[3];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) y[k] = swap_min_f64<false>(rg.mn[k], rg.nmx[k]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    z[k] = swap_min_f64<true>(y[k], y[k + 3]);
+    z[k] = raw_min_f64(z[k], dpp_f64<0xB1>(z[k]));   // quad_perm [1,0,3,2]
+    z[k] = raw_min_f64(z[k], dpp_f64<0x4E>(z[k]));   // quad_perm [2,3,0,1]
+    z[k] = raw_min_f64(z[k], dpp_f64<0x141>(z[k]));  // row_half_mirror
+    z[k] = raw_min_f64(z[k], dpp_f64<0x140>(z[k]));  // row_mirror
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) sh.wres[3 * (lane >> 4) + k][wid] = z[k];
+  }
+  __syncthreads();
+  if (wid == 0) {
+    // lanes 4v .. 4v + 3: value v over the waves, then a quad min
+    double x = INFINITY;
+    if (lane < 4 * NV)
+      for (int k = lane & 3; k < WAVES; k += 4) x = raw_min_f64(x, sh.wres[lane >> 2][k]);
+    x = quad_min_f64(x);
+    // lane 4s: min of slot s; lane 4 (kRangeSlots + s): -max of slot s
+    const int64_t nb = __double_as_longlong(x);
+    const int src = (lane + 4 * kRangeSlots) << 2;
+    const int lo = __builtin_amdgcn_ds_bpermute(src, (int)nb);
+    const int hi = __builtin_amdgcn_ds_bpermute(src, (int)(nb >> 32));
+    const double nmax = __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+    if ((lane & 3) == 0 && (lane >> 2) < M) {
+      const int s = lane >> 2;
+      const double smin = x + 0.0, smax = -nmax + 0.0;  // -0.0 folded into +0.0
+      const BsKey2 k = bs_key2<kFastMinBase>(smin, smax, false, kFastDeltaShift);
+      double* o = p.fused + s * p.out_stride + at;
+      o[0] = smin;
+      o[1] = smax;
+      o[2] = k.c;
+      ((uint64_t*)o)[3] = bs_key2_word(k);
+    }
+  }
 }
 
 // f64 scores need 72 KB of LDS (2 per CU), so only micro-unit scores aim higher
@@ -1068,10 +1192,15 @@ void join_kernel(FuseParams p) {
   if (q >= p.n_queries) return;
   const int N = join_groups<C, KIND>(p, sh, q);
   if (N < 0) return;
-  QF_STAMP_INIT();
-  store_unsorted_sums<C, KIND>(p, sh, N);
+  SlotRange rg;
+  rg.init();
+  const bool ranged = store_unsorted_sums<C, KIND>(p, sh, N, rg);
   if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : sh.U;
-  QF_STAMP(14);
+  // (development stop 16: the sums without the key constants — w3 = 0, the sort
+  // computes them itself)
+  QF_STOP(16, [&] { return 0u; },
+          pair_info<C, KIND>(p, sh, N, false, rg); return;);
+  pair_info<C, KIND>(p, sh, N, ranged, rg);
 }
 
 // ============================================================================
@@ -1111,7 +1240,6 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
                                          int64_t base, bool by_docid) {
   constexpr int ITEMS = C::kItems, WAVES = C::kWaves;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  QF_STAMP_INIT();
   if (tid == 0) {
     sh.kmin = ~0ull;
     sh.kmax = 0ull;
@@ -1222,11 +1350,8 @@ __device__ __forceinline__ void sort_one(const FuseParams& p, SortShared<C>& sh,
       item[j] = ((uint32_t)((wk - wmin) >> lo) << kUBits) | (uint32_t)i;
     }
   }
-  QF_STAMP(0);
   if (hb_full > 0) sort_desc(sx, item, hb - lo, exact, hb_full);  // else all keys equal
-  QF_STAMP(1);
   write_out(sx, item, p, (int64_t)ms * p.out_stride + base);
-  QF_STAMP(2);
 }
 // Method bit of output slot ms.
 __device__ __forceinline__ int slot_method(int methods, int ms) {
@@ -1346,19 +1471,6 @@ constexpr int kJsBucketMax = 128;
 // the counters), then 14 KB for the bucket starts and, from the scatter on, the
 // words by position.  38.2 KB: 4 workgroups per CU.
 // ============================================================================
-// Raw v_min_f64 / v_max_f64, without fmin / fmax's NaN canonicalisation (three
-// more instructions per call): the callers flag NaNs themselves and discard the
-// range when one is present.
-__device__ __forceinline__ double raw_min_f64(double a, double b) {
-  double r;
-  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ double raw_max_f64(double a, double b) {
-  double r;
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 
 // a == s ? if_eq : if_ne as one compare and one v_cndmask (the compiler turns
 // the plain ternary into a branch around the f64 key arithmetic, ~6 more
@@ -1587,15 +1699,6 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
-#if defined(QF_BS_STOP) && QF_BS_STOP == 1  // development: the phases before it only
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) acc += (uint32_t)__double2loint(v[j]);
-    if (acc == 12345u) perm_put(p, po, acc);
-    return false;
-  }
-#endif
   const bool nan = sm.nan != 0;
   if (!BYDOC && sm.mn == sm.mx && !nan) {  // every score equal: first-seen order
 #pragma unroll
@@ -1637,11 +1740,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
         uint32_t b = sel_if_eq_f64(v[j], smin, minb, (uint32_t)(MINBASE - 1) - key);
         b = u < U ? b : (uint32_t)NB;
         ws[j] = b;
-#if defined(QF_BS_STOP) && defined(QF_BS_PROBE_CNT)  // development timing probe: conflict-free counters
-        old[j] = atomicAdd(&cnt[(uint32_t)(tid + j * BLOCK) & (uint32_t)(NB - 1)], 1u);
-#else
         old[j] = atomicAdd(&cnt[b], 1u);
-#endif
       }
     }
     bool bigl = false;
@@ -1686,15 +1785,6 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
     if (tid == 0) perm_put(p, po, kJsUnsorted);
     return true;
   }
-#if defined(QF_BS_STOP) && QF_BS_STOP == 2  // development: the phases before it only
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) acc += ws[j];
-    if (acc == 12345u) perm_put(p, po, acc);
-    return false;
-  }
-#endif
 
   // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
   {
@@ -1722,15 +1812,6 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
     if (tid == 0) bk[NB] = (uint16_t)U;
   }
   __syncthreads();
-#if defined(QF_BS_STOP) && QF_BS_STOP == 3  // development: the phases before it only
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) acc += ws[j] + bk[j];
-    if (acc == 12345u) perm_put(p, po, acc);
-    return false;
-  }
-#endif
 
   const bool nonneg = smin >= 0.0;  // block-uniform (smin folds -0.0 into +0.0)
   // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
@@ -1741,11 +1822,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
     if (j < rows && u < U) {
       const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
       const uint32_t st = bk[b], nx = bk[b + 1];
-#if defined(QF_BS_STOP) && defined(QF_BS_PROBE_SCAT)  // development timing probe: linear positions
-      const uint32_t pos = (uint32_t)u + 0u * (st + at);
-#else
       const uint32_t pos = st + at;
-#endif
       // the rank phase compares integer keys: for a pair without negative scores
       // (every C2 fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
       skey[pos] = nonneg ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);
@@ -1761,15 +1838,6 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
     if (j < rows && u < U) sw[pa[j]] = pw[j];
   }
   __syncthreads();
-#if defined(QF_BS_STOP) && QF_BS_STOP == 4  // development: the phases before it only
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) acc += pa[j] + sw[j];
-    if (acc == 12345u) perm_put(p, po, acc);
-    return false;
-  }
-#endif
 
   // ---- rank inside the bucket, in position order --------------------------------------
   uint32_t P[ROWS], uo[ROWS];
@@ -1808,15 +1876,6 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
       uo[j] = wi >> 20;
     }
   }
-#if defined(QF_BS_STOP) && QF_BS_STOP == 5  // development: the phases before it only
-  {
-    uint32_t acc = 0u;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) acc += P[j] + uo[j];
-    if (acc == 12345u) perm_put(p, po, acc);
-    return false;
-  }
-#endif
   // ---- outputs (every row's position before any store) ----------------------------------
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
@@ -1896,6 +1955,353 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : INLINE_FB ? 7 : 8) void bsort_ke
 }
 
 // ============================================================================
+// bsort_fast_kernel (round 5) — the default path's sort of every non-learned slot
+// with U <= UMAX: bsort_kernel's bucket sort (same order: scores descending, ties in
+// first-seen u order) with fewer instructions per item; bsort_kernel keeps learned
+// fusion's docid-tie slot (BYDOC) and C1's one-wave form.
+//  * key constants from the join (pair_info: the slot's min / max and the key's
+//    constants at fused[slot][base + U]) — no range phase, no block reduction, no
+//    serial wave-0 section; computed here only when the join left none;
+//  * the scores read with buffer loads: one voffset for every row (the row offset in
+//    the instruction), the hardware returns 0.0 past U — no clamp, no per-row address;
+//  * bucket = mul_hi(top - hi32(x), scale): larger scores first without a subtraction;
+//    lanes past U count into spare counters (NB + lane % 16, < 64 arrivals each), so
+//    a bucket overflow is one running max of the arrival indices, read after the
+//    count's barrier;
+//  * the rank walks its bucket including itself (a member never precedes itself): no
+//    singleton select, bucket bounds from the word (u << 16 | size << 8 | arrival);
+//  * perm written with buffer stores (one shift per row).
+// LDS: region A = the keys by position (u64 [UMAX]; before the scatter, the u32
+// counters), region B = the words by position (u32 [UMAX]; before them, the u16
+// bucket starts).  UMAX 3,072 with 512 threads: 36 KB, 4 workgroups per CU.
+// ============================================================================
+constexpr int kFastSpare = 16;  // counters of the lanes past U
+template <int BLOCK, int UMAX>
+struct BsFastLds {
+  static constexpr int kA = 8 * UMAX;
+  static constexpr int kB = 4 * UMAX > 2 * (kFastNB + 8) ? 4 * UMAX : 2 * (kFastNB + 8);
+  static constexpr int kBytes = kA + kB;
+  static_assert(4 * (kFastNB + kFastSpare) <= kA, "counters in region A");
+};
+template <int WAVES>
+struct BsFastShared {
+  uint32_t wtot[WAVES];
+  double mn[WAVES], mx[WAVES];  // the in-kernel range (no constants from the join)
+  uint32_t big, nan;
+};
+
+template <int BLOCK, int UMAX, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
+  constexpr int WAVES = BLOCK / 64, ROWS = UMAX / BLOCK, NB = kFastNB;
+  constexpr int MINSUB = NB / 16, MINBASE = kFastMinBase;
+  static_assert(ROWS * BLOCK == UMAX && UMAX <= 65535, "rows of a wave");
+  static_assert(((UMAX - 1) >> 6) < MINSUB, "minimum sub-bucket shift <= 6");
+  static_assert(NB % (4 * BLOCK) == 0, "whole uint4 counter loads per thread");
+  using LD = BsFastLds<BLOCK, UMAX>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LD::kBytes];
+  __shared__ BsFastShared<WAVES> sm;
+  uint64_t* skey = (uint64_t*)lds;               // region A from the scatter on
+  uint32_t* cnt = (uint32_t*)lds;                // region A until the scan
+  uint32_t* sw = (uint32_t*)(lds + LD::kA);      // region B from the second scatter on
+  uint16_t* bk = (uint16_t*)(lds + LD::kA);      // region B until then
+  const int tid = threadIdx.x, lane = tid & 63,
+            wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = __popc(p.methods);
+  const int64_t bid = block_id();
+  const int64_t grp8 = bid >> 3, ngroups = (p.n_queries + 7) / 8;
+  if (grp8 >= ngroups * M) return;
+  // groups of 8 queries (query q on XCD q % 8, where the join wrote it), in reverse
+  // (the join's last-written scores are the likeliest still cached); grp8 / M by a
+  // scalar multiply-high (exact below 2^20 groups)
+  int64_t gq;
+  if (M == 1) gq = grp8;
+  else if (grp8 < (1 << 20)) gq = (int64_t)__umulhi((uint32_t)grp8, 0xFFFFFFFFu / (uint32_t)M + 1u);
+  else gq = grp8 / M;
+  const int64_t q = (ngroups - 1 - gq) * 8 + (bid & 7);
+  const int ms = (int)(grp8 - gq * M);
+  if ((p.methods & QF_LEARNED) && ms == __popc(p.methods & (QF_LEARNED - 1))) return;
+  if (q >= p.n_queries) return;
+  const int U = p.union_count[q];
+  if (U < 1 || U > UMAX) return;  // a status, or fuse_large_kernel's
+  const int64_t base = p.list_off[q * p.R];
+  const int64_t nq = p.list_off[q * p.R + p.R] - base;
+  const double* io = p.fused + (int64_t)ms * p.out_stride + base;
+  const int64_t po = (int64_t)ms * p.out_stride + base;
+  const int rows = (U + BLOCK - 1) / BLOCK;
+  const int wbase = wid * rows * 64;  // this wave's items / positions: [wbase, wbase + rows * 64)
+
+  // ---- loads (past U: 0.0, masked below) --------------------------------------------
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)io, (short)0, U * 8, 0x00020000);
+  const int voff = (wbase + lane) * 8;
+  double v[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j)
+    if (j < rows)  // uniform
+      v[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff + j * 512, 0,
+                                                                             kBufNT));
+  // the counters zeroed while the loads are in flight
+  for (int i = tid; i < (NB + kFastSpare) / 4; i += BLOCK)
+    ((uint4*)cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid == 0) {
+    sm.big = 0u;
+    sm.nan = 0u;
+  }
+  // ---- the key constants: the join's, else computed here ------------------------------
+  double smin = 0.0, smax = 0.0, kc = 0.0;
+  uint64_t w3 = 0ull;
+  if (nq - U >= kPairInfo) {  // uniform
+    const double* inf = io + U;
+    smin = rfl_f64(inf[0]);
+    smax = rfl_f64(inf[1]);
+    kc = rfl_f64(inf[2]);
+    const uint64_t w = ((const uint64_t*)inf)[3];
+    w3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w);
+  }
+  __syncthreads();  // the counters and flags are zero
+  if (w3 == 0ull) {  // uniform: the range of the valid items, reduced over the block
+    double vmn = INFINITY, vmx = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = wbase + j * 64 + lane;
+      if (j < rows && u < U) {
+        vmn = raw_min_f64(vmn, v[j]);
+        vmx = raw_max_f64(vmx, v[j]);
+        nan |= v[j] != v[j];
+      }
+    }
+    vmn = wave_min_f64_dpp(vmn);
+    vmx = wave_max_f64_dpp(vmx);
+    if (ballot(nan) != 0ull && lane == 0) sm.nan = 1u;
+    if (lane == 63) {
+      sm.mn[wid] = vmn;
+      sm.mx[wid] = vmx;
+    }
+    __syncthreads();
+    double a = sm.mn[0], b = sm.mx[0];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) {
+      a = raw_min_f64(a, sm.mn[w]);
+      b = raw_max_f64(b, sm.mx[w]);
+    }
+    smin = rfl_f64(a + 0.0);
+    smax = rfl_f64(b + 0.0);
+    const bool anynan = sm.nan != 0u;
+    if (anynan) smin = smax = __longlong_as_double(0x7FF8000000000000ll);  // never "all equal"
+    const BsKey2 k = bs_key2<MINBASE>(smin, smax, anynan, kFastDeltaShift);
+    kc = rfl_f64(k.c);
+    const uint64_t w = bs_key2_word(k);
+    w3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w);
+  }
+  if (smin == smax) {  // every score equal: first-seen order
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = wbase + j * 64 + lane;
+      if (j < rows && u < U) perm_put(p, po + u, (uint32_t)u);
+    }
+    return;
+  }
+  if (w3 == kPairMark) {  // a range the key cannot take: the fallback pass
+    if (tid == 0) perm_put(p, po, kJsUnsorted);
+    return;
+  }
+  QF_STOP(21, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += (uint32_t)__double2loint(v[j]); return a; },
+          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
+
+  // ---- count --------------------------------------------------------------------------
+  int ush = 0;  // (U - 1) >> ush < MINSUB: the minimum's sub-bucket is MINBASE + (u >> ush)
+  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
+  const uint32_t lane_sub = (uint32_t)lane >> ush;  // (64-aligned row bases: exact split)
+  const uint32_t spare = (uint32_t)NB + ((uint32_t)lane & (kFastSpare - 1u));
+  uint32_t ws[ROWS];  // bucket | arrival << 16
+  uint32_t omax = 0u;
+  auto count_rows = [&](auto cf, double c, uint32_t top, uint32_t scale) __attribute__((always_inline)) {
+    constexpr bool CF = decltype(cf)::value;
+    uint32_t old[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (j < rows) {  // uniform; every row's atomic issued before any result is used
+        const int u = wbase + j * 64 + lane;
+        const double x = CF ? v[j] + c : (v[j] - smin) + c;
+        const uint32_t hx = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
+        const uint32_t key = __umulhi(top - hx, scale);  // < MINBASE, 0 for the largest
+        const uint32_t minb = ((uint32_t)MINBASE + ((uint32_t)(wbase + 64 * j) >> ush)) + lane_sub;
+        uint32_t b = sel_if_eq_f64(v[j], smin, minb, key);
+        b = u < U ? b : spare;
+        ws[j] = b;
+        old[j] = atomicAdd(&cnt[b], 1u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      if (j < rows) {
+        omax = max(omax, old[j]);
+        ws[j] |= old[j] << 16;
+      }
+    }
+  };
+  auto count = [&](double c, uint64_t w) __attribute__((always_inline)) {
+    const uint32_t top = (uint32_t)w & 0x7FFFFFFFu, scale = (uint32_t)(w >> 32);
+    if ((w >> 31) & 1u) count_rows(std::true_type{}, c, top, scale);
+    else count_rows(std::false_type{}, c, top, scale);
+    if (omax >= (uint32_t)kJsBucketMax) sm.big = 1u;  // (benign race: every writer stores 1)
+  };
+  count(kc, w3);
+  __syncthreads();  // the counters are complete
+  if (sm.big) {  // uniform, rare: recount with delta = range / 2^20
+    __syncthreads();  // every thread has read the flag
+    for (int i = tid; i < (NB + kFastSpare) / 4; i += BLOCK)
+      ((uint4*)cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (tid == 0) sm.big = 0u;
+    const BsKey2 k = bs_key2<MINBASE>(smin, smax, false, kFastRetryShift);
+    __syncthreads();
+    if (!k.ok) {  // uniform
+      if (tid == 0) perm_put(p, po, kJsUnsorted);
+      return;
+    }
+    omax = 0u;
+    const uint64_t w = bs_key2_word(k);
+    count(rfl_f64(k.c), ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w));
+    __syncthreads();
+    if (sm.big) {  // uniform: still a bucket above kJsBucketMax — the fallback pass
+      if (tid == 0) perm_put(p, po, kJsUnsorted);
+      return;
+    }
+  }
+  QF_STOP(22, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += ws[j]; return a; },
+          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
+
+  // ---- exclusive scan of the counters -> u16 bucket starts (region B) ------------------
+  {
+    constexpr int kPer = NB / BLOCK;  // 8 (512 threads) or 4 (1,024)
+    uint32_t c[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer / 4; ++i) {
+      const uint4 x = ((const uint4*)cnt)[tid * (kPer / 4) + i];
+      c[4 * i] = x.x; c[4 * i + 1] = x.y; c[4 * i + 2] = x.z; c[4 * i + 3] = x.w;
+    }
+    uint32_t tot = 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t x = c[i];
+      c[i] = tot;
+      tot += x;
+    }
+    const uint32_t incl = wave_incl_scan_dpp(tot);
+    if (lane == 63) sm.wtot[wid] = incl;
+    __syncthreads();  // also: every counter read before the scatter overwrites them
+    uint32_t pre = incl - tot;
+    for (int w = 0; w < wid; ++w) pre += sm.wtot[w];  // wid is wave-uniform: a scalar loop
+    const uint32_t pre2 = pre * 0x10001u;  // (starts <= U < 2^16: no carry between halves)
+    uint32_t pk[kPer / 2];
+#pragma unroll
+    for (int i = 0; i < kPer / 2; ++i) pk[i] = (c[2 * i] | (c[2 * i + 1] << 16)) + pre2;
+    if constexpr (kPer == 8)
+      ((uint4*)bk)[tid] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    else
+      ((uint2*)bk)[tid] = make_uint2(pk[0], pk[1]);
+    if (tid == 0) bk[NB] = (uint16_t)U;
+  }
+  __syncthreads();
+  QF_STOP(23, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += ws[j] + bk[j]; return a; },
+          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
+
+  // ---- scatter: keys by position, then the words over the dead starts ---------------
+  uint32_t pa[ROWS], pw[ROWS];  // position; u << 16 | size << 8 | arrival
+  const uint32_t ul = (uint32_t)(wbase + lane) << 16;
+  auto scatter = [&](auto nn) __attribute__((always_inline)) {
+    constexpr bool NN = decltype(nn)::value;
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int u = wbase + j * 64 + lane;
+      if (j < rows && u < U) {
+        const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
+        const uint32_t st = bk[b], nx = bk[b + 1];
+        const uint32_t pos = st + at;
+        // the rank phase compares integer keys: without negative scores (every C2
+        // fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
+        skey[pos] = NN ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);
+        pa[j] = pos;
+        pw[j] = (ul + ((uint32_t)(64 * j) << 16)) | ((nx - st) << 8) | at;
+      }
+    }
+  };
+  if (smin >= 0.0) scatter(std::true_type{});  // uniform
+  else scatter(std::false_type{});
+  __syncthreads();  // the starts are dead
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int u = wbase + j * 64 + lane;
+    if (j < rows && u < U) sw[pa[j]] = pw[j];
+  }
+  __syncthreads();
+  QF_STOP(24, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += pa[j] + sw[j]; return a; },
+          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
+
+  // ---- rank inside the bucket, in position order --------------------------------------
+  // LDS byte offsets: keys at 8 * position, words at kA + 4 * position; this lane's
+  // row j reads position wbase + lane + 64 j (the row part an instruction offset)
+  uint32_t P[ROWS], uo[ROWS];
+  const unsigned char* kme = lds + 8 * (wbase + lane);
+  const unsigned char* wme = lds + LD::kA + 4 * (wbase + lane);
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) {
+    const int i = wbase + j * 64 + lane;
+    P[j] = 0u;
+    uo[j] = 0u;
+    if (j < rows && i < U) {
+      const uint64_t ki = *(const uint64_t*)(kme + 512 * j);
+      const uint32_t wi = *(const uint32_t*)(wme + 256 * j);  // also the tie-break key:
+      // u in the top bits (distinct), so the word order is the first-seen order
+      const uint32_t lo = (uint32_t)i - (wi & 0xFFu);
+      uint32_t ka = lo * 8u;                                    // the bucket's first key
+      const uint32_t klast = ka + ((wi >> 8) & 0xFFu) * 8u - 8u;  // its last key
+      uint32_t ta = LD::kA + lo * 4u;                           // the first word
+      uint32_t before = 0u;
+      // every member, itself included (it never precedes itself), two per step
+      for (; ka < klast; ka += 16u, ta += 8u) {
+        // two ds_read_b64 (2 LDS cycles each) rather than a ds_read2_b64 (8 cycles)
+        const uint64_t v0 = *(const uint64_t*)(lds + ka);
+        asm volatile("" ::: "memory");
+        const uint64_t v1 = *(const uint64_t*)(lds + ka + 8);
+        const uint32_t t0 = *(const uint32_t*)(lds + ta), t1 = *(const uint32_t*)(lds + ta + 4);
+        before = add_if_precedes(before, ki, wi, v0, t0);
+        before = add_if_precedes(before, ki, wi, v1, t1);
+      }
+      if (ka == klast)
+        before = add_if_precedes(before, ki, wi, *(const uint64_t*)(lds + ka),
+                                 *(const uint32_t*)(lds + ta));
+      P[j] = lo + before;
+      uo[j] = wi >> 16;
+    }
+  }
+  QF_STOP(25, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += P[j] + uo[j]; return a; },
+          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
+  // ---- perm (every row's position before any store) ------------------------------------
+  if (p.perm32) {  // uniform
+    const auto pr = __builtin_amdgcn_make_buffer_rsrc((uint32_t*)p.perm + po, (short)0, U * 4,
+                                                      0x00020000);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int i = wbase + j * 64 + lane;
+      if (j < rows && i < U) __builtin_amdgcn_raw_buffer_store_b32(uo[j], pr, P[j] * 4, 0, kBufNT);
+    }
+  } else {
+    const auto pr = __builtin_amdgcn_make_buffer_rsrc((uint16_t*)p.perm + po, (short)0, U * 2,
+                                                      0x00020000);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+      const int i = wbase + j * 64 + lane;
+      if (j < rows && i < U)
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)uo[j], pr, P[j] * 2, 0, kBufNT);
+    }
+  }
+}
+
+// ============================================================================
 // join_learned_kernel — learned fusion alone (C5: QF_LEARNED is the call's one
 // method), join and sort in one workgroup per query.  The LDS join as join_kernel
 // (JoinM: N <= 5,120, micro-unit scores), then each thread's documents u = j *
@@ -1921,7 +2327,8 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(F
   if (N < 0) return;
   const int U = sh.U;
   if (U > kJsUMax || sh.status) {  // uniform: the separate sort kernels' share
-    store_unsorted_sums<C, 1, kSortLds>(p, sh, N);
+    SlotRange rg;  // (learned fusion alone keeps no ranges)
+    store_unsorted_sums<C, 1, kSortLds>(p, sh, N, rg);
     if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : U;
     return;
   }
@@ -2454,7 +2861,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
                        uint64_t* t_tie, XlScratch* xs) {
   const int tid = threadIdx.x;
   const int R = p.R, TS = 1 << tb;
-  QF_STAMP_INIT();
   if (tid <= R) s_off[tid] = p.list_off[q * R + tid];
   if (tid == 0) *s_status = 0;
   __syncthreads();
@@ -2473,7 +2879,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     s_rden[tid] = 1.0 / s_den[tid];
   }
   __syncthreads();  // s_status
-  QF_STAMP(0);
   // ---- 1. insert: partitioned, else (a partition too large) the global table --------
   if (!xl_partition_insert<KIND>(p, w, base, N, s_off, (uint32_t*)t_key, s_wsum, xs, s_status)) {
   for (int i = tid; i < TS; i += kXlBlock) {
@@ -2538,7 +2943,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
   if (status) atomicMin(s_status, status);
   xl_sync();
   }
-  QF_STAMP(1);
   if (*s_status) {  // uniform
     if (tid == 0) p.union_count[q] = *s_status;
     __syncthreads();
@@ -2586,7 +2990,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     U += tot;
   }
   xl_sync();
-  QF_STAMP(2);
   // ---- 3. groups and sums -------------------------------------------------------
   uint32_t go = 0;
   for (int c0 = 0; c0 < (int)U; c0 += kXlBlock) {
@@ -2598,7 +3001,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     go += tot;
   }
   xl_sync();
-  QF_STAMP(3);
   r = 0;
   for (int e0 = tid; e0 < N; e0 += kXlUnroll * kXlBlock) {
     uint32_t hs[kXlUnroll], u[kXlUnroll];
@@ -2626,7 +3028,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     }
   }
   xl_sync();
-  QF_STAMP(4);
   const int methods = p.methods;
   const ListConsts lc{s_off, s_w, s_min, s_den, s_rden};
   for (int u = tid; u < (int)U; u += kXlBlock) {
@@ -2641,7 +3042,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     acc.store(p, methods, (double)(ge - gs), base + u);
   }
   xl_sync();
-  QF_STAMP(5);
   // ---- 4. sort every method slot (unions the LDS sorts cannot hold) ---------------
   if ((int)U <= sort_min) {  // uniform: the LDS sort kernels that follow take it
     if (tid == 0) p.union_count[q] = (int)U;
@@ -2657,7 +3057,6 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
     const bool done = by_docid
                           ? xl_bsort<true>(p, io, base, (int)U, po, w, (uint32_t*)t_key, s_wsum, xs)
                           : xl_bsort<false>(p, io, base, (int)U, po, w, (uint32_t*)t_key, s_wsum, xs);
-    QF_STAMP(10);
     if (done) continue;  // uniform
     for (int i = tid; i < NP; i += kXlBlock) {
       uint64_t k = ~0ull, t = ~0ull;  // padding sorts last
@@ -2671,9 +3070,7 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
       w.stie[i] = t;
     }
     xl_sync();
-    QF_STAMP(6);
     xl_tile_pass(w.skey, w.stie, t_key, t_tie, NP, T, 0, 0);  // every stage k <= T
-    QF_STAMP(7);
     for (int kk = 2 * T; kk <= NP; kk <<= 1) {
       for (int j = kk >> 1; j >= T; j >>= 1) {
         for (int t = tid; t < NP / 2; t += kXlBlock) {
@@ -2686,12 +3083,10 @@ __device__ __forceinline__ void xl_one(const FuseParams& p, int64_t q, const XlW
       }
       xl_tile_pass(w.skey, w.stie, t_key, t_tie, NP, T, kk, T >> 1);
     }
-    QF_STAMP(8);
     for (int i = tid; i < (int)U; i += kXlBlock) {
       perm_put(p, po + i, (uint32_t)(w.stie[i] & 0xFFFFFFFFu));
     }
     xl_sync();
-    QF_STAMP(9);
   }
   if (tid == 0) p.union_count[q] = (int)U;
   __syncthreads();
@@ -2863,8 +3258,8 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
     }
     const int M = __builtin_popcount((unsigned)p.methods);
     if (p.methods & ~QF_LEARNED)
-      hipLaunchKernelGGL((bsort_kernel<512, 12, false>), grid_for((p.n_queries + 7) / 8 * 8 * M),
-                         dim3(512), 0, st, p);
+      hipLaunchKernelGGL((bsort_fast_kernel<512, kJsUMax, 8>),
+                         grid_for((p.n_queries + 7) / 8 * 8 * M), dim3(512), 0, st, p);
     if ((p.methods & QF_LEARNED) && !learned_only)
       hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),
                          dim3(512), 0, st, p);
@@ -2961,16 +3356,5 @@ hipError_t topk_launch(int64_t n_queries, int32_t R, const int64_t* list_off,
   return hipGetLastError();
 }
 
-#ifdef QF_STAMPS
-extern "C" int qf_debug_stamps(unsigned long long* host, int n, int clear) {
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) != hipSuccess)
-    return 1;
-  if (clear) {
-    static unsigned long long zeros[kStampBlocks * kStampSlots];
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zeros, sizeof zeros) != hipSuccess) return 1;
-  }
-  return 0;
-}
-#endif
 
 }  // namespace qf

@@ -93,22 +93,6 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // owns prefix i); the sums Java forms left to right are serial chains, and those
 // run batched: one wave, one lane per (list, chain), so a chain costs one lane
 // of one instruction instead of a whole wave's.
-#ifdef QF_STAMPS
-// Diagnostic build only (tools/qpp_stamps.py): per-workgroup phase cycles of wave 0.
-constexpr int kQppStampBlocks = 4096, kQppStampSlots = 8;
-__device__ unsigned long long g_qpp_stamps[kQppStampBlocks * kQppStampSlots];
-#define QPP_STAMP_INIT() unsigned long long _qs_prev = __builtin_amdgcn_s_memtime()
-#define QPP_STAMP(slot)                                                             \
-  do {                                                                              \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();                     \
-    if (threadIdx.x == 0 && block_id() < kQppStampBlocks)                           \
-      g_qpp_stamps[block_id() * kQppStampSlots + (slot)] += _t - _qs_prev;          \
-    _qs_prev = _t;                                                                  \
-  } while (0)
-#else
-#define QPP_STAMP_INIT()
-#define QPP_STAMP(slot)
-#endif
 
 constexpr int kQppLists = 8;
 constexpr int kQppBlock = 64 * kQppLists;
@@ -132,7 +116,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t l = block_id() * kQppLists + w;
   const bool lv = l < n_lists;  // every wave stays for the barriers
-  QPP_STAMP_INIT();
   int k = 0;
   int64_t a = 0;
   if (lv) {
@@ -161,7 +144,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     s_fmask[w] = fmask;
   }
   __syncthreads();
-  QPP_STAMP(1);
 
   // ---- B (lane = list): the serial chains that need only rsv, on two waves at once.
   // The serial loops run to kQppK unrolled (rows are kRow long; values past k
@@ -214,7 +196,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   }
   if (w <= 1) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
-  QPP_STAMP(2);
 
   // ---- C (each list's wave): squared deviations around each prefix mean
   // (lane i = prefix i): simple sum -> NQC of the prefix (NQC, CumNQC),
@@ -273,7 +254,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   const double mx = wave_max(act ? x : -INFINITY);
   const double mn = wave_min(act ? x : INFINITY);
   __syncthreads();
-  QPP_STAMP(3);
 
   // ---- D (wave 0, lane = list * 8 + chain): the left-to-right sums, all chains
   // of all lists at once
@@ -311,7 +291,6 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   }
   if (w <= 1) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
-  QPP_STAMP(4);
 
   if (!lv) return;
   double* o = out + l * kQppCols;
@@ -616,16 +595,3 @@ hipError_t qpp_features_launch(const int64_t* micro, int64_t Q, int32_t R, const
 
 }  // namespace qf
 
-#ifdef QF_STAMPS
-extern "C" int qf_debug_qpp_stamps(unsigned long long* host, int n, int clear) {
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(qf::g_qpp_stamps), sizeof(unsigned long long) * n) !=
-      hipSuccess)
-    return 1;
-  if (clear) {
-    static unsigned long long zeros[qf::kQppStampBlocks * qf::kQppStampSlots];
-    if (hipMemcpyToSymbol(HIP_SYMBOL(qf::g_qpp_stamps), zeros, sizeof zeros) != hipSuccess)
-      return 1;
-  }
-  return 0;
-}
-#endif

@@ -92,9 +92,15 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     return LIB_PATH
 
 
-def build_variant(out: Path, extra_flags) -> Path:
-    """Development builds (e.g. -DQF_STAMPS for tools/stamps.py) from the same sources."""
-    cmd = [_hipcc(), *FLAGS, *extra_flags, "-o", str(out)] + [str(CSRC / s) for s in SOURCES]
+DEV_HOOKS = ROOT.parent / "tools" / "dev" / "qf_dev_hooks.h"
+
+
+def build_variant(out: Path, extra_flags, dev: bool = False) -> Path:
+    """Development builds from the same sources (A/B of -D knobs; dev=True force-includes
+    tools/dev/qf_dev_hooks.h, whose QF_STOP stop points -DQF_STOP_AT=<phase> enables —
+    the library itself never includes it)."""
+    pre = ["-include", str(DEV_HOOKS)] if dev else []
+    cmd = [_hipcc(), *FLAGS, *pre, *extra_flags, "-o", str(out)] + [str(CSRC / s) for s in SOURCES]
     subprocess.run(cmd, check=True)
     return out
 

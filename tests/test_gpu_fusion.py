@@ -800,15 +800,18 @@ def test_caller_owned_workspace(gpu, share):
             assert fz[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)
 
 
+@pytest.mark.parametrize("R,K", [(5, 40), (5, 160), (5, 400), (20, 50)])
 @pytest.mark.parametrize("mode,qidx", [("minmax", 5), ("minmax", -1), ("minmax", 0),
                                        ("zscore", 5), ("zscore", -1)])
-def test_fuse_qpp_weights_in_kernel_equal_normalize_then_fuse(gpu, mode, qidx):
+def test_fuse_qpp_weights_in_kernel_equal_normalize_then_fuse(gpu, mode, qidx, R, K):
     """qf_fuse_qpp (the W-* weights computed in the join from the raw QPP predictors
     and their column statistics) == qf_qpp_normalize's weights fed to qf_fuse, bit
     for bit: union sizes, every method's fused scores and perm; absent lists (weight
-    from a 0.0 value), a constant QPP column."""
+    from a 0.0 value), a constant QPP column.  Every join that computes list_weight:
+    the one-wave join (R*K <= 320), the 256-thread one (<= 1,024), the 512-thread one,
+    and the workspace kernel's (R = 20 > 16 runs)."""
     from qppfuse import engine
-    Q, R, K = 300, 5, 400
+    Q = 300
     off, docid, raw = engine.synth_runs(11, Q, R, K)
     lens = torch.diff(off).cpu().numpy()
     # empty some lists: rebuild the run set without their entries
@@ -841,3 +844,70 @@ def test_fuse_qpp_weights_in_kernel_equal_normalize_then_fuse(gpu, mode, qidx):
         s, u = int(lo[q * R]), int(uc[q])
         assert fa[:, s:s + u].tobytes() == fb[:, s:s + u].tobytes(), q
         assert np.array_equal(pa[:, s:s + u], pb[:, s:s + u]), q
+
+
+def _bs_key2(smin, smax, shift=8, minbase=3840):
+    """Python restatement of qf_fuse.hip's bs_key2 (the bucket key's constants)."""
+    import math
+    import struct
+    hi = lambda x: struct.unpack("<Q", struct.pack("<d", x))[0] >> 32
+    rng = smax - smin
+    delta = math.ldexp(rng, -shift)
+    if not (math.isfinite(rng) and delta > 0.0):
+        return None
+    c = delta - smin
+    cform = math.isfinite(c) and (smin + c) >= 0.5 * delta
+    xmin = smin + c if cform else delta
+    xmax = smax + c if cform else rng + delta
+    if not math.isfinite(xmax):
+        return None
+    b0, top = hi(xmin), hi(xmax)
+    span = (top - b0 + 1) & 0xFFFFFFFF
+    scale = 0xFFFFFFFF if span <= minbase else int(minbase * 4294967296.0 / span) - 1
+    return (c if cform else delta), (scale << 32) | (int(cform) << 31) | top
+
+
+@pytest.mark.parametrize("methods", [ALL, ["combsum", "rrf"], ["wcombsum"], ["rrf"],
+                                     ["combsum", "wcombsum"]])
+def test_join_leaves_the_sort_key_constants(gpu, methods):
+    """Round 5: the join reduces every method slot's min / max over the query's documents
+    (register exchanges across the wave, then across waves) and leaves the bucket sort's
+    key constants at fused[slot][base + U .. + 4) when the query has 4 spare slots:
+    [min, max, c, top | cform << 31 | scale << 32] — exactly the values' extremes (-0.0
+    folded) and bs_key2's constants; a run-time method set (no compile-time slots)
+    leaves w3 = 0 (the sort computes them).  The fused outputs are checked elsewhere."""
+    from qppfuse import engine
+    Q, R, K = 48, 5, 1000
+    off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=5)
+    rng = np.random.default_rng(3)
+    w = torch.from_numpy(rng.random(Q * R).round(6)).to(gpu)
+    w[:R] = 0.0  # query 0: zero weights, outside the sums' division-free fast path
+    out = engine.fuse(off, docid, micro, R, methods, rrf_k=60, weights=w, max_entries=R * K)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    uc = out.union_count.cpu().numpy()
+    fz = out.fused.cpu().numpy()
+    compile_time = methods in (ALL, ["combsum", "rrf"], ["wcombsum"], ["rrf"])
+    checked = 0
+    for q in range(Q):
+        b, n, N = off_h[q * R], uc[q], off_h[q * R + R] - off_h[q * R]
+        if N - n < 4:
+            continue
+        for m in range(len(methods)):
+            vals = fz[m, b:b + n]
+            info = fz[m, b + n:b + n + 4]
+            w3 = int(info[3:4].view(np.uint64)[0])
+            if not compile_time or q == 0:  # the sort computes the constants itself
+                assert w3 == 0, (q, m)
+                continue
+            smin, smax = float(vals.min()) + 0.0, float(vals.max()) + 0.0
+            assert info[0].tobytes() == np.float64(smin).tobytes(), (q, m)
+            assert info[1].tobytes() == np.float64(smax).tobytes(), (q, m)
+            k = _bs_key2(smin, smax)
+            if k is None:
+                assert w3 == 0xFFFFFFFFFFFFFFFF, (q, m)
+            else:
+                assert info[2].tobytes() == np.float64(k[0]).tobytes(), (q, m)
+                assert w3 == k[1], (q, m, hex(w3), hex(k[1]))
+            checked += 1
+    assert checked >= (Q - 1) * len(methods) if compile_time else True
