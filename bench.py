@@ -95,8 +95,13 @@ def parse():
     ap.add_argument("--native-sample", type=int, default=400,
                     help="queries timed through the C oracle (0 = skip)")
     ap.add_argument("--check", type=int, default=8, help="queries checked bit-exact vs oracle")
-    ap.add_argument("--ndcg-sample", type=int, default=256,
+    ap.add_argument("--ndcg-sample", type=int, default=1000,
                     help="queries whose NDCG@10 is recomputed on the CPU reference path")
+    ap.add_argument("--generator", choices=["nq", "legacy"], default="nq",
+                    help="synthetic runs: nq = SURVEY.md §8(d) (qf_synth_runs_nq: 2K shared pool "
+                         "at p 0.5 + the 2,681,468-id NQ pool, Gamma / Beta / ln-Beta scores, the "
+                         "real NQ test qrels planted at Geometric(0.15) ranks); legacy = rounds "
+                         "1-4's exp-decay generator (qf_synth_runs)")
     a = ap.parse_args()
     a.wl = WORKLOADS[a.workload]
     if a.qpp_index is None:
@@ -107,6 +112,39 @@ def parse():
     if a.k is None:
         a.k = a.wl.get("k", 1000)
     return a
+
+
+_NQ_QRELS = None
+
+
+def nq_qrels():
+    """The reference's NQ test qrels (tests/golden/nq_qrels_test.tsv.gz, a data fixture of
+    data/nq/BEIR-nq/qrels/test.tsv): CSR over test0 .. test3451 of corpus ids (doc{n} ->
+    n); every judgment is rel 1."""
+    global _NQ_QRELS
+    if _NQ_QRELS is None:
+        import gzip
+        rows = gzip.decompress((ROOT / "tests" / "golden" / "nq_qrels_test.tsv.gz")
+                               .read_bytes()).decode().splitlines()[1:]
+        per = {}
+        for line in rows:
+            q, d, _ = line.split("\t")
+            per.setdefault(int(q[4:]), []).append(int(d[3:]))
+        n = max(per) + 1
+        off = np.zeros(n + 1, np.int64)
+        off[1:] = np.cumsum([len(per.get(q, ())) for q in range(n)])
+        doc = np.array([d for q in range(n) for d in per.get(q, ())], np.uint32)
+        _NQ_QRELS = (off, doc)
+    return _NQ_QRELS
+
+
+def gen_runs(args, q_begin: int, Q: int, R: int, K: int):
+    """The bench's synthetic runs on device: (list_off, docid, raw score)."""
+    from qppfuse import engine
+    if args.generator == "nq":
+        qo, qd = nq_qrels()
+        return engine.synth_runs_nq(q_begin, Q, R, K, qo, qd, seed=SEED)
+    return engine.synth_runs(q_begin, Q, R, K, seed=SEED)
 
 
 def launch_ranks(args, script=None, argv=None) -> int:
@@ -193,7 +231,7 @@ class Pipeline:
             self.shard_sizes = [e - b for b, e in (shard_range(wl["queries"], world, r)
                                                    for r in range(world))]
         self.methods = args.methods
-        self.off, self.docid, self.raw = engine.synth_runs(self.q_begin, Q, R, K, seed=SEED)
+        self.off, self.docid, self.raw = gen_runs(args, self.q_begin, Q, R, K)
         self.qids = None
         if args.workload == "c4" and args.queries is None:
             self.qids = c4_queries()[0][self.q_begin:self.q_begin + Q]
@@ -249,7 +287,7 @@ class Pipeline:
         through this step's kernels with the step's QPP min / max (after the
         all-reduce: every rank normalises with the same global values)."""
         e, a, R, K = self.engine, self.args, self.R, self.K
-        off, docid, raw = e.synth_runs(q_begin + start, n, R, K, seed=SEED)
+        off, docid, raw = gen_runs(a, q_begin + start, n, R, K)
         _, micro = e.minmax_per_query(raw, off, want_norm=False)
         w, qppw = None, None
         if a.wl["qpp"]:
@@ -372,9 +410,19 @@ class Pipeline:
         return reads + writes, float(uc.mean())
 
 
-def synth_qrels(q_begin: int, Q: int, K: int):
-    """Judged documents of the synthetic queries: 1-3 pool documents each (the first
-    rel 2, the others rel 1) — ids as qf_synth_runs draws pool documents."""
+def synth_qrels(q_begin: int, Q: int, K: int, generator: str = "nq"):
+    """Judged documents of the synthetic queries (qrel_off, docid, rel).  nq: query q's
+    are the NQ test judgments of test{q mod 3452} (the documents qf_synth_runs_nq
+    planted), rel 1.  legacy: 1-3 pool documents each (the first rel 2, the others rel
+    1) — ids as qf_synth_runs draws pool documents."""
+    if generator == "nq":
+        off, doc = nq_qrels()
+        qq = np.arange(q_begin, q_begin + Q, dtype=np.int64) % (len(off) - 1)
+        n = off[qq + 1] - off[qq]
+        qo = np.zeros(Q + 1, np.int64)
+        qo[1:] = np.cumsum(n)
+        idx = np.repeat(off[qq], n) + (np.arange(qo[-1]) - np.repeat(qo[:-1], n))
+        return qo, doc[idx].astype(np.uint32), np.ones(int(qo[-1]), np.int32)
     qg = np.arange(q_begin, q_begin + Q, dtype=np.int64)
     nrel = 1 + qg % 3
     qo = np.zeros(Q + 1, np.int64)
@@ -389,7 +437,7 @@ def synth_qrels(q_begin: int, Q: int, K: int):
 def ndcg_device(p: Pipeline):
     """NDCG@10 of every fused run on device (qf_eval, scores as the .res text)."""
     from qppfuse.evaluation import evaluate_device
-    qo, qd, qr = synth_qrels(p.q_begin, p.Q, p.K)
+    qo, qd, qr = synth_qrels(p.q_begin, p.Q, p.K, p.args.generator)
     t = lambda a: torch.from_numpy(a).to(p.dev)
     qdev = (t(qo), t(qd.view(np.int32)), t(qr))
     o = p.out
@@ -411,7 +459,7 @@ def ndcg_delta(p: Pipeline, dev_vals, nq: int):
     from oracle import _loader as coracle
     h = host_sample(p, nq)
     sc = h["micro"].astype(np.float64) / 1e6
-    qo, qd, qr = synth_qrels(p.q_begin, nq, p.K)
+    qo, qd, qr = synth_qrels(p.q_begin, nq, p.K, p.args.generator)
     worst_q, worst_mean = 0.0, 0.0
     for m, name in enumerate(p.methods):
         if name not in METHODS:
@@ -780,11 +828,18 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "strong" if args.wl["total"] and args.queries is None else "weak",
             "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (on-device counter-based generator, DESIGN.md)",
+            "data": ("synthetic: SURVEY.md §8(d) generator (qf_synth_runs_nq, DESIGN.md §4.5): "
+                     "per list 1000 distinct ids, p 0.5 from a 2K shared pool else the 2,681,468 "
+                     "NQ ids; BM25/Splade Gamma(2,6)+5, BGE/BM25_TCT 0.5+0.4 Beta(5,2), "
+                     "BM25_MonoT5 ln Beta(5,2), sorted + 1e-6 tie-breaker; the real NQ test "
+                     "qrels (4,201) planted at Geometric(0.15) ranks, p_r 0.9/0.5/0.9/0.8/0.9"
+                     if args.generator == "nq" else
+                     "synthetic (rounds 1-4 exp-decay generator, qf_synth_runs)"),
             "config": {"workload": args.wl["desc"],
                        "queries_per_gpu": p.Q, "retrievers": args.retrievers,
                        "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": p.methods,
                        "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1),
+                       "generator": args.generator,
                        "gather_topk_to_rank0": args.gather_topk,
                        "qids": (None if p.qids is None else
                                 f"real BEIR test qids, namespaced: {p.qids[0]} .. {p.qids[-1]}"),

@@ -202,6 +202,8 @@ int qf_qpp_features(const int64_t* micro, int64_t n_queries, int32_t n_retriever
  *   so rank i of query q is union_docid[b + perm[b + i]] with score
  *   fused[b + perm[b + i]], b = list_off[q*R] (+ m*out_stride for perm / fused).
  *   The scores are written once, by the join; the sort writes only perm.
+ *   Slots [b + U_q, b + N_q) of a query's fused / perm rows (N_q its entries) are
+ *   scratch: the join may leave the sort's key constants there.
  */
 int qf_fuse(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
             const uint32_t* docid, const void* score, int32_t score_kind,
@@ -434,6 +436,23 @@ int qf_eval(int64_t n_queries, const int64_t* q_base, int32_t base_stride,
 int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
                   uint64_t seed, double p_shared, int64_t* list_off, uint32_t* docid,
                   double* score, void* stream);
+
+/*
+ * Benchmark / test support: the synthetic runs SURVEY.md §8(d) specifies — per
+ * query and retriever (BGE, BM25, BM25_MonoT5, BM25_TCT, Splade order) K distinct
+ * docids, each with probability 0.5 from the query's shared pool of 2K NQ corpus ids
+ * else from the rest of the 2,681,468; raw scores sorted descending + 1e-6 * (K - 1 -
+ * rank): Gamma(2, 6) + 5 (BM25, Splade), 0.5 + 0.4 Beta(5, 2) (BGE, BM25_TCT),
+ * ln Beta(5, 2) - 0.001 (BM25_MonoT5, negative); the judged documents of qrel query q mod
+ * n_qrel_queries (device CSR qrel_off[n+1] / qrel_doc: corpus ids) planted with
+ * probability {0.9, 0.5, 0.9, 0.8, 0.9} at Geometric(0.15) ranks.  Counter-based
+ * (Philox4x32-10 keyed by seed): any query range regenerates independently;
+ * oracle/synth_oracle.c regenerates it bit for bit.  1 <= k <= 4096.
+ */
+int qf_synth_runs_nq(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
+                     uint64_t seed, const int64_t* qrel_off, const uint32_t* qrel_doc,
+                     int64_t n_qrel_queries, int64_t* list_off, uint32_t* docid, double* score,
+                     void* stream);
 
 /*
  * Measurement support (bench.py's roofline): a device-to-device streaming copy of

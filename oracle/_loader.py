@@ -13,7 +13,8 @@ _lib = None
 
 
 def build() -> Path:
-    srcs = [HERE / "fusion_oracle.c", HERE / "qpp_oracle.c", HERE / "eval_oracle.c"]
+    srcs = [HERE / "fusion_oracle.c", HERE / "qpp_oracle.c", HERE / "eval_oracle.c",
+            HERE / "synth_oracle.c"]
     if not LIB.exists() or any(s.stat().st_mtime > LIB.stat().st_mtime for s in srcs):
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB
@@ -33,6 +34,11 @@ def lib() -> C.CDLL:
         _lib.oracle_eval.argtypes = [i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
         _lib.oracle_qpp_raw.restype = None
         _lib.oracle_qpp_raw.argtypes = [vp, vp, i64, vp, vp, vp, vp]
+        _lib.oracle_synth_runs_nq.restype = C.c_int
+        _lib.oracle_synth_runs_nq.argtypes = [i64, i64, i32, i32, C.c_uint64, vp, vp, i64, vp, vp,
+                                              vp]
+        _lib.oracle_det_log.restype = C.c_double
+        _lib.oracle_det_log.argtypes = [C.c_double]
     return _lib
 
 
@@ -113,3 +119,24 @@ def evaluate(off, docid, score, qrel_off, qrel_docid, qrel_rel, measures, text=F
     if rc != 0:
         raise MemoryError("oracle_eval")
     return out
+
+
+def synth_runs_nq(q_begin, n_queries, R, K, seed, qrel_off, qrel_doc):
+    """CPU regeneration of qf_synth_runs_nq (oracle/synth_oracle.c): list_off, docid,
+    raw scores of lists [q_begin, q_begin + n_queries) x R, bit for bit."""
+    qrel_off = np.ascontiguousarray(qrel_off, dtype=np.int64)
+    qrel_doc = np.ascontiguousarray(qrel_doc, dtype=np.uint32)
+    n = int(n_queries) * int(R)
+    off = np.zeros(n + 1, np.int64)
+    doc = np.zeros(n * int(K), np.uint32)
+    sc = np.zeros(n * int(K), np.float64)
+    rc = lib().oracle_synth_runs_nq(int(q_begin), int(n_queries), int(R), int(K), int(seed),
+                                    _p(qrel_off), _p(qrel_doc), len(qrel_off) - 1, _p(off),
+                                    _p(doc), _p(sc))
+    if rc:
+        raise MemoryError("oracle_synth_runs_nq")
+    return off, doc, sc
+
+
+def det_log(x: float) -> float:
+    return float(lib().oracle_det_log(float(x)))

@@ -525,6 +525,21 @@ int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int3
                "qf_synth_runs");
 }
 
+int qf_synth_runs_nq(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
+                     uint64_t seed, const int64_t* qrel_off, const uint32_t* qrel_doc,
+                     int64_t n_qrel_queries, int64_t* list_off, uint32_t* docid, double* score,
+                     void* stream) {
+  if (q_begin < 0 || n_queries < 0 || n_retrievers <= 0 || k <= 0 || k > 4096 ||
+      n_qrel_queries < 0 || !list_off || (n_queries > 0 && (!docid || !score)) ||
+      (n_qrel_queries > 0 && (!qrel_off || !qrel_doc)))
+    return fail(QF_EINVAL, "qf_synth_runs_nq: bad arguments (1 <= k <= 4096)");
+  if (2 * (int64_t)k >= 2681468)
+    return fail(QF_EINVAL, "qf_synth_runs_nq: k too large for the NQ id space");
+  return check(qf::synth_nq_launch(q_begin, n_queries, n_retrievers, k, seed, qrel_off, qrel_doc,
+                                   n_qrel_queries, list_off, docid, score, (hipStream_t)stream),
+               "qf_synth_runs_nq");
+}
+
 int qf_stream_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   if (nbytes < 0 || (nbytes > 0 && (!dst || !src)) || (nbytes & 15) ||
       (((uintptr_t)dst | (uintptr_t)src) & 15))

@@ -1083,7 +1083,18 @@ __device__ __forceinline__ BsKey2 bs_key2(double smin, double smax, bool nan, in
 __device__ __forceinline__ uint64_t bs_key2_word(const BsKey2& k) {
   return k.ok ? ((uint64_t)k.scale << 32) | ((uint64_t)k.cform << 31) | k.top : kPairMark;
 }
+// two configurations (bsort_fast_kernel): unions up to kJsUMax with 2^12 buckets, and
+// (kJsUMax, kFastUMaxL] — SURVEY §8(d)'s C2 unions, ~4,030 — with 2^13
 constexpr int kFastBits = 12, kFastNB = 1 << kFastBits, kFastMinBase = kFastNB - kFastNB / 16;
+constexpr int kFastBitsL = 13, kFastNBL = 1 << kFastBitsL,
+              kFastMinBaseL = kFastNBL - kFastNBL / 16;
+constexpr int kFastUMaxL = 5120;
+#ifndef QF_DEV_SORT_UNIFIED  // development A/B knob (tools/dev): one configuration for all U
+#define QF_DEV_SORT_UNIFIED 0
+#endif
+#ifndef QF_DEV_BIG_CFG  // development A/B knob: the configuration of unions above 3,072
+#define QF_DEV_BIG_CFG 0
+#endif
 constexpr int kFastDeltaShift = 8;   // delta = range / 2^8 (tools/bsort_sim.py, round 3)
 constexpr int kFastRetryShift = 20;  // the recount after a bucket overflow
 
@@ -1173,7 +1184,8 @@ __device__ __forceinline__ void pair_info(const FuseParams& p, JoinShared<C, KIN
     if ((lane & 3) == 0 && (lane >> 2) < M) {
       const int s = lane >> 2;
       const double smin = x + 0.0, smax = -nmax + 0.0;  // -0.0 folded into +0.0
-      const BsKey2 k = bs_key2<kFastMinBase>(smin, smax, false, kFastDeltaShift);
+      const BsKey2 k = U <= 3072 ? bs_key2<kFastMinBase>(smin, smax, false, kFastDeltaShift)
+                                 : bs_key2<kFastMinBaseL>(smin, smax, false, kFastDeltaShift);
       double* o = p.fused + s * p.out_stride + at;
       o[0] = smin;
       o[1] = smax;
@@ -1406,7 +1418,10 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
       const int64_t q = idx / M;
       const int U = p.union_count[q];
       bool take = U >= umin && U <= C::kUMax;
-      if (FB && U > 1 && U <= kJsUMax)
+      // the fallback pass: a pair within a bucket sort's reach is taken when it marked
+      // it (learned fusion's docid-tie sort reaches kJsUMax, the others kFastUMaxL)
+      const int reach = slot_method(p.methods, (int)(idx % M)) == 6 ? kJsUMax : kFastUMaxL;
+      if (FB && U > 1 && U <= reach)
         take = perm_get(p, (idx % M) * p.out_stride + p.list_off[q * p.R]) == kJsUnsorted;
       if (take) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
     }
@@ -1976,12 +1991,16 @@ __global__ __launch_bounds__(BLOCK, BYDOC ? 6 : INLINE_FB ? 7 : 8) void bsort_ke
 // bucket starts).  UMAX 3,072 with 512 threads: 36 KB, 4 workgroups per CU.
 // ============================================================================
 constexpr int kFastSpare = 16;  // counters of the lanes past U
-template <int BLOCK, int UMAX>
+template <int UMAX, int BITS, bool S32>
 struct BsFastLds {
-  static constexpr int kA = 8 * UMAX;
-  static constexpr int kB = 4 * UMAX > 2 * (kFastNB + 8) ? 4 * UMAX : 2 * (kFastNB + 8);
+  static constexpr int kNB = 1 << BITS;
+  // one position more than UMAX: the sentinel at position U (see the rank phase);
+  // S32: u32 bucket starts (one ds_read2_b32 for a bucket's start and end)
+  static constexpr int kA = 8 * (UMAX + 2);
+  static constexpr int kStarts = (S32 ? 4 : 2) * (kNB + 8);
+  static constexpr int kB = 4 * (UMAX + 2) > kStarts ? 4 * (UMAX + 2) : kStarts;
   static constexpr int kBytes = kA + kB;
-  static_assert(4 * (kFastNB + kFastSpare) <= kA, "counters in region A");
+  static_assert(4 * (kNB + kFastSpare) <= kA, "counters in region A");
 };
 template <int WAVES>
 struct BsFastShared {
@@ -1990,20 +2009,23 @@ struct BsFastShared {
   uint32_t big, nan;
 };
 
-template <int BLOCK, int UMAX, int MINW>
+// UMIN < U <= UMAX of the pairs this configuration sorts; BITS: 2^BITS buckets (the
+// last 1/16 the minimum's sub-buckets); S32: u32 bucket starts.
+template <int BLOCK, int UMIN, int UMAX, int BITS, bool S32, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
-  constexpr int WAVES = BLOCK / 64, ROWS = UMAX / BLOCK, NB = kFastNB;
-  constexpr int MINSUB = NB / 16, MINBASE = kFastMinBase;
+  constexpr int WAVES = BLOCK / 64, ROWS = UMAX / BLOCK, NB = 1 << BITS;
+  constexpr int MINSUB = NB / 16, MINBASE = NB - MINSUB;
   static_assert(ROWS * BLOCK == UMAX && UMAX <= 65535, "rows of a wave");
   static_assert(((UMAX - 1) >> 6) < MINSUB, "minimum sub-bucket shift <= 6");
   static_assert(NB % (4 * BLOCK) == 0, "whole uint4 counter loads per thread");
-  using LD = BsFastLds<BLOCK, UMAX>;
+  using LD = BsFastLds<UMAX, BITS, S32>;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LD::kBytes];
   __shared__ BsFastShared<WAVES> sm;
   uint64_t* skey = (uint64_t*)lds;               // region A from the scatter on
   uint32_t* cnt = (uint32_t*)lds;                // region A until the scan
   uint32_t* sw = (uint32_t*)(lds + LD::kA);      // region B from the second scatter on
-  uint16_t* bk = (uint16_t*)(lds + LD::kA);      // region B until then
+  uint16_t* bk = (uint16_t*)(lds + LD::kA);      // region B until then (u16 starts)
+  uint32_t* bk32 = (uint32_t*)(lds + LD::kA);    // (S32: u32 starts)
   const int tid = threadIdx.x, lane = tid & 63,
             wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = __popc(p.methods);
@@ -2022,7 +2044,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
   if ((p.methods & QF_LEARNED) && ms == __popc(p.methods & (QF_LEARNED - 1))) return;
   if (q >= p.n_queries) return;
   const int U = p.union_count[q];
-  if (U < 1 || U > UMAX) return;  // a status, or fuse_large_kernel's
+  if (U < 1 || U <= UMIN || U > UMAX) return;  // a status, or another kernel's
   const int64_t base = p.list_off[q * p.R];
   const int64_t nq = p.list_off[q * p.R + p.R] - base;
   const double* io = p.fused + (int64_t)ms * p.out_stride + base;
@@ -2195,15 +2217,27 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
     __syncthreads();  // also: every counter read before the scatter overwrites them
     uint32_t pre = incl - tot;
     for (int w = 0; w < wid; ++w) pre += sm.wtot[w];  // wid is wave-uniform: a scalar loop
-    const uint32_t pre2 = pre * 0x10001u;  // (starts <= U < 2^16: no carry between halves)
-    uint32_t pk[kPer / 2];
+    if constexpr (S32) {
 #pragma unroll
-    for (int i = 0; i < kPer / 2; ++i) pk[i] = (c[2 * i] | (c[2 * i + 1] << 16)) + pre2;
-    if constexpr (kPer == 8)
-      ((uint4*)bk)[tid] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    else
-      ((uint2*)bk)[tid] = make_uint2(pk[0], pk[1]);
-    if (tid == 0) bk[NB] = (uint16_t)U;
+      for (int i = 0; i < kPer / 4; ++i)
+        ((uint4*)bk32)[tid * (kPer / 4) + i] =
+            make_uint4(pre + c[4 * i], pre + c[4 * i + 1], pre + c[4 * i + 2], pre + c[4 * i + 3]);
+      if (tid == 0) bk32[NB] = (uint32_t)U;
+    } else {
+      const uint32_t pre2 = pre * 0x10001u;  // (starts <= U < 2^16: no carry between halves)
+      uint32_t pk[kPer / 2];
+#pragma unroll
+      for (int i = 0; i < kPer / 2; ++i) pk[i] = (c[2 * i] | (c[2 * i + 1] << 16)) + pre2;
+      if constexpr (kPer >= 8) {
+#pragma unroll
+        for (int i = 0; i < kPer / 8; ++i)
+          ((uint4*)bk)[tid * (kPer / 8) + i] =
+              make_uint4(pk[4 * i], pk[4 * i + 1], pk[4 * i + 2], pk[4 * i + 3]);
+      } else {
+        ((uint2*)bk)[tid] = make_uint2(pk[0], pk[1]);
+      }
+      if (tid == 0) bk[NB] = (uint16_t)U;
+    }
   }
   __syncthreads();
   QF_STOP(23, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += ws[j] + bk[j]; return a; },
@@ -2219,7 +2253,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
       const int u = wbase + j * 64 + lane;
       if (j < rows && u < U) {
         const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
-        const uint32_t st = bk[b], nx = bk[b + 1];
+        const uint32_t st = S32 ? bk32[b] : bk[b], nx = S32 ? bk32[b + 1] : bk[b + 1];
         const uint32_t pos = st + at;
         // the rank phase compares integer keys: without negative scores (every C2
         // fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
@@ -2236,6 +2270,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
   for (int j = 0; j < ROWS; ++j) {
     const int u = wbase + j * 64 + lane;
     if (j < rows && u < U) sw[pa[j]] = pw[j];
+  }
+  // a sentinel at position U (key 0 = the smallest, tie word ~0 = the largest: it
+  // never precedes anything), so the rank loop may read one member past a bucket's
+  // end — a later bucket's member never precedes either (later buckets hold strictly
+  // smaller scores; the minimum's sub-buckets equal scores with larger u)
+  if (tid == 0) {
+    skey[U] = 0ull;
+    sw[U] = 0xFFFFFFFFu;
   }
   __syncthreads();
   QF_STOP(24, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += pa[j] + sw[j]; return a; },
@@ -2257,12 +2299,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
       const uint32_t wi = *(const uint32_t*)(wme + 256 * j);  // also the tie-break key:
       // u in the top bits (distinct), so the word order is the first-seen order
       const uint32_t lo = (uint32_t)i - (wi & 0xFFu);
-      uint32_t ka = lo * 8u;                                    // the bucket's first key
-      const uint32_t klast = ka + ((wi >> 8) & 0xFFu) * 8u - 8u;  // its last key
-      uint32_t ta = LD::kA + lo * 4u;                           // the first word
+      uint32_t ka = lo * 8u;  // the bucket's first key
+      asm volatile("" : "+v"(ka));  // (kept, not re-derived from i in the loop's preheader)
+      const uint32_t kend = ka + __builtin_amdgcn_ubfe(wi, 8u, 8u) * 8u;  // one past its last
+      uint32_t ta = LD::kA + lo * 4u;  // the first word
       uint32_t before = 0u;
-      // every member, itself included (it never precedes itself), two per step
-      for (; ka < klast; ka += 16u, ta += 8u) {
+      // every member, itself included (it never precedes itself), two per step; an odd
+      // bucket's last step reads the member after it, which never precedes (sentinel)
+      do {  // (a bucket holds this position: at least one step)
         // two ds_read_b64 (2 LDS cycles each) rather than a ds_read2_b64 (8 cycles)
         const uint64_t v0 = *(const uint64_t*)(lds + ka);
         asm volatile("" ::: "memory");
@@ -2270,10 +2314,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
         const uint32_t t0 = *(const uint32_t*)(lds + ta), t1 = *(const uint32_t*)(lds + ta + 4);
         before = add_if_precedes(before, ki, wi, v0, t0);
         before = add_if_precedes(before, ki, wi, v1, t1);
-      }
-      if (ka == klast)
-        before = add_if_precedes(before, ki, wi, *(const uint64_t*)(lds + ka),
-                                 *(const uint32_t*)(lds + ta));
+        ka += 16u;
+        ta += 8u;
+      } while (ka < kend);
       P[j] = lo + before;
       uo[j] = wi >> 16;
     }
@@ -3257,9 +3300,30 @@ hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream
       else launch_join<JoinXL>(p, kind, st);
     }
     const int M = __builtin_popcount((unsigned)p.methods);
-    if (p.methods & ~QF_LEARNED)
-      hipLaunchKernelGGL((bsort_fast_kernel<512, kJsUMax, 8>),
-                         grid_for((p.n_queries + 7) / 8 * 8 * M), dim3(512), 0, st, p);
+    if (p.methods & ~QF_LEARNED) {
+      const dim3 grid = grid_for((p.n_queries + 7) / 8 * 8 * M);
+      if (QF_DEV_SORT_UNIFIED && max_entries > kJsUMax) {
+        hipLaunchKernelGGL((bsort_fast_kernel<1024, 0, kFastUMaxL, kFastBitsL, true, 8>), grid,
+                           dim3(1024), 0, st, p);
+      } else {
+        hipLaunchKernelGGL((bsort_fast_kernel<512, 0, kJsUMax, kFastBits, false, 8>), grid,
+                           dim3(512), 0, st, p);
+        if (max_entries > kJsUMax) {  // unions above 3,072 (SURVEY §8(d)'s C2: ~4,030)
+          if (QF_DEV_BIG_CFG == 1)
+            hipLaunchKernelGGL((bsort_fast_kernel<512, kJsUMax, kFastUMaxL, 12, false, 4>), grid,
+                               dim3(512), 0, st, p);
+          else if (QF_DEV_BIG_CFG == 2)
+            hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, 12, false, 8>), grid,
+                               dim3(1024), 0, st, p);
+          else if (QF_DEV_BIG_CFG == 3)
+            hipLaunchKernelGGL((bsort_fast_kernel<512, kJsUMax, kFastUMaxL, 13, false, 4>), grid,
+                               dim3(512), 0, st, p);
+          else
+            hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, kFastBitsL, true, 8>),
+                               grid, dim3(1024), 0, st, p);
+        }
+      }
+    }
     if ((p.methods & QF_LEARNED) && !learned_only)
       hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),
                          dim3(512), 0, st, p);

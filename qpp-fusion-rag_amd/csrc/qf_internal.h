@@ -186,6 +186,10 @@ hipError_t minmax_colminmax_launch(const double* score, const int64_t* list_off,
 hipError_t minmax_launch(const double* score, const int64_t* list_off, int64_t n_lists,
                          double* out_norm, int32_t* out_micro, hipStream_t st);
 hipError_t stream_copy_launch(void* dst, const void* src, int64_t n16, hipStream_t st);
+hipError_t synth_nq_launch(int64_t q_begin, int64_t n_queries, int32_t R, int32_t K,
+                           uint64_t seed, const int64_t* qrel_off, const uint32_t* qrel_doc,
+                           int64_t n_qrel_q, int64_t* list_off, uint32_t* docid, double* score,
+                           hipStream_t st);
 hipError_t synth_launch(int64_t q_begin, int64_t n_queries, int32_t R, int32_t K, uint64_t seed,
                         double p_shared, int64_t* list_off, uint32_t* docid, double* score,
                         hipStream_t st);

@@ -18,7 +18,8 @@ CSRC = ROOT / "csrc"
 LIB_PATH = PKG_DIR / "libqppfuse.so"
 IO_LIB_PATH = PKG_DIR / "libqfio.so"  # host run-file I/O (C++ / OpenMP)
 IO_SOURCES = ["qf_io.cpp"]
-SOURCES = ["qf_fuse.hip", "qf_qpp.hip", "qf_norm.hip", "qf_eval.hip", "qf_learn.hip", "qf_capi.hip"]
+SOURCES = ["qf_fuse.hip", "qf_qpp.hip", "qf_norm.hip", "qf_eval.hip", "qf_learn.hip", "qf_synth.hip",
+           "qf_capi.hip"]
 ARCH = os.environ.get("QPPFUSE_ARCH", "gfx950")
 # -ffp-contract=off: the reference's arithmetic is sequential IEEE double; an
 # FMA contraction would change bits (fusion sums, Java's Kahan sums).

@@ -66,6 +66,8 @@ SIGNATURES = {
     "qf_fuse_learned_f32": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, C.c_uint32, _i32,
                                       _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_synth_runs": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _f64, _vp, _vp, _vp, _vp]),
+    "qf_synth_runs_nq": (C.c_int, [_i64, _i64, _i32, _i32, _u64, _vp, _vp, _i64, _vp, _vp, _vp,
+                                   _vp]),
     "qf_stream_copy": (C.c_int, [_vp, _vp, _i64, _vp]),
     "qf_fuse_workspace_bytes": (C.c_int64, [_i64, _i32, _i32, _i32, _i32]),
     "qf_fuse_ws": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32,

@@ -337,6 +337,31 @@ def qpp_features(micro: torch.Tensor, n_queries: int, n_retrievers: int, run_of_
     return out
 
 
+def synth_runs_nq(q_begin: int, n_queries: int, n_retrievers: int, k: int, qrel_off=None,
+                  qrel_doc=None, seed: int = 20251212, device=None):
+    """SURVEY.md §8(d)'s synthetic runs on device (qf_synth_runs_nq): (list_off, docid,
+    raw score).  qrel_off / qrel_doc: the judged documents to plant (CSR over qrel
+    queries, corpus ids; numpy or device tensors), None = no planting."""
+    import numpy as np
+    dev = device or require_device()
+    E = n_queries * n_retrievers * k
+    list_off = torch.empty(n_queries * n_retrievers + 1, dtype=torch.int64, device=dev)
+    docid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+    score = torch.empty(max(E, 1), dtype=torch.float64, device=dev)
+    qo = qd = None
+    nq = 0
+    if qrel_off is not None:
+        to = lambda a, dt: (a if isinstance(a, torch.Tensor) else
+                            torch.from_numpy(np.ascontiguousarray(a).view(dt))).to(dev)
+        qo = to(qrel_off, np.int64)
+        qd = to(qrel_doc, np.int32)
+        nq = qo.numel() - 1
+    _lib.call("qf_synth_runs_nq", int(q_begin), int(n_queries), int(n_retrievers), int(k),
+              int(seed) & (2**64 - 1), _ptr(qo), _ptr(qd), nq, _ptr(list_off), _ptr(docid),
+              _ptr(score), _stream())
+    return list_off, docid[:E], score[:E]
+
+
 def synth_runs(q_begin: int, n_queries: int, n_retrievers: int, k: int, seed: int = 20251212,
                p_shared: float = 0.7, device=None):
     """Synthetic (list_off, docid, raw score) on device; see DESIGN.md."""

@@ -11,7 +11,11 @@ tag = path.rstrip("/").split("/")[-1]
 
 
 def short(name):
-    return re.sub(r"^(void )?qf::", "", name.split("(")[0]).split("<")[0][-24:]
+    base = re.sub(r"^(void )?qf::", "", name.split("(")[0])
+    m = re.match(r"(\w+)<(.*)>$", base)
+    if m and "bsort_fast" in m.group(1):  # keep the configuration
+        return "bsort_fast<" + m.group(2).replace(" ", "") + ">"
+    return base.split("<")[0][-24:]
 
 
 if mode == "kstats":

@@ -10,7 +10,13 @@ import torch
 from qppfuse import engine, _lib
 Q, R, K = 3452, 5, 1000
 dev = torch.device("cuda", 0)
-off, docid, raw = engine.synth_runs(0, Q, R, K)
+if os.environ.get("FUSEBENCH_SYNTH", "nq") == "nq":  # SURVEY §8(d)'s generator (bench default)
+    sys.path.insert(0, str(ROOT))
+    import bench
+    qo, qd = bench.nq_qrels()
+    off, docid, raw = engine.synth_runs_nq(0, Q, R, K, qo, qd)
+else:  # rounds 1-4's generator
+    off, docid, raw = engine.synth_runs(0, Q, R, K)
 _, micro = engine.minmax_per_query(raw, off, want_norm=False)
 torch.manual_seed(7)
 w = torch.rand(Q * R, dtype=torch.float64, device=dev)

@@ -1,26 +1,9 @@
-#!/bin/bash
-# Per-phase VALU + time of one kernel: tools/gpu_phases.sh <kernel substring> <lib> [<lib> ...]
-# (development builds that stop after a phase; each lib under rocprofv3: SQ_INSTS_VALU
-# and kernel time of the C2 six-method qf_fuse launch, tools/fusebench.py)
-set -e
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-K=$1; shift
-O=gpurun_out/ph_$K
+# Phase costs of bsort_fast_kernel from development stop builds (tools/ab/lib_stop<n>.so,
+# -DQF_STOP_AT=n: 21 loads + key constants, 22 count, 23 scan, 24 scatter, 25 rank) and the
+# library: rocprofv3 time and one --pmc pass each; FUSEBENCH_SYNTH picks the generator.
+set -o pipefail
+O=${PASS_OUT:-gpurun_out/phases}
 mkdir -p $O
-for L in "$@"; do
-  n=$(basename $L .so)
-  QF_LIB=$L timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --kernel-trace --output-format csv -d $O/v$n -o run -- python3 tools/fusebench.py > $O/v$n.log 2>&1
-  QF_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/k$n -o run -- python3 tools/fusebench.py > $O/k$n.log 2>&1
-  python3 - $O $n $K <<'PY'
-import csv, glob, sys, collections
-O, n, K = sys.argv[1], sys.argv[2], sys.argv[3]
-f = glob.glob(f'{O}/k{n}/**/run_kernel_stats.csv', recursive=True)[0]
-t = {r['Name'][:40]: round(float(r['AverageNs'])/1e3, 1) for r in csv.DictReader(open(f)) if K in r['Name']}
-f = glob.glob(f'{O}/v{n}/**/run_counter_collection.csv', recursive=True)[0]
-acc = collections.defaultdict(list)
-for r in csv.DictReader(open(f)):
-    if K in r['Kernel_Name']: acc[r['Counter_Name']].append(float(r['Counter_Value']))
-print(n, t, {k: '%.4e' % (sum(v)/len(v)) for k, v in acc.items()})
-PY
-done
-echo phases-done
+LIBS="tools/ab/lib_stop21.so tools/ab/lib_stop22.so tools/ab/lib_stop23.so tools/ab/lib_stop24.so tools/ab/lib_stop25.so qpp-fusion-rag_amd/qppfuse/libqppfuse.so"
+REPS=1 tools/ab_run.sh kstats $O/k $LIBS || exit 1
+REPS=1 tools/ab_run.sh pmc $O/p $LIBS || exit 1
