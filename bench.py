@@ -76,7 +76,12 @@ def parse():
     ap.add_argument("--gather-topk", type=int, default=None,
                     help="per step, gather every rank's fused top-k to rank 0 over RCCL "
                          "(default: 100 when N > 1, else 0; 0 = fused lists stay on their "
-                         "rank, as each rank writes its own qid range)")
+                         "rank, as each rank writes its own qid range).  Bytes into rank 0 "
+                         "per step: N x queries x methods x k x 12 (C2 weak-scaled, k 100: "
+                         "24.9 MB per rank, 174 MB from 7 peers at N = 8 — ~290 GB/s at a "
+                         "0.6 ms step, against rank 0's 7 x ~50 GB/s practical xGMI ingress: "
+                         "DESIGN.md §7); the N > 1 line reports the bytes, the host time in "
+                         "the gather's wait and the step without the gather")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="put every rank on GPU 0 (use with --dist-backend gloo)")
     ap.add_argument("--steps", type=int, default=20)
@@ -257,6 +262,8 @@ class Pipeline:
                                    for n in names]
         self.ev = []
         self.pending = None  # the previous step's top-k gather (dist.TopkGather handle)
+        self.wait_s = 0.0    # host seconds rank 0 spends in the gathers' wait() (timed steps)
+        self.timed_steps = 0
         self.gather, self.n_step, self.gathered = None, 0, None
         if world > 1 and args.gather_topk > 0:  # every buffer of the gather, made once
             from qppfuse.dist import TopkGather
@@ -383,7 +390,12 @@ class Pipeline:
             # this step's kernels are queued.  Two buffer sets alternate: the top-k
             # kernel writes this step's rows straight into set n % 2 (no pad, no cat)
             if self.pending is not None:
+                tw = time.perf_counter()
                 self.gathered = self.pending.wait()
+                if timed:
+                    self.wait_s += time.perf_counter() - tw
+            if timed:
+                self.timed_steps += 1
             e.fused_topk(self.out, self.off, self.R, a.gather_topk,
                          dest=self.gather.buffers(self.n_step))
             self.pending = self.gather.start(self.n_step)
@@ -393,7 +405,9 @@ class Pipeline:
     def drain(self):
         """The last step's gather, before the timed region's final synchronize."""
         if self.pending is not None:
+            tw = time.perf_counter()
             self.gathered = self.pending.wait()
+            self.wait_s += time.perf_counter() - tw
             self.pending = None
 
     def fuse_kernel_ms(self):
@@ -766,6 +780,7 @@ def main():
     for _ in range(args.warmup):
         p.step()
     p.drain()
+    p.wait_s, p.timed_steps = 0.0, 0
     progress(f"rank {rank}: timing {args.steps} steps")
     elapsed = timed_loop(p, args.steps, world, dev)
     total_q = p.Q * args.steps
@@ -782,6 +797,22 @@ def main():
         p.ev, args.gather_topk = ms_fuse, k
         without_gather = {"value": round(total_q / e2, 2),
                           "ms_per_step": round(e2 / args.steps * 1e3, 4)}
+    gather_info = None
+    if p.gather is not None:
+        into0 = (p.world - 1) * p.gather.nbytes  # the peers' buffers (rank 0's own stays local)
+        step_s = elapsed / args.steps
+        gather_info = {
+            "topk": args.gather_topk, "bytes_per_rank_per_step": p.gather.nbytes,
+            "bytes_into_rank0_per_step": into0,
+            "ingress_gbs_at_measured_step": round(into0 / step_s / 1e9, 2),
+            "rank0_host_wait_ms_per_step": round(p.wait_s / max(1, p.timed_steps) * 1e3, 4),
+            "step_ms_without_gather": None if without_gather is None
+            else without_gather["ms_per_step"],
+            "gather_cost_ms_per_step": None if without_gather is None
+            else round(step_s * 1e3 - without_gather["ms_per_step"], 4),
+            "note": "RCCL wait() only orders the compute stream behind the gather (no host "
+                    "block), so the host wait is ~0 there; the gather's cost on the step is "
+                    "ms_per_step - step_ms_without_gather (DESIGN.md §7's ingress budget)"}
     value = total_q / elapsed
     fuse_ms = p.fuse_kernel_ms()
     fbytes, mean_u = p.fuse_bytes()
@@ -843,7 +874,7 @@ def main():
                        "gather_topk_to_rank0": args.gather_topk,
                        "qids": (None if p.qids is None else
                                 f"real BEIR test qids, namespaced: {p.qids[0]} .. {p.qids[-1]}"),
-                       "without_gather": without_gather},
+                       "without_gather": without_gather, "gather": gather_info},
             "roofline": {"bound": "hbm", "kernel": "qf_fuse", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

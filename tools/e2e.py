@@ -26,6 +26,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 NAMES = ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade"]
+GENERATOR = os.environ.get("E2E_GENERATOR", "nq")  # bench.py's synthetic runs
+GOLDEN = ROOT / "tests" / "golden"
+MODEL_FILES = {"per_retriever": GOLDEN / "lgbm" / "nq_fusion_per_retriever.json.gz",
+               "multioutput": GOLDEN / "lgbm" / "nq_fusion_multioutput.json.gz",
+               "mlp": GOLDEN / "mlp" / "nq_fusion_mlp.json.gz"}
 METHODS = ["combsum", "combmnz", "rrf", "wcombsum", "wcombmnz", "wrrf"]
 
 
@@ -64,7 +69,9 @@ def generate(d: Path, Q: int, R: int, K: int, cpu: bool = False, raw_files: bool
         qmicro = np.random.default_rng(1).integers(0, 10**6, (Q * R, 13))
     else:
         from qppfuse import engine
-        off, docid, raw = engine.synth_runs(0, Q, R, K)
+        import bench
+        a = SimpleNamespace(generator=GENERATOR)
+        off, docid, raw = bench.gen_runs(a, 0, Q, R, K)
         _, micro = engine.minmax_per_query(raw, off, want_norm=False)
         nt = torch.full((Q,), 4, dtype=torch.int32, device=off.device)
         tf = torch.rand((Q, 2), dtype=torch.float64, device=off.device)
@@ -104,6 +111,11 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--qpp", action="store_true", help="time the 03_qpp stage (see above)")
+    ap.add_argument("--replay", action="store_true",
+                    help="replay scripts/05_fusion.py run_all_methods + 06_eval_fusion.py on the "
+                         "files (tests/driver_replay.py) and check a sample of every written file "
+                         "byte for byte, and the evaluation JSON, on the CPU reference path")
+    ap.add_argument("--sample", type=int, default=64, help="--replay: queries checked per file")
     ap.add_argument("--load-only", action="store_true",
                     help="CPU only: generate with numpy, time load_runs (QFIO_TIMING=1 for phases)")
     a = ap.parse_args()
@@ -122,6 +134,8 @@ def main():
         return
     if a.qpp:
         return qpp_stage(a, d)
+    if a.replay:
+        return replay(a, d)
     torch.cuda.set_device(0)
     t0 = time.perf_counter()
     E = generate(d, a.queries, 5, 1000)
@@ -154,6 +168,50 @@ def main():
                       "output_bytes": out_bytes, "generate_s": round(gen_s, 2), **best,
                       "e2e_fused_queries_per_s": round(a.queries * 6 / best["total_s"], 1),
                       "cpu_threads": os.cpu_count()}), flush=True)
+
+
+def replay(a, d: Path):
+    """--replay: the reference's driver sequence file to file, checked (module docstring)."""
+    import gzip
+    sys.path.insert(0, str(ROOT / "tests"))
+    import driver_replay as dr
+    torch.cuda.set_device(0)
+    runs_dir = d / "runs"
+    runs_dir.mkdir(exist_ok=True)
+    t0 = time.perf_counter()
+    if not any(runs_dir.glob("*.norm.res")):
+        generate(runs_dir, a.queries, 5, 1000)
+    gen_s = time.perf_counter() - t0
+    qpp_dir = runs_dir / "qpp"
+    fused_dir = d / "fused"
+    fused_dir.mkdir(exist_ok=True)
+    qrels = d / "test.tsv"
+    qrels.write_bytes(gzip.decompress((GOLDEN / "nq_qrels_test.tsv.gz").read_bytes()))
+    size = sum(f.stat().st_size for f in runs_dir.glob("*.norm.res"))
+    t0 = time.perf_counter()
+    results = dr.run_all_methods(runs_dir, qpp_dir, fused_dir, model_files=MODEL_FILES)
+    fuse_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    evals = dr.evaluate_fused_runs(fused_dir, qrels, d)
+    eval_s = time.perf_counter() - t0
+    rng = np.random.default_rng(5)
+    sample = [f"test{q}" for q in sorted(rng.choice(a.queries, min(a.sample, a.queries),
+                                                    replace=False))]
+    t0 = time.perf_counter()
+    ok = dr.check_sample(runs_dir, qpp_dir, results, sample, model_files=MODEL_FILES)
+    check_s = time.perf_counter() - t0
+    eval_ok = dr.check_eval(fused_dir, qrels, evals)
+    out_bytes = sum(p.stat().st_size for p in results.values())
+    print(json.dumps({"stage": "05_fusion.run_all_methods + 06_eval_fusion.evaluate_fused_runs",
+                      "queries": a.queries, "input_bytes": size, "output_bytes": out_bytes,
+                      "files": sorted(p.name for p in results.values()),
+                      "generate_s": round(gen_s, 2), "run_all_methods_s": round(fuse_s, 3),
+                      "evaluate_fused_runs_s": round(eval_s, 3),
+                      "sample_queries": len(sample), "bytes_equal_per_file": ok,
+                      "bytes_equal": all(ok.values()), "check_s": round(check_s, 1),
+                      "eval_equal_oracle": eval_ok,
+                      "ndcg10": {r["method"]: round(r["nDCG@10"], 5) for r in evals},
+                      "generator": GENERATOR, "cpu_threads": os.cpu_count()}), flush=True)
 
 
 POOL = """
