@@ -81,22 +81,35 @@ __device__ __forceinline__ double cube(double x) {
   return fma(sq, x, lo * x);
 }
 
-// v of lane l (l wave-uniform) as a scalar: two v_readlane_b32.
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-  return __hiloint2double(hi, lo);
-}
-
-// A workgroup takes kQppLists lists, one wavefront each.  The per-element and
-// per-prefix work is lane parallel inside the list's wave (lane i holds rsv[i] /
-// owns prefix i); the sums Java forms left to right are serial chains, and those
-// run batched: one wave, one lane per (list, chain), so a chain costs one lane
-// of one instruction instead of a whole wave's.
+// A workgroup takes kQppLists lists, one wavefront each.  The per-element work is
+// lane parallel inside the list's wave (lane i holds rsv[i]); the sums Java forms
+// left to right are serial chains, and those run batched: one wave, one lane per
+// (list, chain), so a chain costs one lane of one instruction instead of a whole
+// wave's.
+//
+// SigmaMax and CumNQC (QPPBridge.java:269-293, 400-410) need the population
+// variance of every prefix rsv[0..i].  Java recomputes each from scratch (a
+// compensated prefix mean, then a compensated / simple sum of squared deviations
+// around it): O(k^2).  Here one Welford chain per list carries the running mean
+// and M2, so every prefix variance costs one step, O(k) — the values differ from
+// Java's order by rounding only (<= 1.2e-13 relative over C2's and the section
+// 8(d) generator's lists, tools/qpp_ok_study.py; no "%.6f" .qpp value changes).
+// Every other column keeps Java's exact order: NQC (col 0) and RSD's variance
+// (col 5, the default fusion weight) are the full-list sums of (x - mu)^2, simple
+// and compensated, and RSD's skewness terms follow them.
+//
+// Phases (workgroup barriers between them):
+//   B  chains over rsv: the compensated full-list sum (-> mu), SigmaX pass 1,
+//      the Welford prefix variances (-> SigmaMax, CumNQC)   [waves 0, 1, 2]
+//   C  per element: SMV / WIG / SNQC / UEF terms, (x - mu)^2 [every wave]
+//   D  chains: the five simple sums, SigmaX pass 2, the compensated sum of
+//      (x - mu)^2 (-> RSD's std)                           [waves 0, 1, 2]
+//   E  per element: ((x - mu) / std)^3                      [every wave]
+//   F  chain: the skewness sum                              [wave 0]
 
 constexpr int kQppLists = 8;
 constexpr int kQppBlock = 64 * kQppLists;
-constexpr int kChains = 6;   // cum, smv, wig, skew, snqc, uw
+constexpr int kRows = 5;     // smv, wig, snqc, uw, (x - mu)^2; then the skew terms
 constexpr int kRow = 65;     // padded LDS row (doubles)
 constexpr int kQppK = 50;    // k = min(50, n), QPPBridge.java:141
 
@@ -104,11 +117,11 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const double* __restrict__ score, const int64_t* __restrict__ list_off, int64_t n_lists,
     int32_t R, int32_t top_k, const int32_t* __restrict__ num_terms,
     const double* __restrict__ text_feat, double* __restrict__ out) {
-  __shared__ double s_x[kQppLists][kRow];           // rsv (float32-rounded)
-  __shared__ double s_pf[kQppLists][kRow];          // prefix sums (Kahan s + c)
-  __shared__ double s_ps[kQppLists][kRow];          // prefix sums (simple)
-  __shared__ double s_t[kQppLists][kChains][kRow];  // per-element terms of the chains
-  __shared__ double s_res[kQppLists][kChains];      // chain sums
+  __shared__ double s_x[kQppLists][kRow];          // rsv (float32-rounded)
+  __shared__ double s_t[kQppLists][kRows][kRow];   // per-element terms of the chains
+  __shared__ double s_res[kQppLists][kRows];       // simple chain sums (D)
+  __shared__ double s_mu[kQppLists], s_cum[kQppLists], s_vmax[kQppLists];
+  __shared__ double s_var[kQppLists], s_skew[kQppLists];
   __shared__ double s_sigmax[kQppLists];
   __shared__ double s_mf[kQppLists];  // SigmaX's compensated mean over F (pass 1)
   __shared__ unsigned long long s_fmask[kQppLists];
@@ -125,8 +138,7 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     k = n64 < 50 ? (int)n64 : 50;                // QPPBridge.java:141
   }
   const bool act = lane < k;
-  // the query's inputs issued with the scores (one latency, not three: they were
-  // loaded where first used, each a stall of the whole workgroup's phase)
+  // the query's inputs issued with the scores (one latency, not three)
   // (unconditional: q = 0 for a padding wave, whose values go unused)
   const int64_t q = lv ? l / R : 0;
   const int nt_raw = num_terms[q];
@@ -145,39 +157,28 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   }
   __syncthreads();
 
-  // ---- B (lane = list): the serial chains that need only rsv, on two waves at once.
+  // ---- B (lane = list): the chains that need only rsv, on three waves at once.
   // The serial loops run to kQppK unrolled (rows are kRow long; values past k
-  // unused), only the arithmetic predicated; every sum keeps its order.  (The
-  // compiler sinks each LDS read into its predicated step.  Round 4 measured the
-  // chains branch-free with their reads issued four steps ahead, and phase C's x_j
-  // by readlane instead of an LDS broadcast: bit-identical, 65.1 vs 65.2 us for
-  // C2 — the kernel is bound by its VALU issue, not by these latencies — and 12 %
-  // more VALU instructions; not kept.)
-  // The chains are the workgroup's critical path (its other six waves wait at the
-  // barrier) while the CU's other workgroups keep the SIMD busy: the chain waves run
-  // at raised issue priority (s_setprio), so each dependent step issues as soon as
-  // its operands are ready instead of queueing behind other waves' instructions.
-  if (w <= 1) __builtin_amdgcn_s_setprio(3);
+  // unused), only the arithmetic predicated; every sum keeps its order.  The
+  // chains are the workgroup's critical path (its other waves wait at the barrier)
+  // while the CU's other workgroups keep the SIMD busy: the chain waves run at
+  // raised issue priority (s_setprio), so each dependent step issues as soon as its
+  // operands are ready instead of queueing behind other waves' instructions.
+  if (w <= 2) __builtin_amdgcn_s_setprio(3);
   if (w == 0 && lane < kQppLists) {
-    // Java's compensated prefix sums (DoubleStream.average of rsv[0..i]): the
-    // chain keeps only the Kahan state; computeFinalSum and the division by
-    // i + 1 run lane-parallel in C
+    // Arrays.stream(rsvs).average(): the JDK's compensated sum / n
     const int kl = s_k[lane];
     Kahan kp;
     kahan_init(kp);
 #pragma unroll
     for (int j = 0; j < kQppK; ++j) {
       const double v = s_x[lane][j];
-      if (j < kl) {
-        kahan_add(kp, v);
-        s_pf[lane][j] = kahan_final_sum(kp);
-        s_ps[lane][j] = kp.simple;
-      }
+      if (j < kl) kahan_add(kp, v);
     }
+    s_mu[lane] = kl > 0 ? div_int(kahan_final(kp), kl) : 0.0;
   } else if (w == 1 && lane < kQppLists) {
     // SigmaX, pass 1: the compensated mean over F.  Pass 2 (the compensated mean of
-    // (x - mean)^2) runs in D beside the left-to-right sums: the two passes in a row
-    // were this phase's critical path (100 steps against the prefix chain's 50)
+    // (x - mean)^2) runs in D beside the left-to-right sums.
     const int kl = s_k[lane];
     const uint64_t fm = s_fmask[lane];
     const int nf = __popcll(fm);
@@ -193,72 +194,77 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       mf = div_int(kahan_final(kf), nf);
     }
     s_mf[lane] = mf;
+  } else if (w == 2 && lane < kQppLists) {
+    // Welford: mean_i = mean_{i-1} + d / (i + 1), M2_i = M2_{i-1} + d (x_i - mean_i),
+    // var_i = M2_i / (i + 1); SigmaMax takes the largest var_i of the prefixes of 2..k
+    // elements (sqrt is monotone: the max of the sigmas is the sigma of the max),
+    // CumNQC their sum in prefix order (the NQC of a prefix is its variance).
+    const int kl = s_k[lane];
+    double mean = 0.0, m2 = 0.0, cum = 0.0, vmax = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQppK; ++j) {
+      const double v = s_x[lane][j];
+      const double inv = 1.0 / (double)(j + 1);  // a literal: the loop is unrolled
+      if (j < kl) {
+        const double d = v - mean;
+        mean = fma(d, inv, mean);
+        m2 = fma(d, v - mean, m2);
+        if (j >= 1) {
+          const double var = m2 * inv;
+          cum += var;
+          vmax = fmax(vmax, var);
+        }
+      }
+    }
+    s_cum[lane] = cum;
+    s_vmax[lane] = vmax;
   }
-  if (w <= 1) __builtin_amdgcn_s_setprio(0);
+  if (w <= 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
 
-  // ---- C (each list's wave): squared deviations around each prefix mean
-  // (lane i = prefix i): simple sum -> NQC of the prefix (NQC, CumNQC),
-  // compensated average -> population variance (SigmaMax, RSD)
+  // ---- C (each list's wave): the per-element terms (transcendentals once each)
   const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
-  double mean_i = 0.0;
-  if (act) {  // computeFinalSum of prefix i, / (i + 1)
-    const double tmp = s_pf[w][lane], simple = s_ps[w][lane];
-    mean_i = div_int(kahan_final_pick(tmp, simple), lane + 1);
-  }
-  const double mu = k > 0 ? readlane_f64(mean_i, k - 1) : 0.0;  // Arrays.stream(rsvs).average()
-  Kahan kv;
-  kahan_init(kv);
-  double sq = 0.0;
-#pragma unroll
-  for (int j = 0; j < kQppK; ++j) {
-    const double del = s_x[w][j] - mean_i;
-    const double d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
-    if (j < k && j <= lane) {
-      sq += d2;
-      kahan_add(kv, d2);
-    }
-  }
-  const double nqc_i = div_int(sq, lane + 1);
-  const double var_i = div_int(kahan_final(kv), lane + 1);
-  const double sigma_i = sqrt(var_i);
-  const double nqc = k > 0 ? readlane_f64(nqc_i, k - 1) : 0.0;  // col 0: NQC (:202-216)
-  const double var_full = k > 0 ? readlane_f64(var_i, k - 1) : 0.0;
-  double sm = (lane >= 1 && act) ? sigma_i : 0.0;                // col 3: SigmaMax (:269-293)
-  sm = wave_max(sm);
-  const double sigmamax = k < 2 ? 0.0 : sm / sqrt((double)numTerms);
-
-  // per-element terms, one element per lane (transcendentals run once each)
+  const double mu = s_mu[w];
   const double muhat = mu <= 0.0 ? 1.0 : mu;                  // SMV
   const double baseline = 1.0 / (0.01 > mu ? 0.01 : mu);      // WIG
-  const double std_full = sqrt(var_full);                     // RSD
-  double t_smv = 0.0, t_snqc = 0.0, t_skew = 0.0, t_wig = 0.0, t_uw = 0.0;
+  double t_smv = 0.0, t_snqc = 0.0, t_wig = 0.0, t_uw = 0.0, t_d2 = 0.0;
   if (act) {
+    const double del = x - mu;
+    t_d2 = del * del;  // Math.pow(s - mean, 2) == s*s exactly
     if (x > 0.0) {
       t_smv = x * fabs(log(x / muhat));
-      const double del = x - mu;
-      t_snqc = snqc_term((del * del) / x);
+      t_snqc = snqc_term(t_d2 / x);
     }
-    t_skew = cube((x - mu) / std_full);
     t_wig = x - baseline;
     if (lane < 20) t_uw = x * uefw;  // UEF (:349-363)
   }
   // Java adds the x <= 0 terms of SMV / SNQC as "skip": adding +0.0 is the same.
-  // col 9: CumNQC (:400-410) sums the NQC of prefix sizes 2..n in order.
-  s_t[w][0][lane] = (lane >= 1 && act) ? nqc_i : 0.0;
-  s_t[w][1][lane] = t_smv;
-  s_t[w][2][lane] = t_wig;
-  s_t[w][3][lane] = t_skew;
-  s_t[w][4][lane] = t_snqc;
-  s_t[w][5][lane] = t_uw;
+  s_t[w][0][lane] = t_smv;
+  s_t[w][1][lane] = t_wig;
+  s_t[w][2][lane] = t_snqc;
+  s_t[w][3][lane] = t_uw;
+  s_t[w][4][lane] = t_d2;
   const double mx = wave_max(act ? x : -INFINITY);
   const double mn = wave_min(act ? x : INFINITY);
   __syncthreads();
 
-  // ---- D (wave 0, lane = list * 8 + chain): the left-to-right sums, all chains
-  // of all lists at once
-  if (w <= 1) __builtin_amdgcn_s_setprio(3);  // the critical path again (see B)
-  if (w == 1 && lane < kQppLists) {  // SigmaX, pass 2 (pass 1 in B)
+  // ---- D: the left-to-right sums (wave 0, lane = list * 8 + row: SMV, WIG, SNQC,
+  // UEF, NQC's simple sum of (x - mu)^2), SigmaX pass 2 (wave 1) and RSD's
+  // compensated mean of (x - mu)^2 (wave 2), all lists at once
+  if (w <= 2) __builtin_amdgcn_s_setprio(3);
+  if (w == 0 && (lane & 7) < kRows) {
+    const int ll = lane >> 3, c = lane & 7;
+    const int kl = s_k[ll];
+    const int len = c == 3 ? (kl < 20 ? kl : 20) : kl;
+    const double* row = s_t[ll][c];
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQppK; ++j) {
+      const double v = row[j];
+      if (j < len) acc += v;
+    }
+    s_res[ll][c] = acc;
+  } else if (w == 1 && lane < kQppLists) {  // SigmaX, pass 2 (pass 1 in B)
     const int kl = s_k[lane];
     const uint64_t fm = s_fmask[lane];
     const int nf = __popcll(fm);
@@ -275,21 +281,38 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       sigmax = sqrt(div_int(kahan_final(kfv), nf));
     }
     s_sigmax[lane] = sigmax;
+  } else if (w == 2 && lane < kQppLists) {  // RSD (:320-344): std of the full list
+    const int kl = s_k[lane];
+    Kahan kv;
+    kahan_init(kv);
+#pragma unroll
+    for (int j = 0; j < kQppK; ++j) {
+      const double v = s_t[lane][4][j];
+      if (j < kl) kahan_add(kv, v);
+    }
+    s_var[lane] = kl > 0 ? div_int(kahan_final(kv), kl) : 0.0;
   }
-  if (w == 0 && (lane & 7) < kChains) {
-    const int ll = lane >> 3, c = lane & 7;
-    const int kl = s_k[ll];
-    const int len = c == 5 ? (kl < 20 ? kl : 20) : kl;
-    const double* row = s_t[ll][c];
+  if (w <= 2) __builtin_amdgcn_s_setprio(0);
+  __syncthreads();
+
+  // ---- E (each list's wave): RSD's skewness terms, over the row D has consumed
+  const double std_full = sqrt(s_var[w]);
+  s_t[w][4][lane] = act ? cube((x - mu) / std_full) : 0.0;
+  __syncthreads();
+
+  // ---- F (wave 0, lane = list): the skewness sum
+  if (w == 0 && lane < kQppLists) {
+    __builtin_amdgcn_s_setprio(3);
+    const int kl = s_k[lane];
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < kQppK; ++j) {
-      const double v = row[j];
-      if (j < len) acc += v;
+      const double v = s_t[lane][4][j];
+      if (j < kl) acc += v;
     }
-    s_res[ll][c] = acc;
+    s_skew[lane] = acc;
+    __builtin_amdgcn_s_setprio(0);
   }
-  if (w <= 1) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
 
   if (!lv) return;
@@ -298,21 +321,19 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     if (lane < kQppCols) o[lane] = 0.0;
     return;
   }
-  const double cum = s_res[w][0], smv = s_res[w][1], wig = s_res[w][2], skew = s_res[w][3];
-  const double snqc = s_res[w][4], util = s_res[w][5];
-  const double sigmax = s_sigmax[w];
-  const double cumnqc = k < 2 ? 0.0 : div_int(cum, k - 1);
+  const double smv = s_res[w][0], wig = s_res[w][1], snqc = s_res[w][2], util = s_res[w][3];
+  const double sq = s_res[w][4], skew = s_skew[w];
   double res[kQppCols];
-  res[0] = nqc;
+  res[0] = div_int(sq, k);                                             // NQC (:202-216)
   res[1] = div_int(smv, k);
   res[2] = div_int(wig, numTerms * k);
-  res[3] = sigmamax;
-  res[4] = sigmax;
+  res[3] = k < 2 ? 0.0 : sqrt(s_vmax[w]) / sqrt((double)numTerms);    // SigmaMax
+  res[4] = s_sigmax[w];
   res[5] = (k < 3 || std_full < 1e-10) ? 0.0 : div_int(skew, k);
   res[6] = util / wsum;
   res[7] = tf0;
   res[8] = tf1;
-  res[9] = cumnqc;
+  res[9] = k < 2 ? 0.0 : div_int(s_cum[w], k - 1);                    // CumNQC
   res[10] = mu <= 0.0 ? 0.0 : div_int(snqc, k);
   const double range = mx - mn;
   res[11] = (k < 2 || !(range > 0.0)) ? 0.0 : log(1.0 + 1.0 / range);

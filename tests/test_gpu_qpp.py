@@ -1,10 +1,12 @@
 """Parity of the HIP QPP kernels with the oracle — needs an MI355X.
 
 Tolerance: the north star allows 1e-5 relative for QPP scores; the kernels
-reproduce Java's summation order, so the only differences left are ulps of
-log/pow/sqrt between ROCm's device libm and glibc.  Checked at rtol 1e-9
-(atol 1e-12) on the raw predictors; the "%.6f"-rounded outputs agree exactly
-except where two libms round to different sides of a 6th-decimal boundary.
+reproduce Java's summation order except for SigmaMax / CumNQC's prefix variances
+(O(k) Welford, csrc/qf_qpp.hip), so the differences left are those rounding paths
+and ulps of log/exp/pow between ROCm's device libm and glibc.  Checked at rtol
+1e-12 on the raw predictors (atol 1e-15 for values that are themselves ~0); the
+"%.6f"-rounded outputs agree exactly except where two libms round to different
+sides of a 6th-decimal boundary (none on C2's lists: tests/test_gpu_qpp_scale.py).
 """
 import math
 
@@ -17,7 +19,7 @@ from oracle import ref_port
 
 pytestmark = pytest.mark.gpu
 
-RTOL, ATOL = 1e-9, 1e-12
+RTOL, ATOL = 1e-12, 1e-15
 
 
 def _lists(seed=3):
