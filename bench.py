@@ -493,6 +493,77 @@ def ndcg_delta(p: Pipeline, dev_vals, nq: int):
     return worst_q, worst_mean
 
 
+def ndcg_delta_learned(p: Pipeline, dev_vals, nq: int):
+    """C5: NDCG@10 of learned fusion on the CPU reference path vs the device values —
+    the 13 predictors of every list of the batch by the Java restatement
+    (oracle/qpp_oracle.c), min-max per retriever column over the batch and "%.6f"
+    (src/qpp.py:340-374, 329-335), the features in the model's retriever order, the
+    LightGBM walk restated (oracle/lgbm_oracle.py), the weighted groupby-sum as pandas'
+    Kahan sum in run order (src/fusion.py:436-446), the trec_eval restatement."""
+    from oracle import _loader as coracle
+    from oracle import lgbm_oracle
+    from qppfuse import lgbm
+    R, K, Q = p.R, p.K, p.Q
+    off_all = p.off.cpu().numpy()
+    raw_all = p.raw[: off_all[-1]].cpu().numpy()
+    cut = [raw_all[off_all[l]:off_all[l + 1]][: p.args.qpp_top_k or None] for l in range(Q * R)]
+    coff = np.zeros(Q * R + 1, np.int64)
+    coff[1:] = np.cumsum([len(c) for c in cut])
+    nt, tf = p.nt.cpu().numpy(), p.tf.cpu().numpy()
+    qraw = coracle.qpp_raw(np.concatenate(cut), coff, np.repeat(nt, R), np.repeat(tf[:, 0], R),
+                           np.repeat(tf[:, 1], R))
+    feats = np.zeros((Q * R, 13))
+    for r in range(R):  # one .qpp file per retriever: min-max over its queries, "%.6f"
+        col = qraw[r::R]
+        lo, hi = col.min(axis=0), col.max(axis=0)
+        sc = np.where(hi > lo, hi - lo, 1.0)
+        feats[r::R] = np.array([[float(f"{v:.6f}") for v in row] for row in (col - lo) / sc])
+    model = lgbm.load_fusion_model(ROOT / "tests" / "golden" / "lgbm" /
+                                   "nq_fusion_multioutput.json.gz")
+    names = NAMES[:R]
+    X = np.zeros((nq, 13 * len(model.retrievers)))
+    for j, rn in enumerate(model.retrievers):
+        if rn in names:
+            X[:, 13 * j:13 * j + 13] = feats[names.index(rn)::R][:nq]
+    pred = lgbm_oracle.model_predict(model, X)
+    w = np.array([[pred[q, model.retrievers.index(n)] if n in model.retrievers else 1.0 / len(model.retrievers)
+                   for n in names] for q in range(nq)])
+    h = host_sample(p, nq)
+    sc = h["micro"].astype(np.float64) / 1e6
+    qo, qd, qr = synth_qrels(p.q_begin, nq, p.K, p.args.generator)
+    roff, rdoc, rsc = [0], [], []
+    for q in range(nq):
+        ent_d, ent_v = [], []
+        for r in range(R):  # pandas concat order: run by run, row by row
+            a, b = h["off"][q * R + r], h["off"][q * R + r + 1]
+            ent_d.append(h["docid"][a:b])
+            ent_v.append(sc[a:b] * w[q, r])
+        d = np.concatenate(ent_d)
+        v = np.concatenate(ent_v)
+        order = np.argsort(d, kind="stable")  # each document's terms in run order
+        d, v = d[order], v[order]
+        first = np.r_[True, d[1:] != d[:-1]]
+        g = np.cumsum(first) - 1
+        pos = np.arange(len(d)) - np.flatnonzero(first)[g]
+        acc = np.zeros(g[-1] + 1)
+        comp = np.zeros(g[-1] + 1)
+        for t in range(int(pos.max()) + 1):  # Kahan, one term of every document at a time
+            m = pos == t
+            y = v[m] - comp[g[m]]
+            tt = acc[g[m]] + y
+            c = (tt - acc[g[m]]) - y
+            comp[g[m]] = np.where(np.isnan(c), 0.0, c)
+            acc[g[m]] = tt
+        rdoc.append(d[first])
+        rsc.append(acc)
+        roff.append(roff[-1] + len(acc))
+    ref = coracle.evaluate(np.array(roff, np.int64), np.concatenate(rdoc),
+                           np.concatenate(rsc), qo, qd, qr, ["nDCG@10"], text=True)[:, 0]
+    dv = dev_vals[p.methods.index("learned"), :nq]
+    return (float(np.nanmax(np.abs(dv - ref))),
+            abs(float(np.nanmean(dv)) - float(np.nanmean(ref))))
+
+
 def host_sample(p: Pipeline, nq: int):
     """Copy the first nq queries' inputs + device outputs to host numpy.  When the
     step's fusion took its W-* weights from the QPP predictors (qf_fuse_qpp), `w` is
@@ -905,6 +976,14 @@ def main():
                 "queries": nq, "max_abs_per_query": dq, "max_abs_mean": dm,
                 "ref": "CPU reference path: C oracle fusion + trec_eval restatement "
                        "(oracle/), scores as the .res text"}
+        elif world == 1 and args.ndcg_sample > 0 and p.methods == ["learned"]:
+            nq = min(args.ndcg_sample, p.Q)
+            dq, dm = ndcg_delta_learned(p, ndcg_vals, nq)
+            result["ndcg10_delta_vs_ref"] = {
+                "queries": nq, "max_abs_per_query": dq, "max_abs_mean": dm,
+                "ref": "CPU reference path: QPP by the Java restatement (oracle/qpp_oracle.c), "
+                       "min-max + '%.6f', LightGBM walk restated (oracle/lgbm_oracle.py), "
+                       "pandas' Kahan groupby-sum in run order, trec_eval restatement"}
         os.write(out_fd, (json.dumps(result) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()

@@ -1419,8 +1419,10 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
       const int U = p.union_count[q];
       bool take = U >= umin && U <= C::kUMax;
       // the fallback pass: a pair within a bucket sort's reach is taken when it marked
-      // it (learned fusion's docid-tie sort reaches kJsUMax, the others kFastUMaxL)
-      const int reach = slot_method(p.methods, (int)(idx % M)) == 6 ? kJsUMax : kFastUMaxL;
+      // it (learned fusion's docid-tie sort reaches p.learned_reach, the others kFastUMaxL)
+      const int reach = slot_method(p.methods, (int)(idx % M)) == 6
+                            ? (p.learned_reach ? p.learned_reach : kJsUMax)
+                            : kFastUMaxL;
       if (FB && U > 1 && U <= reach)
         take = perm_get(p, (idx % M) * p.out_stride + p.list_off[q * p.R]) == kJsUnsorted;
       if (take) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
@@ -1630,7 +1632,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
   static_assert(LD::kBcBytes >= 4 * UMAX && LD::kStart >= 8 * BLOCK, "region BC layout");
   double* sval = (double*)lds;                                   // region A
   uint64_t* skey = (uint64_t*)lds;  // region A from the scatter on: bs_rank_key by position
-  uint32_t* sw = (uint32_t*)(lds + 8 * UMAX);                    // region BC: u << 20 | size << 8 | at
+  uint32_t* sw = (uint32_t*)(lds + 8 * UMAX);                    // region BC: u << 16 | size << 8 | at
   uint16_t* bk = (uint16_t*)(lds + 8 * UMAX + LD::kStart);       // bucket starts [NB + 8]
   uint32_t* cnt = (uint32_t*)(sval + 2 * BLOCK);                 // [NB + 1] u32
   uint32_t* sd = (uint32_t*)(lds + LD::kSd);                     // docid by position (BYDOC)
@@ -1830,7 +1832,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
 
   const bool nonneg = smin >= 0.0;  // block-uniform (smin folds -0.0 into +0.0)
   // ---- scatter: the value by position; u, bucket size and arrival kept ------------------
-  uint32_t pa[ROWS], pw[ROWS];  // position; u << 20 | size << 8 | arrival
+  uint32_t pa[ROWS], pw[ROWS];  // position; u << 16 | size << 8 | arrival
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int u = ub0 + j * ustep + lane;
@@ -1843,7 +1845,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
       skey[pos] = nonneg ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);
       if (BYDOC) sd[pos] = d[j];
       pa[j] = pos;
-      pw[j] = ((uint32_t)u << 20) | ((nx - st) << 8) | at;
+      pw[j] = ((uint32_t)u << 16) | ((nx - st) << 8) | at;  // size <= kJsBucketMax
     }
   }
   __syncthreads();  // the starts are dead: the u | size | arrival words over them
@@ -1867,7 +1869,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
       // the tie-break key: the whole word, whose top bits are u — distinct, so the
       // word order is the first-seen order — or, BYDOC, the docid
       const uint32_t ti = BYDOC ? sd[i] : wi;
-      const uint32_t lo = (uint32_t)i - (wi & 0xFFu), hi = lo + ((wi >> 8) & 0xFFFu);
+      const uint32_t lo = (uint32_t)i - (wi & 0xFFu), hi = lo + ((wi >> 8) & 0xFFu);
       uint32_t before = 0u;
       // the bucket's members by pointer (two per step; a bucket of one: nothing to
       // count): no index arithmetic inside the loop
@@ -1888,7 +1890,7 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
       }
       if (pv < pend) before = add_if_precedes(before, ki, ti, pv[0], tp[0]);
       P[j] = lo + before;
-      uo[j] = wi >> 20;
+      uo[j] = wi >> 16;
     }
   }
   // ---- outputs (every row's position before any store) ----------------------------------
@@ -2215,8 +2217,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
     const uint32_t incl = wave_incl_scan_dpp(tot);
     if (lane == 63) sm.wtot[wid] = incl;
     __syncthreads();  // also: every counter read before the scatter overwrites them
+    // the waves before this one: lane w reads wave w's total (one LDS read, not a
+    // serial loop of up to 15 dependent ones), a DPP scan, the lane wid - 1 of it
     uint32_t pre = incl - tot;
-    for (int w = 0; w < wid; ++w) pre += sm.wtot[w];  // wid is wave-uniform: a scalar loop
+    const uint32_t wt = wave_incl_scan_dpp(lane < WAVES ? sm.wtot[lane] : 0u);
+    if (wid > 0) pre += readlane_u32(wt, wid - 1);
     if constexpr (S32) {
 #pragma unroll
       for (int i = 0; i < kPer / 4; ++i)
@@ -2353,15 +2358,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
 // first entry's input docid), and the bucket sort by docid ties (bsort_core,
 // BYDOC) ranks them in the join's dead LDS.  The separate sort kernel re-read
 // every score from HBM and ran at 3 workgroups per CU for the docid array;
-// here the scores never leave the registers.  A union above kJsUMax (or a query
-// with a status) is left unsorted to fuse_large_kernel, as the join_kernel path
-// leaves it.
+// here the scores never leave the registers.  Unions up to kLearnedUMax = 4,608
+// (SURVEY §8(d)'s C2 unions: 3,856-4,148): the sort's 72 KB of LDS (12-bit keys,
+// docids by position) over the join's dead tables, two workgroups per CU.  A union
+// above it (or a query with a status) is left unsorted to fuse_large_kernel, as
+// the join_kernel path leaves it.
 // ============================================================================
+constexpr int kLearnedUMax = 4608;
 template <class C>
 __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(FuseParams p) {
-  constexpr int BLOCK = C::kBlock, ROWS = (kJsUMax + BLOCK - 1) / BLOCK;
+  constexpr int BLOCK = C::kBlock, ROWS = (kLearnedUMax + BLOCK - 1) / BLOCK;
   static_assert(BLOCK == 512, "bsort_core is instantiated for 512 threads");
-  constexpr int kSortLds = BsLds<12, true>::kBytes;
+  constexpr int kSortLds = BsLds<12, true, kLearnedUMax>::kBytes;
   __shared__ JoinShared<C, 1, kSortLds> sh;
   __shared__ BsShared<BLOCK / 64> sm;
   const int64_t q = block_id();
@@ -2369,7 +2377,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(F
   const int N = join_groups<C, 1, kSortLds>(p, sh, q);
   if (N < 0) return;
   const int U = sh.U;
-  if (U > kJsUMax || sh.status) {  // uniform: the separate sort kernels' share
+  if (U > kLearnedUMax || sh.status) {  // uniform: the fallback pass's share
     SlotRange rg;  // (learned fusion alone keeps no ranges)
     store_unsorted_sums<C, 1, kSortLds>(p, sh, N, rg);
     if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : U;
@@ -2404,7 +2412,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(F
   }
   if (tid == 0) p.union_count[q] = U;
   __syncthreads();  // the groups are dead: their LDS is the sort's
-  bsort_core<BLOCK, 12, true>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK, base);
+  bsort_core<BLOCK, 12, true, kLearnedUMax>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK, base);
 }
 
 // ============================================================================
@@ -3176,6 +3184,7 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
 using JoinT = JoinCfg<64, 5, 10, 6>;  // N <= 320: one wave per query (C1)
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
 using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
+using JoinML = JoinCfg<512, 10, 13, 4>;  // join_learned_kernel: 2 per CU (its sort's LDS)
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
 using JoinXL = JoinCfg<1024, 10, 14>; // N <= 10240 (e.g. 10 runs x top-1000; 143 KB LDS)
 using SortT = SortCfg<64, 5, 8>;      // U <= 320: one wave per (query, method) (C1)
@@ -3278,21 +3287,23 @@ static hipError_t launch_xl(const FuseParams& p, int kind, int max_entries, int 
   return hipGetLastError();
 }
 
-hipError_t fuse_launch(const FuseParams& p, int kind, int max_entries, hipStream_t st,
+hipError_t fuse_launch(const FuseParams& p0, int kind, int max_entries, hipStream_t st,
                        void* ws_user, size_t ws_bytes) {
   void* ws = nullptr;
   hipError_t e = hipSuccess;
+  FuseParams p = p0;
   if (p.R <= kRMax && max_entries <= JoinXL::kNMax && max_entries > JoinS::kNMax) {
     // the join kernel, then the bucket sort per (query, method) for U <= kJsUMax
     const bool learned_only = p.methods == QF_LEARNED && kind == 1 &&
                               max_entries <= JoinM::kNMax;
+    if (learned_only) p.learned_reach = kLearnedUMax;
     // (Measured, not kept, round 4: every method's sort in the join's workgroup too —
     // the sums stored, each slot read back L2-hot by the thread that stored it and
     // ranked by bsort_core in the join's dead LDS: 349-352 us against join 126 +
     // bsort 202-204 us; the six sorts in turn at 3 workgroups per CU lose more than
     // the HBM re-read they save.)
     if (learned_only) {  // join + sort in one kernel (C5)
-      hipLaunchKernelGGL((join_learned_kernel<JoinM>), grid_for(p.n_queries), dim3(512), 0, st,
+      hipLaunchKernelGGL((join_learned_kernel<JoinML>), grid_for(p.n_queries), dim3(512), 0, st,
                          p);
     } else {
       if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);

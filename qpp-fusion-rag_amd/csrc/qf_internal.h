@@ -44,6 +44,9 @@ struct FuseParams {
   const double* qpp_raw;
   const double* qpp_stats;
   int32_t qpp_mode, qpp_index;
+  // the largest union learned fusion's bucket sort reaches in this call (0: kJsUMax);
+  // the fallback pass takes a learned pair above it or marked below it
+  int32_t learned_reach;
 };
 // perm element i (m * out_stride + base + rank): every kernel writes perm through
 // these, so one flag switches a call between the uint16 and uint32 layouts

@@ -75,8 +75,13 @@ def run_all_methods(runs_dir: Path, qpp_dir: Path, fused_dir: Path, qpp_model: s
 def evaluate_fused_runs(fused_dir: Path, qrels_path: Path, output_dir: Path):
     """scripts/06_eval_fusion.py:52-140 on qppfuse (without its printed table)."""
     from qppfuse.config import config
-    from qppfuse.data_utils import load_qrels, load_run_file
+    from qppfuse.data_utils import load_qrels, load_run_file as _load_run
     from qppfuse.evaluation import IREvaluator
+
+    def load_run_file(run_path):  # scripts/06_eval_fusion.py:42-49
+        return {qid: sorted([(d, s) for d, s, r in docs], key=lambda x: -x[1])
+                for qid, docs in _load_run(run_path).items()}
+
     qrels = load_qrels(qrels_path)
     res_files = sorted(fused_dir.glob("*.res"))
     evaluator = IREvaluator(metrics=config.evaluation.ir_metrics[:6])

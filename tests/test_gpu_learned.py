@@ -200,11 +200,12 @@ def test_learned_fusion_matches_reference_pandas(gpu, name, ties, tmp_path, caps
 def test_learned_fusion_large_lists_join_and_sort_in_one_kernel(gpu, k, ties):
     """5 runs x top-k (C5's shape: 1,025-5,120 entries per query, micro-unit
     scores) take join_learned_kernel — the join, the Kahan sums and the docid-tie
-    bucket sort in one workgroup — bit for bit the reference's pandas calls."""
+    bucket sort in one workgroup, unions up to 4,608 (SURVEY §8(d)'s ~4,030) — bit
+    for bit the reference's pandas calls; larger unions take the fallback pass."""
     from qppfuse import fusion
     rng = np.random.default_rng(k + ties)
     model = _model("fusion_multioutput")
-    qids = [f"test{i}" for i in range(12)]
+    qids = [f"test{i}" for i in range(24)]
     runs = _runs(rng, qids, ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade"], k, ties=ties)
     qpp = {q: {r: [float(np.round(v, 6)) for v in rng.uniform(0, 1, 13)]
                for r in model.retrievers} for q in qids}
@@ -214,6 +215,10 @@ def test_learned_fusion_large_lists_join_and_sort_in_one_kernel(gpu, k, ties):
     assert list(got.keys()) == sorted(want.keys())
     for q in want:
         assert got[q] == want[q], q
+    if k == 1000:  # unions on both sides of kJsUMax and of kLearnedUMax
+        us = [len(want[q]) for q in qids]
+        assert any(u <= 3072 for u in us) and any(3072 < u <= 4608 for u in us)
+        assert any(u > 4608 for u in us)
     for q in qids[:3]:  # and the ranked order write_runfile takes
         ids, sc = got.arrays(q)
         w = sorted(want[q], key=lambda x: x[1], reverse=True)
