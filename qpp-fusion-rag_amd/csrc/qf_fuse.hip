@@ -1089,12 +1089,6 @@ constexpr int kFastBits = 12, kFastNB = 1 << kFastBits, kFastMinBase = kFastNB -
 constexpr int kFastBitsL = 13, kFastNBL = 1 << kFastBitsL,
               kFastMinBaseL = kFastNBL - kFastNBL / 16;
 constexpr int kFastUMaxL = 5120;
-#ifndef QF_DEV_SORT_UNIFIED  // development A/B knob (tools/dev): one configuration for all U
-#define QF_DEV_SORT_UNIFIED 0
-#endif
-#ifndef QF_DEV_BIG_CFG  // development A/B knob: the configuration of unions above 3,072
-#define QF_DEV_BIG_CFG 0
-#endif
 constexpr int kFastDeltaShift = 8;   // delta = range / 2^8 (tools/bsort_sim.py, round 3)
 constexpr int kFastRetryShift = 20;  // the recount after a bucket overflow
 
@@ -2011,6 +2005,18 @@ struct BsFastShared {
   uint32_t big, nan;
 };
 
+// one 16-byte LDS store: the compiler splits a uint4 store whose registers it did
+// not allocate as an aligned tuple into b96 + write2 + b32 stores, which at the
+// scan's 32-byte lane stride conflict eight ways (round 5: 53 us of the 1,024-thread
+// configuration's 332; two-way as one b128)
+typedef unsigned int qf_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_store_b128(void* at, uint32_t a, uint32_t b, uint32_t c,
+                                               uint32_t d) {
+  const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)at;
+  const qf_u32x4 v = {a, b, c, d};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
 // UMIN < U <= UMAX of the pairs this configuration sorts; BITS: 2^BITS buckets (the
 // last 1/16 the minimum's sub-buckets); S32: u32 bucket starts.
 template <int BLOCK, int UMIN, int UMAX, int BITS, bool S32, int MINW>
@@ -2045,10 +2051,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
   const int ms = (int)(grp8 - gq * M);
   if ((p.methods & QF_LEARNED) && ms == __popc(p.methods & (QF_LEARNED - 1))) return;
   if (q >= p.n_queries) return;
+  // the three loads in flight together (the offsets before the range check: one
+  // memory latency, not two, before the scores' loads can issue)
   const int U = p.union_count[q];
-  if (U < 1 || U <= UMIN || U > UMAX) return;  // a status, or another kernel's
   const int64_t base = p.list_off[q * p.R];
   const int64_t nq = p.list_off[q * p.R + p.R] - base;
+  if (U < 1 || U <= UMIN || U > UMAX) return;  // a status, or another kernel's
   const double* io = p.fused + (int64_t)ms * p.out_stride + base;
   const int64_t po = (int64_t)ms * p.out_stride + base;
   const int rows = (U + BLOCK - 1) / BLOCK;
@@ -2225,8 +2233,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
     if constexpr (S32) {
 #pragma unroll
       for (int i = 0; i < kPer / 4; ++i)
-        ((uint4*)bk32)[tid * (kPer / 4) + i] =
-            make_uint4(pre + c[4 * i], pre + c[4 * i + 1], pre + c[4 * i + 2], pre + c[4 * i + 3]);
+        lds_store_b128(&bk32[(tid * (kPer / 4) + i) * 4], pre + c[4 * i], pre + c[4 * i + 1],
+                       pre + c[4 * i + 2], pre + c[4 * i + 3]);
       if (tid == 0) bk32[NB] = (uint32_t)U;
     } else {
       const uint32_t pre2 = pre * 0x10001u;  // (starts <= U < 2^16: no carry between halves)
@@ -2236,8 +2244,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
       if constexpr (kPer >= 8) {
 #pragma unroll
         for (int i = 0; i < kPer / 8; ++i)
-          ((uint4*)bk)[tid * (kPer / 8) + i] =
-              make_uint4(pk[4 * i], pk[4 * i + 1], pk[4 * i + 2], pk[4 * i + 3]);
+          lds_store_b128(&bk[(tid * (kPer / 8) + i) * 8], pk[4 * i], pk[4 * i + 1], pk[4 * i + 2],
+                         pk[4 * i + 3]);
       } else {
         ((uint2*)bk)[tid] = make_uint2(pk[0], pk[1]);
       }
@@ -3310,30 +3318,13 @@ hipError_t fuse_launch(const FuseParams& p0, int kind, int max_entries, hipStrea
       else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
       else launch_join<JoinXL>(p, kind, st);
     }
-    const int M = __builtin_popcount((unsigned)p.methods);
     if (p.methods & ~QF_LEARNED) {
-      const dim3 grid = grid_for((p.n_queries + 7) / 8 * 8 * M);
-      if (QF_DEV_SORT_UNIFIED && max_entries > kJsUMax) {
-        hipLaunchKernelGGL((bsort_fast_kernel<1024, 0, kFastUMaxL, kFastBitsL, true, 8>), grid,
-                           dim3(1024), 0, st, p);
-      } else {
-        hipLaunchKernelGGL((bsort_fast_kernel<512, 0, kJsUMax, kFastBits, false, 8>), grid,
-                           dim3(512), 0, st, p);
-        if (max_entries > kJsUMax) {  // unions above 3,072 (SURVEY §8(d)'s C2: ~4,030)
-          if (QF_DEV_BIG_CFG == 1)
-            hipLaunchKernelGGL((bsort_fast_kernel<512, kJsUMax, kFastUMaxL, 12, false, 4>), grid,
-                               dim3(512), 0, st, p);
-          else if (QF_DEV_BIG_CFG == 2)
-            hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, 12, false, 8>), grid,
-                               dim3(1024), 0, st, p);
-          else if (QF_DEV_BIG_CFG == 3)
-            hipLaunchKernelGGL((bsort_fast_kernel<512, kJsUMax, kFastUMaxL, 13, false, 4>), grid,
-                               dim3(512), 0, st, p);
-          else
-            hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, kFastBitsL, true, 8>),
-                               grid, dim3(1024), 0, st, p);
-        }
-      }
+      const dim3 grid = grid_for((p.n_queries + 7) / 8 * 8 * __builtin_popcount((unsigned)p.methods));
+      hipLaunchKernelGGL((bsort_fast_kernel<512, 0, kJsUMax, kFastBits, false, 8>), grid,
+                         dim3(512), 0, st, p);
+      if (max_entries > kJsUMax)  // unions above 3,072 (SURVEY §8(d)'s C2: 3,856-4,148)
+        hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, kFastBitsL, true, 8>),
+                           grid, dim3(1024), 0, st, p);
     }
     if ((p.methods & QF_LEARNED) && !learned_only)
       hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),

@@ -156,6 +156,8 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     s_fmask[w] = fmask;
   }
   __syncthreads();
+  QF_STOP(31, [&] { return (uint32_t)__double2loint(x) + nt_raw + __double2loint(tf0 + tf1); },
+          if (_qf_acc == 12345u && lv) out[l * kQppCols] = 0.0; return;);
 
   // ---- B (lane = list): the chains that need only rsv, on three waves at once.
   // The serial loops run to kQppK unrolled (rows are kRow long; values past k
@@ -221,6 +223,8 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   }
   if (w <= 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
+  QF_STOP(32, [&] { return (uint32_t)__double2loint(s_mu[w] + s_cum[w] + s_vmax[w] + s_mf[w]) + nt_raw + __double2loint(tf0 + tf1); },
+          if (_qf_acc == 12345u && lv) out[l * kQppCols] = 0.0; return;);
 
   // ---- C (each list's wave): the per-element terms (transcendentals once each)
   const int numTerms = nt_raw > 1 ? nt_raw : 1;  // Math.max(1, terms.length)
@@ -247,6 +251,8 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   const double mx = wave_max(act ? x : -INFINITY);
   const double mn = wave_min(act ? x : INFINITY);
   __syncthreads();
+  QF_STOP(33, [&] { return (uint32_t)__double2loint(mx + mn) + nt_raw + __double2loint(tf0 + tf1 + uefw + wsum); },
+          if (_qf_acc == 12345u && lv) out[l * kQppCols] = 0.0; return;);
 
   // ---- D: the left-to-right sums (wave 0, lane = list * 8 + row: SMV, WIG, SNQC,
   // UEF, NQC's simple sum of (x - mu)^2), SigmaX pass 2 (wave 1) and RSD's
@@ -294,11 +300,15 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
   }
   if (w <= 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
+  QF_STOP(34, [&] { return (uint32_t)__double2loint(mx + mn + s_res[w][0] + s_var[w] + s_sigmax[w]) + nt_raw + __double2loint(tf0 + tf1 + uefw + wsum); },
+          if (_qf_acc == 12345u && lv) out[l * kQppCols] = 0.0; return;);
 
   // ---- E (each list's wave): RSD's skewness terms, over the row D has consumed
   const double std_full = sqrt(s_var[w]);
   s_t[w][4][lane] = act ? cube((x - mu) / std_full) : 0.0;
   __syncthreads();
+  QF_STOP(35, [&] { return (uint32_t)__double2loint(mx + mn + s_res[w][0] + s_var[w] + s_sigmax[w]) + nt_raw + __double2loint(tf0 + tf1 + uefw + wsum); },
+          if (_qf_acc == 12345u && lv) out[l * kQppCols] = 0.0; return;);
 
   // ---- F (wave 0, lane = list): the skewness sum
   if (w == 0 && lane < kQppLists) {

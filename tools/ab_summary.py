@@ -18,7 +18,12 @@ def short(name):
     return base.split("<")[0][-24:]
 
 
-if mode == "kstats":
+if mode == "kbench":
+    f = glob.glob(f"{path}/**/run_kernel_stats.csv", recursive=True)[0]
+    t = {short(r["Name"]): round(float(r["AverageNs"]) / 1e3, 1) for r in csv.DictReader(open(f))
+         if "qf::" in r["Name"] and "synth" not in r["Name"] and "copy" not in r["Name"]}
+    print(tag, t, flush=True)
+elif mode == "kstats":
     f = glob.glob(f"{path}/**/run_kernel_stats.csv", recursive=True)[0]
     log = open(sys.argv[3]).read()
     dg = re.findall(r"ok ([0-9a-f]{16})", log)
