@@ -107,6 +107,18 @@ __device__ __forceinline__ double cube(double x) {
 //   E  per element: ((x - mu) / std)^3                      [every wave]
 //   F  chain: the skewness sum                              [wave 0]
 
+// A chain's next kBatch values read together: volatile, so the compiler cannot sink
+// each read into its predicated step (it did: one exposed LDS latency per step of
+// every serial chain — 50 per chain, the workgroup's critical path), and the reads'
+// latency overlaps the previous batch's arithmetic.
+constexpr int kBatch = 10;
+__device__ __forceinline__ void lds_batch(const double* row, int j0, double (&b)[kBatch]) {
+  typedef __attribute__((address_space(3))) const volatile double lds_f64;
+  lds_f64* r = (lds_f64*)(__attribute__((address_space(3))) const double*)row;
+#pragma unroll
+  for (int t = 0; t < kBatch; ++t) b[t] = r[j0 + t];
+}
+
 constexpr int kQppLists = 8;
 constexpr int kQppBlock = 64 * kQppLists;
 constexpr int kRows = 5;     // smv, wig, snqc, uw, (x - mu)^2; then the skew terms
@@ -173,9 +185,12 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     Kahan kp;
     kahan_init(kp);
 #pragma unroll
-    for (int j = 0; j < kQppK; ++j) {
-      const double v = s_x[lane][j];
-      if (j < kl) kahan_add(kp, v);
+    for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+      double b[kBatch];
+      lds_batch(s_x[lane], j0, b);
+#pragma unroll
+      for (int t = 0; t < kBatch; ++t)
+        if (j0 + t < kl) kahan_add(kp, b[t]);
     }
     s_mu[lane] = kl > 0 ? div_int(kahan_final(kp), kl) : 0.0;
   } else if (w == 1 && lane < kQppLists) {
@@ -189,9 +204,12 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       Kahan kf;
       kahan_init(kf);
 #pragma unroll
-      for (int j = 0; j < kQppK; ++j) {
-        const double v = s_x[lane][j];
-        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kf, v);
+      for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+        double b[kBatch];
+        lds_batch(s_x[lane], j0, b);
+#pragma unroll
+        for (int t = 0; t < kBatch; ++t)
+          if (j0 + t < kl && ((fm >> (j0 + t)) & 1ull)) kahan_add(kf, b[t]);
       }
       mf = div_int(kahan_final(kf), nf);
     }
@@ -204,17 +222,22 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const int kl = s_k[lane];
     double mean = 0.0, m2 = 0.0, cum = 0.0, vmax = 0.0;
 #pragma unroll
-    for (int j = 0; j < kQppK; ++j) {
-      const double v = s_x[lane][j];
-      const double inv = 1.0 / (double)(j + 1);  // a literal: the loop is unrolled
-      if (j < kl) {
-        const double d = v - mean;
-        mean = fma(d, inv, mean);
-        m2 = fma(d, v - mean, m2);
-        if (j >= 1) {
-          const double var = m2 * inv;
-          cum += var;
-          vmax = fmax(vmax, var);
+    for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+      double b[kBatch];
+      lds_batch(s_x[lane], j0, b);
+#pragma unroll
+      for (int t = 0; t < kBatch; ++t) {
+        const int j = j0 + t;
+        const double inv = 1.0 / (double)(j + 1);  // a literal: the loop is unrolled
+        if (j < kl) {
+          const double d = b[t] - mean;
+          mean = fma(d, inv, mean);
+          m2 = fma(d, b[t] - mean, m2);
+          if (j >= 1) {
+            const double var = m2 * inv;
+            cum += var;
+            vmax = fmax(vmax, var);
+          }
         }
       }
     }
@@ -265,9 +288,12 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const double* row = s_t[ll][c];
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < kQppK; ++j) {
-      const double v = row[j];
-      if (j < len) acc += v;
+    for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+      double b[kBatch];
+      lds_batch(row, j0, b);
+#pragma unroll
+      for (int t = 0; t < kBatch; ++t)
+        if (j0 + t < len) acc += b[t];
     }
     s_res[ll][c] = acc;
   } else if (w == 1 && lane < kQppLists) {  // SigmaX, pass 2 (pass 1 in B)
@@ -280,9 +306,14 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
       Kahan kfv;
       kahan_init(kfv);
 #pragma unroll
-      for (int j = 0; j < kQppK; ++j) {
-        const double dv = s_x[lane][j] - mf;
-        if (j < kl && ((fm >> j) & 1ull)) kahan_add(kfv, dv * dv);
+      for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+        double b[kBatch];
+        lds_batch(s_x[lane], j0, b);
+#pragma unroll
+        for (int t = 0; t < kBatch; ++t) {
+          const double dv = b[t] - mf;
+          if (j0 + t < kl && ((fm >> (j0 + t)) & 1ull)) kahan_add(kfv, dv * dv);
+        }
       }
       sigmax = sqrt(div_int(kahan_final(kfv), nf));
     }
@@ -292,9 +323,12 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     Kahan kv;
     kahan_init(kv);
 #pragma unroll
-    for (int j = 0; j < kQppK; ++j) {
-      const double v = s_t[lane][4][j];
-      if (j < kl) kahan_add(kv, v);
+    for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+      double b[kBatch];
+      lds_batch(s_t[lane][4], j0, b);
+#pragma unroll
+      for (int t = 0; t < kBatch; ++t)
+        if (j0 + t < kl) kahan_add(kv, b[t]);
     }
     s_var[lane] = kl > 0 ? div_int(kahan_final(kv), kl) : 0.0;
   }
@@ -316,9 +350,12 @@ __global__ __launch_bounds__(kQppBlock, 8) void qpp_raw_kernel(
     const int kl = s_k[lane];
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < kQppK; ++j) {
-      const double v = s_t[lane][4][j];
-      if (j < kl) acc += v;
+    for (int j0 = 0; j0 < kQppK; j0 += kBatch) {
+      double b[kBatch];
+      lds_batch(s_t[lane][4], j0, b);
+#pragma unroll
+      for (int t = 0; t < kBatch; ++t)
+        if (j0 + t < kl) acc += b[t];
     }
     s_skew[lane] = acc;
     __builtin_amdgcn_s_setprio(0);
