@@ -45,7 +45,7 @@ for k, d in pmc.items():
                   "insts_valu": v,
                   "avg_ns": stats.get(k)}
 # qf_fuse = its join kernel + the sort kernels (every launch of one qf_fuse call)
-parts = [k for k in summary if any(s in k for s in ("join_kernel", "fuse_kernel", "fuse_large_kernel", "bsort_kernel", "bucket_sort_kernel", "join_sort_kernel", "join_learned_kernel", "join_sort_all_kernel", "join_sort_xl_kernel"))]
+parts = [k for k in summary if any(s in k for s in ("join_kernel", "fuse_kernel", "fuse_large_kernel", "bsort_kernel", "bsort_fast_kernel", "bucket_sort_kernel", "join_sort_kernel", "join_learned_kernel", "join_sort_all_kernel", "join_sort_xl_kernel"))]
 if parts:
     tot = lambda f: (None if any(summary[k][f] is None for k in parts)
                      else sum(summary[k][f] for k in parts))
