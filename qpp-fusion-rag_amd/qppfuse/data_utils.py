@@ -7,6 +7,8 @@ load_qpp_scores :262-293).  Host text parsing — no compute to accelerate.
 from __future__ import annotations
 
 from collections import defaultdict
+
+import numpy as np
 from pathlib import Path
 from typing import Dict, List, Tuple, Union
 
@@ -26,7 +28,38 @@ def load_qrels(qrels_path: PathLike) -> Dict[str, Dict[str, int]]:
 
 
 def load_run_file(run_path: PathLike) -> Dict[str, List[Tuple[str, float, int]]]:
-    """TREC run -> {qid: [(docid, score, rank)]} sorted by rank (stable)."""
+    """TREC run -> {qid: [(docid, score, rank)]} sorted by rank (stable), queries in
+    first-appearance order (src/data_utils.py:204-231).  The file is parsed by the
+    native loader (qfio, as load_runs: the same float() / int() values); a file it
+    rejects (a line without exactly 6 fields — the reference skips lines with fewer
+    and ignores fields past the sixth) takes the reference's line loop."""
+    try:
+        from .fastio import read_run_rows
+        qids, docnos, rq, rd, rr, rsc = read_run_rows(str(run_path))
+    except ValueError:  # a format the loader rejects: the reference's loop decides
+        return _load_run_file_lines(run_path)
+    if len(rq) == 0:
+        return {}
+    # queries by first appearance; rows of a query by rank, stable (file order)
+    _, first = np.unique(rq, return_index=True)
+    qorder = np.argsort(first, kind="stable")      # codes in first-appearance order
+    pos = np.empty(len(first), np.int64)
+    pos[qorder] = np.arange(len(first))
+    order = np.lexsort((rr, pos[rq]))               # stable: ties keep file order
+    q_sorted = pos[rq][order]
+    bounds = np.flatnonzero(np.diff(q_sorted)) + 1
+    d_col = docnos[rd[order]].tolist()
+    s_col = rsc[order].tolist()
+    r_col = rr[order].tolist()
+    rows = list(zip(d_col, s_col, r_col))
+    starts = [0] + bounds.tolist()
+    ends = bounds.tolist() + [len(rows)]
+    codes = qorder.tolist()
+    return {str(qids[codes[i]]): rows[a:b] for i, (a, b) in enumerate(zip(starts, ends))}
+
+
+def _load_run_file_lines(run_path: PathLike) -> Dict[str, List[Tuple[str, float, int]]]:
+    """src/data_utils.py:218-231, line by line."""
     out: Dict[str, list] = defaultdict(list)
     with open(run_path, "r") as fh:
         for line in fh:

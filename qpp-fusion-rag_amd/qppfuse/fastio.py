@@ -282,6 +282,40 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
     return rs, frames
 
 
+def read_run_rows(path: str, n_threads: int = 0):
+    """One TREC run file's rows in file order: (qids, docnos, qid code, docno code,
+    rank, score) — the string tables as object arrays, the codes into them, rank
+    int64 and score float64 as parsed by qfio (the loader of load_runs).  Raises
+    ValueError for a file the loader rejects (a line without exactly 6 fields),
+    FileNotFoundError for a missing one."""
+    L = lib()
+    arr = (C.c_char_p * 1)(os.fsencode(path))
+    h = _vp()
+    _check(L.qfio_load_runs(arr, 1, int(n_threads), C.byref(h)), "read_run_rows")
+    try:
+        sz = np.zeros(8, np.int64)
+        L.qfio_runset_sizes(h, _p(sz))
+        Q, D, E, qb, db = (int(x) for x in sz[:5])
+        n_iter, n_tag = int(sz[6]) & 0xFFFFFFFF, int(sz[6]) >> 32
+        ib, tb = int(sz[7]) & 0xFFFFFFFF, int(sz[7]) >> 32
+        qo, qc = np.empty(Q + 1, np.int64), np.zeros(max(qb, 1), np.uint8)
+        do, dc = np.empty(D + 1, np.int64), np.empty(max(db, 1), np.uint8)
+        io, ic = np.empty(n_iter + 1, np.int64), np.zeros(max(ib, 1), np.uint8)
+        to, tc = np.empty(n_tag + 1, np.int64), np.zeros(max(tb, 1), np.uint8)
+        L.qfio_runset_strings(h, _p(qo), _p(qc), _p(do), _p(dc), _p(io), _p(ic), _p(to), _p(tc))
+        L.qfio_runset_drop_text(h)
+        owner = _RunSetOwner(h)
+        h = None
+        ptrs = (C.c_void_p * 12)()
+        L.qfio_runset_views(owner.h, ptrs)
+        rq, rd = owner.array(ptrs[6], E, np.uint32), owner.array(ptrs[7], E, np.uint32)
+        rr, rsc = owner.array(ptrs[10], E, np.int64), owner.array(ptrs[11], E, np.float64)
+    finally:
+        if h is not None:
+            L.qfio_runset_free(h)
+    return _strings(qo, qc), _strings(do, dc), rq, rd, rr, rsc
+
+
 def string_table(rs, which: str) -> Tuple[np.ndarray, bytes]:
     """(offsets [n+1], bytes) of a RunSet's qids or docnos (cached)."""
     tab = getattr(rs, "_strtab", None)

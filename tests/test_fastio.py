@@ -559,3 +559,21 @@ def test_rawarray_large_then_small_resize(tmp_path):
                    timeout=300)
     r = subprocess.run([str(exe)], env=dict(os.environ, MALLOC_CHECK_="3"), timeout=60)
     assert r.returncode == 0
+
+
+@pytest.mark.parametrize("extra", ["", "q1 Q0 short 1\n", "q2 Q0 d7 3 0.5 tag more\n"])
+def test_load_run_file_native_equals_the_reference_loop(tmp_path, extra):
+    """data_utils.load_run_file parses with qfio and builds the reference's dict
+    (src/data_utils.py:204-231: first-appearance query order, rows stably sorted by
+    rank, float / int values); a file qfio rejects takes the reference's loop."""
+    from qppfuse import data_utils as du
+    rng = np.random.default_rng(3)
+    lines = [f"q{rng.integers(0, 40)} Q0 d{rng.integers(0, 500)} {rng.integers(1, 60)} "
+             f"{rng.random() * 20:.6f} run\n" for _ in range(4000)]
+    lines += ["q3 Q0 dX 7 1e-7 run\n", "q9 Q0 dY 2 -3.25 tagg\n", "q9 Q0 dZ 2 21.35099 tagg\n"]
+    p = tmp_path / "run.res"
+    p.write_text("".join(lines) + extra)
+    got = du.load_run_file(p)
+    want = du._load_run_file_lines(p)
+    assert list(got) == list(want)
+    assert got == want
