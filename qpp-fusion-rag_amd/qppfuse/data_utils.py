@@ -51,11 +51,20 @@ def load_run_file(run_path: PathLike) -> Dict[str, List[Tuple[str, float, int]]]
     d_col = docnos[rd[order]].tolist()
     s_col = rsc[order].tolist()
     r_col = rr[order].tolist()
-    rows = list(zip(d_col, s_col, r_col))
-    starts = [0] + bounds.tolist()
-    ends = bounds.tolist() + [len(rows)]
-    codes = qorder.tolist()
-    return {str(qids[codes[i]]): rows[a:b] for i, (a, b) in enumerate(zip(starts, ends))}
+    # millions of tuples: without the cyclic collector's passes over them (they hold
+    # no cycles), 13 -> ~1.5 s for C2's 14 M rows
+    import gc
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        rows = list(zip(d_col, s_col, r_col))
+        starts = [0] + bounds.tolist()
+        ends = bounds.tolist() + [len(rows)]
+        codes = qorder.tolist()
+        return {str(qids[codes[i]]): rows[a:b] for i, (a, b) in enumerate(zip(starts, ends))}
+    finally:
+        if enabled:
+            gc.enable()
 
 
 def _load_run_file_lines(run_path: PathLike) -> Dict[str, List[Tuple[str, float, int]]]:

@@ -138,6 +138,9 @@ def _run_arrays(run) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray, np.
         groups = {k: list(zip(g["d"], g["s"])) for k, g in df.groupby("q", sort=False)}
         run = groups
     qids = [str(k) for k in run.keys()]
+    fast = _run_arrays_flat(run, qids)
+    if fast is not None:
+        return fast
     per_q = []
     for qid in run:
         items = run[qid]
@@ -161,6 +164,34 @@ def _run_arrays(run) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray, np.
     docid = np.concatenate(docid_parts) if docid_parts else np.zeros(0, np.uint32)
     score = np.concatenate(score_parts) if score_parts else np.zeros(0)
     return qids, all_docs, off, docid, score
+
+
+def _run_arrays_flat(run, qids):
+    """_run_arrays for a run without a repeated (query, docno): the same arrays from
+    one flat pass — docnos sorted and coded by pandas.factorize, each query's list
+    ordered by a stable lexsort on (query, -score) — instead of per-query dicts and a
+    binary search of every docno in the sorted table (C2's 14 M rows: ~1 min -> s).
+    None when a query repeats a docno (the dict semantics decide: the slow path)."""
+    lists = []
+    for qid in run:
+        items = run[qid]
+        lists.append(list(items.items()) if isinstance(items, Mapping) else items)
+    lens = np.fromiter((len(x) for x in lists), dtype=np.int64, count=len(lists))
+    n = int(lens.sum())
+    off = np.zeros(len(lists) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    if n == 0:
+        return qids, np.zeros(0, dtype=object), off, np.zeros(0, np.uint32), np.zeros(0)
+    docs = np.empty(n, dtype=object)
+    docs[:] = [str(it[0]) for x in lists for it in x]
+    sc = np.fromiter((float(it[1]) for x in lists for it in x), dtype=np.float64, count=n)
+    codes, uniq = pd.factorize(docs, sort=True)
+    qi = np.repeat(np.arange(len(lists), dtype=np.int64), lens)
+    if np.unique(qi * len(uniq) + codes).size != n:
+        return None
+    order = np.lexsort((-sc, qi))  # stable: equal scores keep their list order
+    all_docs = np.asarray(uniq, dtype=object)
+    return qids, all_docs, off, codes[order].astype(np.uint32), sc[order]
 
 
 class IREvaluator:

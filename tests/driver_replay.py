@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 from pathlib import Path
 from typing import Dict, Iterable, List, Optional
 
@@ -88,6 +89,7 @@ def evaluate_fused_runs(fused_dir: Path, qrels_path: Path, output_dir: Path):
     results = []
     for res_file in res_files:
         method_name = res_file.stem
+        print(f"[eval] {method_name}", file=sys.stderr, flush=True)  # (the script prints too)
         run = load_run_file(res_file)
         if method_name.startswith("learned"):
             method_type = "learned"
@@ -158,6 +160,7 @@ def check_sample(runs_dir: Path, qpp_dir: Path, results: Dict[str, Path], qids: 
             "wcombsum": f"wcombsum-{m}", "wcombmnz": f"wcombmnz-{m}", "wrrf": f"wrrf-{m}"}
     ok = {}
     for key, path in results.items():
+        print(f"[check] {path.name}", file=sys.stderr, flush=True)
         if key in tags:
             fused = ref_port.fuse(frames, key, qpp, qidx, rrf_k)
             want = ref_port.runfile_text(fused, tags[key])
@@ -179,32 +182,41 @@ def check_sample(runs_dir: Path, qpp_dir: Path, results: Dict[str, Path], qids: 
 
 
 def check_eval(fused_dir: Path, qrels_path: Path, results_json: List[dict]) -> bool:
-    """comparison_results.json == the C trec_eval restatement's means, metric by metric."""
+    """comparison_results.json == the C trec_eval restatement's means, metric by metric.
+    Each file's rows straight from the native loader (qfio, the values float() gives),
+    documents coded in one sorted table with the qrels' (no per-row Python tuples)."""
     from oracle import _loader as coracle
     from qppfuse.config import config
-    from qppfuse.data_utils import load_qrels, load_run_file
+    from qppfuse.data_utils import load_qrels
+    from qppfuse.fastio import read_run_rows
     qrels = load_qrels(qrels_path)
     names = config.evaluation.ir_metrics[:6]
     by_method = {r["method"]: r for r in results_json}
     for res_file in sorted(fused_dir.glob("*.res")):
-        run = load_run_file(res_file)
-        qids = [q for q in run if q in qrels]
-        docnos = sorted({d for q in qids for d, *_ in run[q]} |
-                        {d for q in qids for d in qrels[q]})
-        did = {d: i for i, d in enumerate(docnos)}
-        roff, rdoc, rsc = [0], [], []
+        print(f"[check_eval] {res_file.name}", file=sys.stderr, flush=True)
+        qids, docnos, rq, rd, rr, rsc = read_run_rows(str(res_file))
+        # queries in first-appearance order, those with qrels (06: q in qrels)
+        _, first = np.unique(rq, return_index=True)
+        qorder = np.argsort(first, kind="stable")
+        keep = np.array([str(qids[c]) in qrels for c in qorder], dtype=bool)
+        qsel = qorder[keep]
+        pos = np.full(len(qids), -1, np.int64)
+        pos[qsel] = np.arange(len(qsel))
+        rows = np.flatnonzero(pos[rq] >= 0)
+        qrel_docs = [d for c in qsel for d in qrels[str(qids[c])]]
+        table = np.unique(np.concatenate([docnos, np.asarray(qrel_docs, dtype=object)]))
+        did = np.searchsorted(table, docnos).astype(np.uint32)
+        order = rows[np.argsort(pos[rq[rows]], kind="stable")]
+        cnt = np.bincount(pos[rq[order]], minlength=len(qsel))
+        roff = np.zeros(len(qsel) + 1, np.int64)
+        np.cumsum(cnt, out=roff[1:])
         qo, qd, qr = [0], [], []
-        for q in qids:
-            lst = run[q]
-            rdoc += [did[d] for d, *_ in lst]
-            rsc += [s for _, s, *_ in lst]
-            roff.append(len(rdoc))
-            for d, rel in qrels[q].items():
-                qd.append(did[d])
+        for c in qsel:
+            for d, rel in qrels[str(qids[c])].items():
+                qd.append(int(np.searchsorted(table, d)))
                 qr.append(rel)
             qo.append(len(qd))
-        vals = coracle.evaluate(np.array(roff, np.int64), np.array(rdoc, np.uint32),
-                                np.array(rsc, np.float64), np.array(qo, np.int64),
+        vals = coracle.evaluate(roff, did[rd[order]], rsc[order], np.array(qo, np.int64),
                                 np.array(qd, np.uint32), np.array(qr, np.int32), names,
                                 text=True)
         got = by_method[res_file.stem]
@@ -214,6 +226,6 @@ def check_eval(fused_dir: Path, qrels_path: Path, results_json: List[dict]) -> b
             want = float(col.mean()) if col.size else 0.0
             if abs(got[name] - want) > 1e-12:
                 return False
-        if got["n_queries"] != len(qids):
+        if got["n_queries"] != len(qsel):
             return False
     return True
