@@ -55,10 +55,13 @@ if parts:
         "avg_ns": None if any(summary[k]["avg_ns"] is None for k in parts)
         else sum(summary[k]["avg_ns"] for k in parts)}
 # the correction checked on a known byte count: the min-max kernel reads every raw f64
-# score of the bench's C2 run set once (3,452 x 5 x 1,000) plus the list offsets
-mm = [k for k in summary if "minmax_per_query_kernel" in k]
+# score of the bench's C2 run set once (3,452 x 5 x 1,000) plus the list offsets (the
+# fused min-max + QPP column kernel also the 13 raw predictors of every list)
+mm = [k for k in summary if "minmax_per_query_kernel" in k or "minmax_colminmax_kernel" in k]
 if mm and summary[mm[0]]["fetch_size_raw_bytes"]:
     known = 3452 * 5 * 1000 * 8 + (3452 * 5 + 1) * 8
+    if "colminmax" in mm[0]:
+        known += 3452 * 5 * 13 * 8
     summary["fetch_calibration"] = {
         "kernel": mm[0], "known_read_bytes": known,
         "fetch_size_raw_bytes": summary[mm[0]]["fetch_size_raw_bytes"],
