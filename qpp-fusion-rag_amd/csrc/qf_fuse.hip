@@ -685,11 +685,15 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       if (d == kEmpty) status = QF_QSTATUS_BADDOC;
       while (e >= end) end = sh.offr[++r + 1];
       rj[j] = (uint32_t)r;
-      uint32_t h = (d * 0x9E3779B1u) >> (32 - C::kTB);
+      // triangular probes (h + 1, + 2, + 3 ...: every slot of the power-of-two table):
+      // no primary clustering.  A wave's row waits for its longest chain; on SURVEY
+      // §8(d)'s unions (table load ~0.5) linear probes made the insert 55 of the
+      // join's ~190 us, these 16 us less (round 5)
+      uint32_t h = (d * 0x9E3779B1u) >> (32 - C::kTB), step = 1u;
       while (true) {
         const uint32_t prev = atomicCAS(&tkey[h], kEmpty, d);
         if (prev == kEmpty || prev == d) break;
-        h = (h + 1) & (TS - 1);
+        h = (h + step++) & (TS - 1);
       }
       const uint32_t hs = (h & 1u) * 16u;
       const uint32_t old = atomicOr(&tmask2[h >> 1], (1u << r) << hs);
