@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import re
 from collections.abc import Mapping
+from operator import itemgetter
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -166,12 +167,38 @@ def _run_arrays(run) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray, np.
     return qids, all_docs, off, docid, score
 
 
+def _coded_by_table(flat, n):
+    """Rows whose docnos are the very str objects of the last table read_run_rows
+    returned (load_run_file's rows, through the 06 script's per-query sort): their
+    codes into the run's sorted docnos by object identity and the table's Arrow sort
+    — (codes, sorted docnos), or None when any row holds another object."""
+    from .fastio import docno_tables
+    if not docno_tables or n == 0:
+        return None
+    tab = docno_tables[-1]
+    if len(tab.objs) == 0:
+        return None
+    at = tab.id_index().get_indexer(np.fromiter(map(id, map(itemgetter(0), flat)), np.uint64, n))
+    if at.min() < 0:                           # a row holds another object
+        return None
+    # (at: rows -> table positions; the table holds the objects, so no id is reused)
+    srt = tab.sorted_order()                   # table positions, ascending strings
+    used = np.zeros(len(srt), bool)
+    used[at] = True
+    srt = srt[used[srt]]                       # the run's docnos, ascending
+    rank = np.empty(len(used), np.int64)
+    rank[srt] = np.arange(len(srt))
+    return rank[at], tab.objs[srt]
+
+
 def _run_arrays_flat(run, qids):
     """_run_arrays for a run without a repeated (query, docno): the same arrays from
-    one flat pass — docnos sorted and coded by pandas.factorize, each query's list
-    ordered by a stable lexsort on (query, -score) — instead of per-query dicts and a
-    binary search of every docno in the sorted table (C2's 14 M rows: ~1 min -> s).
-    None when a query repeats a docno (the dict semantics decide: the slow path)."""
+    one flat pass — docnos coded by identity with load_run_file's table when the rows
+    hold its strings, else sorted and coded by pandas.factorize; each query's list
+    ordered by a stable lexsort on (query, -score) unless already in that order —
+    instead of per-query dicts and a binary search of every docno in the sorted
+    table (C2's 14 M rows: ~1 min -> s).  None when a query repeats a docno (the
+    dict semantics decide: the slow path)."""
     lists = []
     for qid in run:
         items = run[qid]
@@ -182,15 +209,24 @@ def _run_arrays_flat(run, qids):
     np.cumsum(lens, out=off[1:])
     if n == 0:
         return qids, np.zeros(0, dtype=object), off, np.zeros(0, np.uint32), np.zeros(0)
-    docs = np.empty(n, dtype=object)
-    docs[:] = [str(it[0]) for x in lists for it in x]
-    sc = np.fromiter((float(it[1]) for x in lists for it in x), dtype=np.float64, count=n)
-    codes, uniq = pd.factorize(docs, sort=True)
+    flat = [it for x in lists for it in x]
+    sc = np.fromiter(map(float, map(itemgetter(1), flat)), dtype=np.float64, count=n)
+    coded = _coded_by_table(flat, n)
+    if coded is not None:
+        codes, all_docs = coded
+    else:
+        docs = np.empty(n, dtype=object)
+        docs[:] = [str(d) for d in map(itemgetter(0), flat)]
+        codes, uniq = pd.factorize(docs, sort=True)
+        all_docs = np.asarray(uniq, dtype=object)
+    del flat
     qi = np.repeat(np.arange(len(lists), dtype=np.int64), lens)
-    if np.unique(qi * len(uniq) + codes).size != n:
+    if np.unique(qi * len(all_docs) + codes).size != n:
         return None
-    order = np.lexsort((-sc, qi))  # stable: equal scores keep their list order
-    all_docs = np.asarray(uniq, dtype=object)
+    # stable: equal scores keep their list order (already so after 06's per-query sort)
+    if n > 1 and bool(np.all((sc[1:] <= sc[:-1]) | (qi[1:] != qi[:-1]))):
+        return qids, all_docs, off, codes.astype(np.uint32), sc
+    order = np.lexsort((-sc, qi))
     return qids, all_docs, off, codes[order].astype(np.uint32), sc[order]
 
 

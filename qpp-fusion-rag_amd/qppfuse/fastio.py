@@ -12,6 +12,7 @@ exact "%.6f".
 from __future__ import annotations
 
 import ctypes as C
+import collections
 import os
 from pathlib import Path
 from typing import Dict, List, Sequence, Tuple
@@ -282,6 +283,39 @@ def parse_runs(paths: Sequence[str], names: Sequence[str], n_threads: int = 0):
     return rs, frames
 
 
+class DocnoTable:
+    """The docno table of the last read_run_rows call: the object array of str it
+    returned with the UTF-8 offsets / bytes it was decoded from.  The evaluator
+    (evaluation._run_arrays_flat) codes rows that hold these very str objects by
+    identity — no hashing or sorting of millions of Python strings — and sorts the
+    table once in Arrow (byte order of UTF-8 = code-point order, Python's order)."""
+
+    def __init__(self, objs: np.ndarray, off: np.ndarray, chars: np.ndarray):
+        self.objs, self.off, self.chars = objs, off, chars
+        self._ids = self._sorted = None
+
+    def id_index(self) -> pd.Index:
+        """pandas Index of every element's id() (a hash table: position by identity)."""
+        if self._ids is None:
+            self._ids = pd.Index(np.fromiter(map(id, self.objs), np.uint64, len(self.objs)))
+        return self._ids
+
+    def sorted_order(self) -> np.ndarray:
+        """Element positions in ascending string order."""
+        if self._sorted is None:
+            import pyarrow as pa
+            import pyarrow.compute as pc
+            arr = pa.LargeStringArray.from_buffers(
+                len(self.objs), pa.py_buffer(np.ascontiguousarray(self.off, np.int64)),
+                pa.py_buffer(np.ascontiguousarray(self.chars, np.uint8)))
+            self._sorted = pc.sort_indices(arr).to_numpy().astype(np.int64)
+        return self._sorted
+
+
+# the last table only (a run being evaluated is the one just loaded): bounded memory
+docno_tables: "collections.deque[DocnoTable]" = collections.deque(maxlen=1)
+
+
 def read_run_rows(path: str, n_threads: int = 0):
     """One TREC run file's rows in file order: (qids, docnos, qid code, docno code,
     rank, score) — the string tables as object arrays, the codes into them, rank
@@ -313,7 +347,9 @@ def read_run_rows(path: str, n_threads: int = 0):
     finally:
         if h is not None:
             L.qfio_runset_free(h)
-    return _strings(qo, qc), _strings(do, dc), rq, rd, rr, rsc
+    docnos = _strings(do, dc)
+    docno_tables.append(DocnoTable(docnos, do, dc))
+    return _strings(qo, qc), docnos, rq, rd, rr, rsc
 
 
 def string_table(rs, which: str) -> Tuple[np.ndarray, bytes]:
