@@ -45,12 +45,17 @@ def load_run_file(run_path: PathLike) -> Dict[str, List[Tuple[str, float, int]]]
     qorder = np.argsort(first, kind="stable")      # codes in first-appearance order
     pos = np.empty(len(first), np.int64)
     pos[qorder] = np.arange(len(first))
-    order = np.lexsort((rr, pos[rq]))               # stable: ties keep file order
-    q_sorted = pos[rq][order]
+    pq = pos[rq]
+    if bool(np.all(pq[1:] >= pq[:-1])) and bool(np.all((rr[1:] >= rr[:-1]) | (pq[1:] != pq[:-1]))):
+        q_sorted, d_col, s_col, r_col = pq, docnos[rd].tolist(), rsc.tolist(), rr.tolist()
+    else:  # (a file already grouped by query in rank order — every run file this
+        # package writes — needs no sort: the stable sort below is the identity there)
+        order = np.lexsort((rr, pq))                # stable: ties keep file order
+        q_sorted = pq[order]
+        d_col = docnos[rd[order]].tolist()
+        s_col = rsc[order].tolist()
+        r_col = rr[order].tolist()
     bounds = np.flatnonzero(np.diff(q_sorted)) + 1
-    d_col = docnos[rd[order]].tolist()
-    s_col = rsc[order].tolist()
-    r_col = rr[order].tolist()
     # millions of tuples: without the cyclic collector's passes over them (they hold
     # no cycles), 13 -> ~1.5 s for C2's 14 M rows
     import gc

@@ -577,3 +577,20 @@ def test_load_run_file_native_equals_the_reference_loop(tmp_path, extra):
     want = du._load_run_file_lines(p)
     assert list(got) == list(want)
     assert got == want
+
+
+def test_load_run_file_grouped_file_equals_the_reference_loop(tmp_path):
+    """A file already grouped by query in rank order (ties included) takes
+    load_run_file's no-sort branch: the same dict as the reference's loop."""
+    from qppfuse import data_utils as du
+    rng = np.random.default_rng(8)
+    lines = []
+    for q in rng.permutation(30):
+        ranks = np.sort(rng.integers(1, 40, size=50))  # repeated ranks: stable ties
+        lines += [f"q{q} Q0 d{rng.integers(0, 900)} {r} {rng.random():.6f} run\n" for r in ranks]
+    p = tmp_path / "grouped.res"
+    p.write_text("".join(lines))
+    got = du.load_run_file(p)
+    want = du._load_run_file_lines(p)
+    assert list(got) == list(want)
+    assert got == want
