@@ -92,3 +92,24 @@ def test_repeated_docno_declines_both_ways(tmp_path):
     assert E._run_arrays_flat(run, qids) is None
     _, want = _both(run)
     assert want is None
+
+
+def test_non_ascii_docnos_sort_as_python_strings(tmp_path):
+    """The table's Arrow sort (UTF-8 bytes) orders docnos as Python's str order (code
+    points): accents, CJK, astral-plane and mixed-case ids."""
+    rng = np.random.default_rng(6)
+    alphabet = ["a", "B", "é", "É", "z", "中", "文", "\U0001F600", "ß", "0", "_"]
+    lines = []
+    for q in range(12):
+        docs = {"".join(rng.choice(alphabet, size=int(rng.integers(1, 6)))) + f"{q}_{i}"
+                for i in range(80)}
+        for i, d in enumerate(sorted(docs)):
+            lines.append(f"q{q} Q0 {d} {i + 1} {rng.random():.6f} t\n")
+    p = tmp_path / "u.res"
+    p.write_text("".join(lines), encoding="utf-8")
+    run = _wrapper(load_run_file(p))
+    qids = [str(k) for k in run]
+    got = E._run_arrays_flat(run, qids)
+    assert got is not None and list(got[1]) == sorted(got[1])
+    _, want = _both(run)
+    _assert_same(got, want)
