@@ -8,7 +8,8 @@ inputs already resident in HBM:
   1. per-query min-max of every list -> the .norm.res values (micro-units)
   2. 13 QPP predictors per (query, retriever) list (top_k = 100, k = 50)
   3. per-column min/max of the predictors (+ RCCL MIN all-reduce when N > 1)
-  4. normalise + "%.6f" + RSD weight per (query, retriever)
+  4. normalise all 13 columns + "%.6f" (the .qpp table, src/qpp.py:324-372) and the
+     RSD weight per (query, retriever) — inside the fusion launch (qf_fuse_qpp_micro)
   5. all six fusions (CombSUM, CombMNZ, RRF, W-CombSUM, W-CombMNZ, W-RRF) of
      every query, full fused lists sorted (what write_runfile needs).
 Queries shard across ranks (weak scaling); the only collective is the 1 KB
@@ -247,6 +248,9 @@ class Pipeline:
         self.micro = torch.empty(E, dtype=torch.int32, device=dev)
         self.qraw = torch.empty((Q * R, 13), dtype=torch.float64, device=dev)
         self.mm = torch.empty(2 * R * 13, dtype=torch.float64, device=dev)
+        # the .qpp table of the batch (every list's 13 "%.6f" values, src/qpp.py:324-334):
+        # written by the join (qf_fuse_qpp_micro) or the normalisation launch
+        self.qmicro = torch.empty(Q * R * 13, dtype=torch.int64, device=dev)
         self.out = engine.alloc_fuse_out(Q, E, engine.methods_mask(self.methods), dev)
         self.w = None
         if "learned" in self.methods:
@@ -374,13 +378,15 @@ class Pipeline:
             else:  # the mean of 13 columns per list: the normalisation launch (qf_fuse_qpp
                 # would put 13 normalisations per list on the join's start; C4: 0.665 ->
                 # 0.73 ms per step)
-                w = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax",
-                                    a.qpp_index, want_micro=False)["weights"]
+                nz = e.qpp_normalize(self.qraw, self.mm, self.off, self.R, "minmax",
+                                     a.qpp_index, want_micro=True)
+                w, self.qmicro = nz["weights"], nz["micro"]
         if timed:
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0.record()
         e.fuse(self.off, self.docid, self.micro, self.R, self.methods, 60, weights=w,
-               max_entries=self.R * self.K, out=self.out, qpp=qppw)
+               max_entries=self.R * self.K, out=self.out, qpp=qppw,
+               qpp_micro_out=self.qmicro if qppw is not None else None)
         if timed:
             t1.record()
             self.ev.append((t0, t1))
@@ -421,6 +427,10 @@ class Pipeline:
         weighted = any(m.startswith("w") or m == "learned" for m in self.methods)
         reads = N * (4 + 4) + (self.Q * self.R * 8 if weighted else 0) + (self.Q * self.R + 1) * 8
         writes = int(uc.sum()) * (4 + M * (2 + 8)) + self.Q * 4
+        if self.args.wl["qpp"] and self.args.qpp_index >= 0 and "learned" not in self.methods:
+            # qf_fuse_qpp_micro: the raw predictors in, the .qpp micro-units out
+            reads += self.Q * self.R * 13 * 8
+            writes += self.Q * self.R * 13 * 8
         return reads + writes, float(uc.mean())
 
 

@@ -231,6 +231,21 @@ int qf_fuse_qpp(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off
                 int64_t out_stride, void* stream);
 
 /*
+ * qf_fuse_qpp + the .qpp file's values: the join also writes qpp_micro_out[(q*R +
+ * r)*13 + c] = the "%.6f" micro-units of normalised predictor c of list (q, r) —
+ * qf_qpp_normalize's micro_out, bit for bit (src/qpp.py:324-334, 356-372) — for
+ * every column, so one fusion launch produces both the fused runs and the whole
+ * .qpp table the metric's "13 QPP" names.  n_retrievers <= 16.
+ */
+int qf_fuse_qpp_micro(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                      const uint32_t* docid, const void* score, int32_t score_kind,
+                      const int32_t* rank, const double* qpp_raw, const double* qpp_stats,
+                      int32_t qpp_mode, int32_t qpp_index, int32_t methods, int32_t rrf_k,
+                      int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
+                      uint16_t* perm, double* fused, int64_t out_stride, int64_t* qpp_micro_out,
+                      void* stream);
+
+/*
  * The explicit workspace of qf_fuse (the library allocates only in
  * an explicit workspace).  qf_fuse_workspace_bytes: the bytes a call with these
  * sizes would allocate stream-ordered for its workspace kernel (queries above
@@ -446,8 +461,9 @@ int qf_synth_runs(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int3
  * ln Beta(5, 2) - 0.001 (BM25_MonoT5, negative); the judged documents of qrel query q mod
  * n_qrel_queries (device CSR qrel_off[n+1] / qrel_doc: corpus ids) planted with
  * probability {0.9, 0.5, 0.9, 0.8, 0.9} at Geometric(0.15) ranks.  Counter-based
- * (Philox4x32-10 keyed by seed): any query range regenerates independently;
- * oracle/synth_oracle.c regenerates it bit for bit.  1 <= k <= 4096.
+ * (Philox4x32-10 keyed by seed, a 32-bit key word: seed > 0xFFFFFFFF fails with
+ * QF_EINVAL): any query range regenerates independently; oracle/synth_oracle.c
+ * regenerates it bit for bit.  1 <= k <= 4096.
  */
 int qf_synth_runs_nq(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, int32_t k,
                      uint64_t seed, const int64_t* qrel_off, const uint32_t* qrel_doc,

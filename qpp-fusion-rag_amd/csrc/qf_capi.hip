@@ -33,6 +33,7 @@ int check(hipError_t e, const char* what) {
 }
 
 constexpr int kMaxR = 32;  // qf_fuse: > 16 runs take the workspace kernel
+constexpr int kMaxRLds = 16;  // runs of the LDS join (qf_fuse_qpp_micro's values are its)
 }  // namespace
 
 extern "C" {
@@ -136,7 +137,8 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
                        void* stream, const char* fn, uint32_t learned_f32 = 0u,
                        void* ws = nullptr, size_t ws_bytes = 0,
                        const double* qpp_raw = nullptr, const double* qpp_stats = nullptr,
-                       int32_t qpp_mode = 0, int32_t qpp_index = -1) {
+                       int32_t qpp_mode = 0, int32_t qpp_index = -1,
+                       int64_t* qpp_micro = nullptr) {
   if (n_queries < 0 || n_retrievers <= 0 || n_retrievers > kMaxR)
     return fail(QF_EINVAL, "%s: n_retrievers must be in [1, %d]", fn, kMaxR);
   if (methods <= 0 ||
@@ -175,6 +177,7 @@ static int fuse_common(int64_t n_queries, int32_t n_retrievers, const int64_t* l
   p.qpp_stats = qpp_stats;
   p.qpp_mode = qpp_mode;
   p.qpp_index = qpp_index;
+  p.qpp_micro = qpp_micro;
   if (learned_f32) {
     const uint32_t all = n_retrievers == 32 ? 0xFFFFFFFFu : (1u << n_retrievers) - 1u;
     p.learned_f32 = learned_f32 & all;
@@ -221,6 +224,25 @@ int qf_fuse_qpp(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off
                      methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
                      0, fused, out_stride, stream, "qf_fuse_qpp", 0u, nullptr, 0, qpp_raw,
                      qpp_stats, qpp_mode, qpp_index);
+}
+
+int qf_fuse_qpp_micro(int64_t n_queries, int32_t n_retrievers, const int64_t* list_off,
+                      const uint32_t* docid, const void* score, int32_t score_kind,
+                      const int32_t* rank, const double* qpp_raw, const double* qpp_stats,
+                      int32_t qpp_mode, int32_t qpp_index, int32_t methods, int32_t rrf_k,
+                      int32_t max_entries, uint32_t* union_docid, int32_t* union_count,
+                      uint16_t* perm, double* fused, int64_t out_stride, int64_t* qpp_micro_out,
+                      void* stream) {
+  if (methods & QF_PROBFUSE)
+    return fail(QF_EINVAL, "qf_fuse_qpp_micro: QF_PROBFUSE needs qf_fuse_probfuse (segment table)");
+  if (n_queries > 0 && (!qpp_raw || !qpp_micro_out))
+    return fail(QF_EINVAL, "qf_fuse_qpp_micro: null buffer");
+  if (n_retrievers > kMaxRLds)  // the workspace join of 17-32 runs writes none
+    return fail(QF_EINVAL, "qf_fuse_qpp_micro: at most %d runs", kMaxRLds);
+  return fuse_common(n_queries, n_retrievers, list_off, docid, score, score_kind, rank, nullptr,
+                     methods, rrf_k, nullptr, 0, 0, max_entries, union_docid, union_count, perm,
+                     0, fused, out_stride, stream, "qf_fuse_qpp_micro", 0u, nullptr, 0, qpp_raw,
+                     qpp_stats, qpp_mode, qpp_index, qpp_micro_out);
 }
 
 int64_t qf_fuse_workspace_bytes(int64_t n_queries, int32_t n_retrievers, int32_t max_entries,
@@ -535,6 +557,8 @@ int qf_synth_runs_nq(int64_t q_begin, int64_t n_queries, int32_t n_retrievers, i
     return fail(QF_EINVAL, "qf_synth_runs_nq: bad arguments (1 <= k <= 4096)");
   if (2 * (int64_t)k >= 2681468)
     return fail(QF_EINVAL, "qf_synth_runs_nq: k too large for the NQ id space");
+  if (seed > 0xFFFFFFFFull)  // Philox's key word: seeds differing above bit 31 would coincide
+    return fail(QF_EINVAL, "qf_synth_runs_nq: seed must fit 32 bits");
   return check(qf::synth_nq_launch(q_begin, n_queries, n_retrievers, k, seed, qrel_off, qrel_doc,
                                    n_qrel_queries, list_off, docid, score, (hipStream_t)stream),
                "qf_synth_runs_nq");

@@ -47,6 +47,9 @@ struct FuseParams {
   // the largest union learned fusion's bucket sort reaches in this call (0: kJsUMax);
   // the fallback pass takes a learned pair above it or marked below it
   int32_t learned_reach;
+  // qf_fuse_qpp_micro: the join also writes the .qpp "%.6f" micro-units of all 13
+  // normalised columns of its query's lists ([Q*R][13], qf_qpp_normalize's micro_out)
+  int64_t* qpp_micro;
 };
 // perm element i (m * out_stride + base + rank): every kernel writes perm through
 // these, so one flag switches a call between the uint16 and uint32 layouts

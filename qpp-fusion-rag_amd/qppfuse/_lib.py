@@ -50,6 +50,8 @@ SIGNATURES = {
                           _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_fuse_qpp": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32,
                               _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "qf_fuse_qpp_micro": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32,
+                                    _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "qf_fuse_probfuse": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _vp,
                                    _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "qf_fused_topk": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp,

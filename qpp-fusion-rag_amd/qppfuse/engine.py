@@ -114,7 +114,8 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
          out: Optional[FuseOut] = None, seg_prob: Optional[torch.Tensor] = None,
          n_segments: int = 0, seg_len: int = 0,
          learned_f32: Optional[int] = None,
-         workspace: Optional[torch.Tensor] = None, qpp=None) -> FuseOut:
+         workspace: Optional[torch.Tensor] = None, qpp=None,
+         qpp_micro_out: Optional[torch.Tensor] = None) -> FuseOut:
     """qf_fuse over every query of a packed run set (see include/qppfuse.h); with
     "probfuse" among the methods, qf_fuse_probfuse with the [R, x] segment table;
     methods == ["learned"] with learned_f32 (run bitmask: float32 model weights,
@@ -126,7 +127,9 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
     mode, qpp_index): the W-* weights from the raw QPP predictors and their column
     statistics, computed inside the fusion (qf_fuse_qpp — the weights qpp_normalize
     would give, one launch fewer); for the uint16-perm path without a workspace
-    (other calls normalise first and pass `weights`)."""
+    (other calls normalise first and pass `weights`).  `qpp_micro_out` (with `qpp`):
+    int64 [Q * R * 13] receiving the .qpp "%.6f" micro-units of all 13 columns
+    (qf_fuse_qpp_micro — qpp_normalize's "micro", written by the join)."""
     dev = require_device()
     R = int(n_retrievers)
     Q = (list_off.numel() - 1) // R
@@ -167,6 +170,8 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
                   _ptr(out.union_docid), _ptr(out.union_count), _ptr(out.perm), _ptr(out.fused),
                   out.fused.shape[1], _stream())
         return out
+    if qpp_micro_out is not None and qpp is None:
+        raise ValueError("qpp_micro_out needs qpp=(raw, stats, mode, qpp_index)")
     if qpp is not None:
         raw_qpp, stats, mode, qidx = qpp
         mode_id = {"none": _lib.NORM_NONE, "minmax": _lib.NORM_MINMAX,
@@ -176,6 +181,16 @@ def fuse(list_off: torch.Tensor, docid: torch.Tensor, score: torch.Tensor, n_ret
                              "/ learned fusion")
         if raw_qpp.dtype != torch.float64 or raw_qpp.numel() != Q * R * _lib.QPP_COLS:
             raise ValueError(f"qpp raw must be float64 [{Q * R}, {_lib.QPP_COLS}]")
+        if qpp_micro_out is not None:
+            if qpp_micro_out.dtype != torch.int64 or qpp_micro_out.numel() != Q * R * _lib.QPP_COLS \
+                    or not qpp_micro_out.is_contiguous():
+                raise ValueError(f"qpp_micro_out must be contiguous int64 [{Q * R * _lib.QPP_COLS}]")
+            _lib.call("qf_fuse_qpp_micro", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
+                      _ptr(rank), _ptr(raw_qpp), _ptr(stats), mode_id, int(qidx), mask,
+                      int(rrf_k), int(max_entries), _ptr(out.union_docid), _ptr(out.union_count),
+                      _ptr(out.perm), _ptr(out.fused), out.fused.shape[1], _ptr(qpp_micro_out),
+                      _stream())
+            return out
         _lib.call("qf_fuse_qpp", Q, R, _ptr(list_off), _ptr(docid), _ptr(score), kind,
                   _ptr(rank), _ptr(raw_qpp), _ptr(stats), mode_id, int(qidx), mask, int(rrf_k),
                   int(max_entries), _ptr(out.union_docid), _ptr(out.union_count),
@@ -350,14 +365,32 @@ def synth_runs_nq(q_begin: int, n_queries: int, n_retrievers: int, k: int, qrel_
     score = torch.empty(max(E, 1), dtype=torch.float64, device=dev)
     qo = qd = None
     nq = 0
+    if not 0 <= int(seed) < 2**32:  # Philox is keyed by a 32-bit seed (include/qppfuse.h)
+        raise ValueError(f"synth_runs_nq: seed {seed} outside [0, 2**32)")
     if qrel_off is not None:
-        to = lambda a, dt: (a if isinstance(a, torch.Tensor) else
-                            torch.from_numpy(np.ascontiguousarray(a).view(dt))).to(dev)
-        qo = to(qrel_off, np.int64)
-        qd = to(qrel_doc, np.int32)
+        # converted by value (an int64 docid array must not be reinterpreted as twice as
+        # many int32 words); corpus ids are uint32, carried as int32 bits on device
+        if isinstance(qrel_off, torch.Tensor):
+            qo = qrel_off.to(device=dev, dtype=torch.int64)
+        else:
+            qo = torch.from_numpy(np.ascontiguousarray(qrel_off, dtype=np.int64)).to(dev)
+        if isinstance(qrel_doc, torch.Tensor):
+            qd = qrel_doc.to(device=dev)
+            if qd.dtype != torch.int32:  # (int32: already the uint32 bits)
+                qd = qd.to(torch.int64)
+                if qd.numel() and (int(qd.min()) < 0 or int(qd.max()) >= 2**32):
+                    raise ValueError("synth_runs_nq: qrel docids must fit uint32")
+                qd = torch.where(qd >= 2**31, qd - 2**32, qd).to(torch.int32)
+        else:
+            d = np.asarray(qrel_doc)
+            if d.size and (d.min() < 0 or d.max() >= 2**32):
+                raise ValueError("synth_runs_nq: qrel docids must fit uint32")
+            qd = torch.from_numpy(np.ascontiguousarray(d.astype(np.uint32)).view(np.int32)).to(dev)
         nq = qo.numel() - 1
+        if int(qo[-1]) > qd.numel():
+            raise ValueError("synth_runs_nq: qrel_off ends past qrel_doc")
     _lib.call("qf_synth_runs_nq", int(q_begin), int(n_queries), int(n_retrievers), int(k),
-              int(seed) & (2**64 - 1), _ptr(qo), _ptr(qd), nq, _ptr(list_off), _ptr(docid),
+              int(seed), _ptr(qo), _ptr(qd), nq, _ptr(list_off), _ptr(docid),
               _ptr(score), _stream())
     return list_off, docid[:E], score[:E]
 

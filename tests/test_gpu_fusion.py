@@ -875,14 +875,17 @@ def test_join_leaves_the_sort_key_constants(gpu, methods):
     key constants at fused[slot][base + U .. + 4) when the query has 4 spare slots:
     [min, max, c, top | cform << 31 | scale << 32] — exactly the values' extremes (-0.0
     folded) and bs_key2's constants; a run-time method set (no compile-time slots)
-    leaves w3 = 0 (the sort computes them).  The fused outputs are checked elsewhere."""
+    leaves w3 = 0 (the sort computes them).  The fused outputs are checked elsewhere.
+    Round 6: that is the join_kernel + bsort_fast_kernel path of max_entries above
+    5,120 (here 7,680: JoinL); join_sort_kernel (max_entries <= 5,120) keeps the same
+    constants in LDS for its own sorts."""
     from qppfuse import engine
     Q, R, K = 48, 5, 1000
     off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=5)
     rng = np.random.default_rng(3)
     w = torch.from_numpy(rng.random(Q * R).round(6)).to(gpu)
     w[:R] = 0.0  # query 0: zero weights, outside the sums' division-free fast path
-    out = engine.fuse(off, docid, micro, R, methods, rrf_k=60, weights=w, max_entries=R * K)
+    out = engine.fuse(off, docid, micro, R, methods, rrf_k=60, weights=w, max_entries=7680)
     torch.cuda.synchronize()
     off_h = off.cpu().numpy()
     uc = out.union_count.cpu().numpy()
