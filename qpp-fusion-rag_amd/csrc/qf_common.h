@@ -17,6 +17,12 @@
   do {                            \
   } while (0)
 #endif
+// Development timing probe (qf_dev_hooks.h, -DQF_CF_SCATTER): the bucket sort's scatter
+// position; a probe build stores each item at its own index instead (conflict-free
+// LDS addresses, wrong results) to price the scatter's bank conflicts.
+#ifndef QF_DEV_SCATTER_POS
+#define QF_DEV_SCATTER_POS(pos, lin) (pos)
+#endif
 
 namespace qf {
 

@@ -1154,16 +1154,13 @@ __device__ __forceinline__ double swap_min_f64(double a, double b) {
 // each row (row r then holds values 3r .. 3r + 2), one lane per row stores them, and
 // wave 0 reduces the waves' results — no LDS transposition (round 5's first form,
 // whose transposed reads hit one bank per lane quad: join +48 us).
-// TOLDS (join_sort_kernel): the constants of slot s into kout[s] (2^13-bucket keys
-// whatever U), not global memory; the caller passes ranged, M <= kRangeSlots.
-template <class C, int KIND, int EXTRA, bool TOLDS = false>
+template <class C, int KIND, int EXTRA>
 __device__ __forceinline__ void pair_info(const FuseParams& p, JoinShared<C, KIND, EXTRA>& sh,
-                                          int N, bool ranged, const SlotRange& rg,
-                                          double (*kout)[4] = nullptr) {
+                                          int N, bool ranged, const SlotRange& rg) {
   constexpr int WAVES = C::kWaves, NV = 2 * kRangeSlots;
   static_assert(NV == 12, "three values per 16-lane row after the two exchanges");
   const int U = sh.U;
-  if (sh.status || (!TOLDS && N - U < kPairInfo)) return;  // uniform
+  if (sh.status || N - U < kPairInfo) return;  // uniform
   const int M = __popc(p.methods);
   const int64_t at = sh.off[0] + U;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1202,16 +1199,8 @@ __device__ __forceinline__ void pair_info(const FuseParams& p, JoinShared<C, KIN
     if ((lane & 3) == 0 && (lane >> 2) < M) {
       const int s = lane >> 2;
       const double smin = x + 0.0, smax = -nmax + 0.0;  // -0.0 folded into +0.0
-      const BsKey2 k = (!TOLDS && U <= 3072)
-                           ? bs_key2<kFastMinBase>(smin, smax, false, kFastDeltaShift)
-                           : bs_key2<kFastMinBaseL>(smin, smax, false, kFastDeltaShift);
-      if constexpr (TOLDS) {
-        kout[s][0] = smin;
-        kout[s][1] = smax;
-        kout[s][2] = k.c;
-        kout[s][3] = __longlong_as_double((int64_t)bs_key2_word(k));
-        return;
-      }
+      const BsKey2 k = U <= 3072 ? bs_key2<kFastMinBase>(smin, smax, false, kFastDeltaShift)
+                                 : bs_key2<kFastMinBaseL>(smin, smax, false, kFastDeltaShift);
       double* o = p.fused + s * p.out_stride + at;
       o[0] = smin;
       o[1] = smax;
@@ -1448,7 +1437,7 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void fuse_large_kernel(Fus
       // it (learned fusion's docid-tie sort reaches p.learned_reach, the others kFastUMaxL)
       const int reach = slot_method(p.methods, (int)(idx % M)) == 6
                             ? (p.learned_reach ? p.learned_reach : kJsUMax)
-                            : kFastUMaxL;
+                            : (p.fast_reach ? p.fast_reach : kJsUMax);
       if (FB && U > 1 && U <= reach)
         take = perm_get(p, (idx % M) * p.out_stride + p.list_off[q * p.R]) == kJsUnsorted;
       if (take) s_list[atomicAdd(&s_n, 1)] = (int)(idx - c0);
@@ -2049,320 +2038,6 @@ __device__ __forceinline__ void lds_store_b128(void* at, uint32_t a, uint32_t b,
   asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 
-// The bucket sort of one (query, method slot) pair whose scores are in registers:
-// item j of this lane is u = ub0 + j * ustep + lane (chunked: ub0 = wid * rows * 64,
-// ustep = 64 — bsort_fast_kernel; STRIDED: ub0 = wid * 64, ustep = BLOCK — the join's
-// own document mapping, join_sort_kernel), v[j] its score (0.0 past U: masked).
-// Positions of the rank phase take the same mapping.  consts(smin, smax, kc, w3)
-// gives the key constants (w3 = 0: none, computed here from v) and is called while
-// the counters are zeroed.  Writes perm[po + i] (or marks perm[po] for the fallback
-// pass).  Every thread of the block calls it, with block-uniform U / po; lds and sm
-// are its own until it returns (the caller's barrier before reusing them).
-// after_scatter() runs once v is dead (its last use, the scatter): join_sort_kernel
-// loads the next slot's scores into v there, so their latency hides behind this
-// slot's rank phase.
-template <int BLOCK, int UMAX, int BITS, bool S32, bool STRIDED, class Consts, class Next>
-__device__ __forceinline__ void bsort_fast_body(const FuseParams& p, unsigned char* lds,
-                                                BsFastShared<BLOCK / 64>& sm,
-                                                double (&v)[UMAX / BLOCK], int U,
-                                                int64_t po, Consts consts, Next after_scatter) {
-  constexpr int WAVES = BLOCK / 64, ROWS = UMAX / BLOCK, NB = 1 << BITS;
-  constexpr int MINSUB = NB / 16, MINBASE = NB - MINSUB;
-  static_assert(ROWS * BLOCK == UMAX && UMAX <= 65535, "rows of a wave");
-  static_assert(((UMAX - 1) >> 6) < MINSUB, "minimum sub-bucket shift <= 6");
-  static_assert(NB % (4 * BLOCK) == 0, "whole uint4 counter loads per thread");
-  using LD = BsFastLds<UMAX, BITS, S32>;
-  uint64_t* skey = (uint64_t*)lds;               // region A from the scatter on
-  uint32_t* cnt = (uint32_t*)lds;                // region A until the scan
-  uint32_t* sw = (uint32_t*)(lds + LD::kA);      // region B from the second scatter on
-  uint16_t* bk = (uint16_t*)(lds + LD::kA);      // region B until then (u16 starts)
-  uint32_t* bk32 = (uint32_t*)(lds + LD::kA);    // (S32: u32 starts)
-  const int tid = threadIdx.x, lane = tid & 63,
-            wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rows = (U + BLOCK - 1) / BLOCK;
-  // this lane's item / position j: ub0 + j * ustep + lane
-  const int ub0 = STRIDED ? wid * 64 : wid * rows * 64;
-  constexpr int ustep = STRIDED ? BLOCK : 64;
-
-  // the counters zeroed while the caller's loads are in flight
-  for (int i = tid; i < (NB + kFastSpare) / 4; i += BLOCK)
-    ((uint4*)cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (tid == 0) {
-    sm.big = 0u;
-    sm.nan = 0u;
-  }
-  // ---- the key constants: the join's, else computed here ------------------------------
-  double smin = 0.0, smax = 0.0, kc = 0.0;
-  uint64_t w3 = 0ull;
-  consts(smin, smax, kc, w3);
-  __syncthreads();  // the counters and flags are zero
-  if (w3 == 0ull) {  // uniform: the range of the valid items, reduced over the block
-    double vmn = INFINITY, vmx = -INFINITY;
-    bool nan = false;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = ub0 + j * ustep + lane;
-      if (j < rows && u < U) {
-        vmn = raw_min_f64(vmn, v[j]);
-        vmx = raw_max_f64(vmx, v[j]);
-        nan |= v[j] != v[j];
-      }
-    }
-    vmn = wave_min_f64_dpp(vmn);
-    vmx = wave_max_f64_dpp(vmx);
-    if (ballot(nan) != 0ull && lane == 0) sm.nan = 1u;
-    if (lane == 63) {
-      sm.mn[wid] = vmn;
-      sm.mx[wid] = vmx;
-    }
-    __syncthreads();
-    double a = sm.mn[0], b = sm.mx[0];
-#pragma unroll
-    for (int w = 1; w < WAVES; ++w) {
-      a = raw_min_f64(a, sm.mn[w]);
-      b = raw_max_f64(b, sm.mx[w]);
-    }
-    smin = rfl_f64(a + 0.0);
-    smax = rfl_f64(b + 0.0);
-    const bool anynan = sm.nan != 0u;
-    if (anynan) smin = smax = __longlong_as_double(0x7FF8000000000000ll);  // never "all equal"
-    const BsKey2 k = bs_key2<MINBASE>(smin, smax, anynan, kFastDeltaShift);
-    kc = rfl_f64(k.c);
-    const uint64_t w = bs_key2_word(k);
-    w3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 32)) << 32) |
-         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w);
-  }
-  if (smin == smax) {  // every score equal: first-seen order
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = ub0 + j * ustep + lane;
-      if (j < rows && u < U) perm_put(p, po + u, (uint32_t)u);
-    }
-    return;
-  }
-  if (w3 == kPairMark) {  // a range the key cannot take: the fallback pass
-    if (tid == 0) perm_put(p, po, kJsUnsorted);
-    return;
-  }
-  QF_STOP(21, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += (uint32_t)__double2loint(v[j]); return a; },
-          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
-
-  // ---- count --------------------------------------------------------------------------
-  int ush = 0;  // (U - 1) >> ush < MINSUB: the minimum's sub-bucket is MINBASE + (u >> ush)
-  while (((uint32_t)(U - 1) >> ush) >= (uint32_t)MINSUB) ++ush;
-  const uint32_t lane_sub = (uint32_t)lane >> ush;  // (64-aligned row bases: exact split)
-  const uint32_t spare = (uint32_t)NB + ((uint32_t)lane & (kFastSpare - 1u));
-  uint32_t ws[ROWS];  // bucket | arrival << 16
-  uint32_t omax = 0u;
-  auto count_rows = [&](auto cf, double c, uint32_t top, uint32_t scale) __attribute__((always_inline)) {
-    constexpr bool CF = decltype(cf)::value;
-    uint32_t old[ROWS];
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      if (j < rows) {  // uniform; every row's atomic issued before any result is used
-        const int u = ub0 + j * ustep + lane;
-        const double x = CF ? v[j] + c : (v[j] - smin) + c;
-        const uint32_t hx = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
-        const uint32_t key = __umulhi(top - hx, scale);  // < MINBASE, 0 for the largest
-        const uint32_t minb = ((uint32_t)MINBASE + ((uint32_t)(ub0 + ustep * j) >> ush)) + lane_sub;
-        uint32_t b = sel_if_eq_f64(v[j], smin, minb, key);
-        b = u < U ? b : spare;
-        ws[j] = b;
-        old[j] = atomicAdd(&cnt[b], 1u);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      if (j < rows) {
-        omax = max(omax, old[j]);
-        ws[j] |= old[j] << 16;
-      }
-    }
-  };
-  auto count = [&](double c, uint64_t w) __attribute__((always_inline)) {
-    const uint32_t top = (uint32_t)w & 0x7FFFFFFFu, scale = (uint32_t)(w >> 32);
-    if ((w >> 31) & 1u) count_rows(std::true_type{}, c, top, scale);
-    else count_rows(std::false_type{}, c, top, scale);
-    if (omax >= (uint32_t)kJsBucketMax) sm.big = 1u;  // (benign race: every writer stores 1)
-  };
-  count(kc, w3);
-  __syncthreads();  // the counters are complete
-  if (sm.big) {  // uniform, rare: recount with delta = range / 2^20
-    __syncthreads();  // every thread has read the flag
-    for (int i = tid; i < (NB + kFastSpare) / 4; i += BLOCK)
-      ((uint4*)cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid == 0) sm.big = 0u;
-    const BsKey2 k = bs_key2<MINBASE>(smin, smax, false, kFastRetryShift);
-    __syncthreads();
-    if (!k.ok) {  // uniform
-      if (tid == 0) perm_put(p, po, kJsUnsorted);
-      return;
-    }
-    omax = 0u;
-    const uint64_t w = bs_key2_word(k);
-    count(rfl_f64(k.c), ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 32)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w));
-    __syncthreads();
-    if (sm.big) {  // uniform: still a bucket above kJsBucketMax — the fallback pass
-      if (tid == 0) perm_put(p, po, kJsUnsorted);
-      return;
-    }
-  }
-  QF_STOP(22, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += ws[j]; return a; },
-          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
-
-  // ---- exclusive scan of the counters -> u16 bucket starts (region B) ------------------
-  {
-    constexpr int kPer = NB / BLOCK;  // 8 (512 threads) or 4 (1,024)
-    uint32_t c[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer / 4; ++i) {
-      const uint4 x = ((const uint4*)cnt)[tid * (kPer / 4) + i];
-      c[4 * i] = x.x; c[4 * i + 1] = x.y; c[4 * i + 2] = x.z; c[4 * i + 3] = x.w;
-    }
-    uint32_t tot = 0u;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const uint32_t x = c[i];
-      c[i] = tot;
-      tot += x;
-    }
-    const uint32_t incl = wave_incl_scan_dpp(tot);
-    if (lane == 63) sm.wtot[wid] = incl;
-    __syncthreads();  // also: every counter read before the scatter overwrites them
-    // the waves before this one: lane w reads wave w's total (one LDS read, not a
-    // serial loop of up to 15 dependent ones), a DPP scan, the lane wid - 1 of it
-    uint32_t pre = incl - tot;
-    const uint32_t wt = wave_incl_scan_dpp(lane < WAVES ? sm.wtot[lane] : 0u);
-    if (wid > 0) pre += readlane_u32(wt, wid - 1);
-    if constexpr (S32) {
-#pragma unroll
-      for (int i = 0; i < kPer / 4; ++i)
-        lds_store_b128(&bk32[(tid * (kPer / 4) + i) * 4], pre + c[4 * i], pre + c[4 * i + 1],
-                       pre + c[4 * i + 2], pre + c[4 * i + 3]);
-      if (tid == 0) bk32[NB] = (uint32_t)U;
-    } else {
-      const uint32_t pre2 = pre * 0x10001u;  // (starts <= U < 2^16: no carry between halves)
-      uint32_t pk[kPer / 2];
-#pragma unroll
-      for (int i = 0; i < kPer / 2; ++i) pk[i] = (c[2 * i] | (c[2 * i + 1] << 16)) + pre2;
-      if constexpr (kPer >= 8) {
-#pragma unroll
-        for (int i = 0; i < kPer / 8; ++i)
-          lds_store_b128(&bk[(tid * (kPer / 8) + i) * 8], pk[4 * i], pk[4 * i + 1], pk[4 * i + 2],
-                         pk[4 * i + 3]);
-      } else {
-        ((uint2*)bk)[tid] = make_uint2(pk[0], pk[1]);
-      }
-      if (tid == 0) bk[NB] = (uint16_t)U;
-    }
-  }
-  __syncthreads();
-  QF_STOP(23, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += ws[j] + bk[j]; return a; },
-          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
-
-  // ---- scatter: keys by position, then the words over the dead starts ---------------
-  uint32_t pa[ROWS], pw[ROWS];  // position; u << 16 | size << 8 | arrival
-  const uint32_t ul = (uint32_t)(ub0 + lane) << 16;
-  auto scatter = [&](auto nn) __attribute__((always_inline)) {
-    constexpr bool NN = decltype(nn)::value;
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int u = ub0 + j * ustep + lane;
-      if (j < rows && u < U) {
-        const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
-        const uint32_t st = S32 ? bk32[b] : bk[b], nx = S32 ? bk32[b + 1] : bk[b + 1];
-        const uint32_t pos = st + at;
-        // the rank phase compares integer keys: without negative scores (every C2
-        // fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
-        skey[pos] = NN ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);
-        pa[j] = pos;
-        pw[j] = (ul + ((uint32_t)(ustep * j) << 16)) | ((nx - st) << 8) | at;
-      }
-    }
-  };
-  if (smin >= 0.0) scatter(std::true_type{});  // uniform
-  else scatter(std::false_type{});
-  after_scatter();
-  __syncthreads();  // the starts are dead
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int u = ub0 + j * ustep + lane;
-    if (j < rows && u < U) sw[pa[j]] = pw[j];
-  }
-  // a sentinel at position U (key 0 = the smallest, tie word ~0 = the largest: it
-  // never precedes anything), so the rank loop may read one member past a bucket's
-  // end — a later bucket's member never precedes either (later buckets hold strictly
-  // smaller scores; the minimum's sub-buckets equal scores with larger u)
-  if (tid == 0) {
-    skey[U] = 0ull;
-    sw[U] = 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  QF_STOP(24, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += pa[j] + sw[j]; return a; },
-          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
-
-  // ---- rank inside the bucket, in position order --------------------------------------
-  // LDS byte offsets: keys at 8 * position, words at kA + 4 * position; this lane's
-  // row j reads position ub0 + lane + ustep * j (the row part an instruction offset)
-  uint32_t P[ROWS], uo[ROWS];
-  const unsigned char* kme = lds + 8 * (ub0 + lane);
-  const unsigned char* wme = lds + LD::kA + 4 * (ub0 + lane);
-#pragma unroll
-  for (int j = 0; j < ROWS; ++j) {
-    const int i = ub0 + j * ustep + lane;
-    P[j] = 0u;
-    uo[j] = 0u;
-    if (j < rows && i < U) {
-      const uint64_t ki = *(const uint64_t*)(kme + 8 * ustep * j);
-      const uint32_t wi = *(const uint32_t*)(wme + 4 * ustep * j);  // also the tie-break key:
-      // u in the top bits (distinct), so the word order is the first-seen order
-      const uint32_t lo = (uint32_t)i - (wi & 0xFFu);
-      uint32_t ka = lo * 8u;  // the bucket's first key
-      asm volatile("" : "+v"(ka));  // (kept, not re-derived from i in the loop's preheader)
-      const uint32_t kend = ka + __builtin_amdgcn_ubfe(wi, 8u, 8u) * 8u;  // one past its last
-      uint32_t ta = LD::kA + lo * 4u;  // the first word
-      uint32_t before = 0u;
-      // every member, itself included (it never precedes itself), two per step; an odd
-      // bucket's last step reads the member after it, which never precedes (sentinel)
-      do {  // (a bucket holds this position: at least one step)
-        // two ds_read_b64 (2 LDS cycles each) rather than a ds_read2_b64 (8 cycles)
-        const uint64_t v0 = *(const uint64_t*)(lds + ka);
-        asm volatile("" ::: "memory");
-        const uint64_t v1 = *(const uint64_t*)(lds + ka + 8);
-        const uint32_t t0 = *(const uint32_t*)(lds + ta), t1 = *(const uint32_t*)(lds + ta + 4);
-        before = add_if_precedes(before, ki, wi, v0, t0);
-        before = add_if_precedes(before, ki, wi, v1, t1);
-        ka += 16u;
-        ta += 8u;
-      } while (ka < kend);
-      P[j] = lo + before;
-      uo[j] = wi >> 16;
-    }
-  }
-  QF_STOP(25, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += P[j] + uo[j]; return a; },
-          if (_qf_acc == 12345u) perm_put(p, po, 0u); return;);
-  // ---- perm (every row's position before any store) ------------------------------------
-  if (p.perm32) {  // uniform
-    const auto pr = __builtin_amdgcn_make_buffer_rsrc((uint32_t*)p.perm + po, (short)0, U * 4,
-                                                      0x00020000);
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int i = ub0 + j * ustep + lane;
-      if (j < rows && i < U) __builtin_amdgcn_raw_buffer_store_b32(uo[j], pr, P[j] * 4, 0, kBufNT);
-    }
-  } else {
-    const auto pr = __builtin_amdgcn_make_buffer_rsrc((uint16_t*)p.perm + po, (short)0, U * 2,
-                                                      0x00020000);
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) {
-      const int i = ub0 + j * ustep + lane;
-      if (j < rows && i < U)
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)uo[j], pr, P[j] * 2, 0, kBufNT);
-    }
-  }
-}
-
 // UMIN < U <= UMAX of the pairs this configuration sorts; BITS: 2^BITS buckets (the
 // last 1/16 the minimum's sub-buckets); S32: u32 bucket starts.
 template <int BLOCK, int UMIN, int UMAX, int BITS, bool S32, int MINW>
@@ -2613,7 +2288,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
       if (j < rows && u < U) {
         const uint32_t b = ws[j] & 0xFFFFu, at = ws[j] >> 16;
         const uint32_t st = S32 ? bk32[b] : bk[b], nx = S32 ? bk32[b + 1] : bk[b + 1];
-        const uint32_t pos = st + at;
+        const uint32_t pos = QF_DEV_SCATTER_POS(st + at, (uint32_t)u);
         // the rank phase compares integer keys: without negative scores (every C2
         // fusion) the f64 bits of v + 0.0 (-0.0 folded) already ascend
         skey[pos] = NN ? (uint64_t)__double_as_longlong(v[j] + 0.0) : bs_rank_key(v[j]);
@@ -2700,93 +2375,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void bsort_fast_kernel(FuseParams p) {
       if (j < rows && i < U)
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)uo[j], pr, P[j] * 2, 0, kBufNT);
     }
-  }
-}
-
-// ============================================================================
-// join_sort_kernel (round 6) — the default path for queries of up to 5,120 entries
-// (SURVEY §8(d)'s C2: 5 x top-1,000, unions of 3,856-4,148): the join and every
-// non-learned slot's bucket sort in ONE workgroup of 1,024 threads per query.
-// join_kernel + bsort_fast_kernel wrote the 667 MB of unsorted fused scores of a C2
-// launch and read them straight back from HBM (PMC traffic 1.69x the algorithmic
-// bytes, the sort's load phase 112 of its 295 us), and launched a workgroup per
-// (query, slot) of each sort configuration whatever the unions were (the empty one:
-// 20 us).  Here the thread that stores document u's sums (u = tid + j * 1,024, the
-// sums loop's mapping) reads slot ms's score back for the sort (an L2 hit of its own
-// store) — bsort_fast_body with the same strided mapping, 2^13 buckets, the key
-// constants from the sums loop's ranges (pair_info into LDS) — so the scores cross
-// HBM once, and one launch covers every union size (no empty dispatch).  LDS: the
-// sort's 73.8 KB over the join's dead tables (51 / 70 KB), two workgroups per CU —
-// the separate sort's occupancy (32 waves per CU); the join's phases (HBM-bound)
-// overlap the other workgroup's sorts (VALU-bound).
-// (Round 4 measured every method's sort in the join's 512-thread workgroup at three
-// per CU on the legacy data and older sorts: 349 vs 330 us — 24 waves per CU for
-// the sorts against the sort kernel's 32.)
-// A pair the bucket sort cannot order is marked (perm[0] = kJsUnsorted) for the
-// fallback pass; learned fusion's docid-tie slot is left to bsort_kernel<BYDOC>.
-// ============================================================================
-using JoinJS = JoinCfg<1024, 5, 13, 8>;  // N <= 5,120
-using JsSortLds = BsFastLds<kFastUMaxL, kFastBitsL, true>;
-template <class C, int KIND>
-__global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_sort_kernel(FuseParams p) {
-  constexpr int BLOCK = C::kBlock, ROWS = kFastUMaxL / BLOCK, EXTRA = JsSortLds::kBytes;
-  static_assert(C::kNMax == kFastUMaxL, "every union of the join within the sort's reach");
-  __shared__ JoinShared<C, KIND, EXTRA> sh;
-  __shared__ BsFastShared<BLOCK / 64> sm;
-  __shared__ double kinfo[kRangeSlots][4];
-  const int64_t q = block_id();
-  if (q >= p.n_queries) return;
-  const int N = join_groups<C, KIND, EXTRA>(p, sh, q);
-  if (N < 0) return;
-  SlotRange rg;
-  rg.init();
-  const bool ranged = store_unsorted_sums<C, KIND, EXTRA>(p, sh, N, rg);
-  const int U = sh.U, M = __popc(p.methods);
-  if (threadIdx.x == 0) p.union_count[q] = sh.status ? sh.status : U;
-  if (sh.status || U < 1) return;  // uniform
-  const bool have_k = ranged && M <= kRangeSlots;
-  if (have_k) pair_info<C, KIND, EXTRA, true>(p, sh, N, true, rg, kinfo);
-  QF_STOP(30, [&] { return 0u; }, return;);  // (development: the join's share)
-  const int lslot = (p.methods & QF_LEARNED) ? __popc(p.methods & (QF_LEARNED - 1)) : -1;
-  const int64_t base = sh.off[0];
-  const int tid = threadIdx.x;
-  const int rows = (U + BLOCK - 1) / BLOCK;
-  double v[ROWS];
-  // slot ms's scores: this thread's own stores (u = tid + j * BLOCK; 0.0 past U)
-  auto load = [&](int ms) __attribute__((always_inline)) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.fused + (int64_t)ms * p.out_stride + base), (short)0, U * 8, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j)
-      if (j < rows)  // uniform
-        v[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, j * BLOCK * 8, 0));
-  };
-  bool have = false;  // v holds slot ms's scores already (block-uniform)
-  for (int ms = lslot == 0 ? 1 : 0; ms < M;) {
-    const int next = ms + 1 == lslot ? ms + 2 : ms + 1;
-    if (!have) load(ms);
-    have = false;
-    const int64_t po = (int64_t)ms * p.out_stride + base;
-    __syncthreads();  // the previous slot's (or the join's) LDS is dead
-    bsort_fast_body<BLOCK, kFastUMaxL, kFastBitsL, true, true>(
-        p, sh.smem, sm, v, U, po,
-        [&](double& smin, double& smax, double& kc, uint64_t& w3) __attribute__((always_inline)) {
-          if (have_k) {  // uniform
-            smin = rfl_f64(kinfo[ms][0]);
-            smax = rfl_f64(kinfo[ms][1]);
-            kc = rfl_f64(kinfo[ms][2]);
-            const uint64_t w = __double_as_longlong(kinfo[ms][3]);
-            w3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(w >> 32)) << 32) |
-                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w);
-          }
-        },
-        [&]() __attribute__((always_inline)) {
-          if (next < M) {  // the next slot's loads in flight during this slot's rank phase
-            load(next);
-            have = true;
-          }
-        });
-    ms = next;
   }
 }
 
@@ -3743,41 +3331,32 @@ hipError_t fuse_launch(const FuseParams& p0, int kind, int max_entries, hipStrea
     // ranked by bsort_core in the join's dead LDS: 349-352 us against join 126 +
     // bsort 202-204 us; the six sorts in turn at 3 workgroups per CU lose more than
     // the HBM re-read they save.)
-    // development knobs (A/B on one library; read once): QF_DEV_JOIN_SORT=1 takes
-    // join_sort_kernel, QF_DEV_CHUNK_Q=n runs join + sorts over chunks of n queries
-    static const int dev_join_sort = getenv("QF_DEV_JOIN_SORT") ? atoi(getenv("QF_DEV_JOIN_SORT")) : 0;
-    static const int dev_chunk = getenv("QF_DEV_CHUNK_Q") ? atoi(getenv("QF_DEV_CHUNK_Q")) : 0;
-    const bool join_sort = dev_join_sort && !learned_only && max_entries <= JoinJS::kNMax;
-    const int64_t chunk = dev_chunk > 0 ? dev_chunk : p.n_queries;
-    for (int64_t q0 = 0; q0 < p.n_queries; q0 += chunk) {
-      FuseParams c = p;
-      c.n_queries = p.n_queries - q0 < chunk ? p.n_queries - q0 : chunk;
-      c.list_off = p.list_off + q0 * p.R;  // entry offsets stay absolute
-      c.union_count = p.union_count + q0;
-      if (p.weights) c.weights = p.weights + q0 * p.R;
-      if (p.qpp_raw) c.qpp_raw = p.qpp_raw + q0 * p.R * kQppCols;
-      if (p.qpp_micro) c.qpp_micro = p.qpp_micro + q0 * p.R * kQppCols;
-      if (learned_only) {  // join + sort in one kernel (C5)
-        hipLaunchKernelGGL((join_learned_kernel<JoinML>), grid_for(c.n_queries), dim3(512), 0, st,
-                           c);
-      } else if (join_sort) {  // join + every non-learned slot's sort (every union <= 5,120)
-        if (kind == 1)
-          hipLaunchKernelGGL((join_sort_kernel<JoinJS, 1>), grid_for(c.n_queries), dim3(1024), 0, st, c);
-        else
-          hipLaunchKernelGGL((join_sort_kernel<JoinJS, 0>), grid_for(c.n_queries), dim3(1024), 0, st, c);
-      } else {
-        if (max_entries <= JoinM::kNMax) launch_join<JoinM>(c, kind, st);
-        else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(c, kind, st);
-        else launch_join<JoinXL>(c, kind, st);
-      }
-      if ((c.methods & ~QF_LEARNED) && !join_sort) {
-        const dim3 grid = grid_for((c.n_queries + 7) / 8 * 8 * __builtin_popcount((unsigned)c.methods));
-        hipLaunchKernelGGL((bsort_fast_kernel<512, 0, kJsUMax, kFastBits, false, 8>), grid,
-                           dim3(512), 0, st, c);
-        if (max_entries > kJsUMax)  // unions above 3,072 (SURVEY §8(d)'s C2: 3,856-4,148)
-          hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, kFastBitsL, true, 8>),
-                             grid, dim3(1024), 0, st, c);
-      }
+    // (Measured, not kept, round 6 — profiles/r06_ab_join_sort_and_chunks.txt: the join
+    // and every slot's sort in one 1,024-thread workgroup per query, each slot re-read
+    // by the thread that stored it, 500-561 us against this pair's 485-503; and
+    // Infinity-Cache-sized query chunks, join(chunk) then its sorts, 549-666 against
+    // 499-503 — the sort is VALU / LDS-bound, so MALL-resident reads do not speed it,
+    // and every chunk adds a join tail.)
+    // the sorts' reach: 5,120 with the 1,024-thread configuration launched, else
+    // 3,072 — a query above max_entries that the LDS join still holds (JoinM takes N <=
+    // 5,120 whatever max_entries says) is then the fallback pass's (it
+    // was left unsorted)
+    p.fast_reach = max_entries > kJsUMax ? kFastUMaxL : kJsUMax;
+    if (learned_only) {  // join + sort in one kernel (C5)
+      hipLaunchKernelGGL((join_learned_kernel<JoinML>), grid_for(p.n_queries), dim3(512), 0, st,
+                         p);
+    } else {
+      if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
+      else if (max_entries <= JoinL::kNMax) launch_join<JoinL>(p, kind, st);
+      else launch_join<JoinXL>(p, kind, st);
+    }
+    if (p.methods & ~QF_LEARNED) {
+      const dim3 grid = grid_for((p.n_queries + 7) / 8 * 8 * __builtin_popcount((unsigned)p.methods));
+      hipLaunchKernelGGL((bsort_fast_kernel<512, 0, kJsUMax, kFastBits, false, 8>), grid,
+                         dim3(512), 0, st, p);
+      if (max_entries > kJsUMax)  // unions above 3,072 (SURVEY §8(d)'s C2: 3,856-4,148)
+        hipLaunchKernelGGL((bsort_fast_kernel<1024, kJsUMax, kFastUMaxL, kFastBitsL, true, 8>),
+                           grid, dim3(1024), 0, st, p);
     }
     if ((p.methods & QF_LEARNED) && !learned_only)
       hipLaunchKernelGGL((bsort_kernel<512, 12, true>), grid_for((p.n_queries + 7) / 8 * 8),

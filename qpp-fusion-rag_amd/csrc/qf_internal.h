@@ -47,6 +47,10 @@ struct FuseParams {
   // the largest union learned fusion's bucket sort reaches in this call (0: kJsUMax);
   // the fallback pass takes a learned pair above it or marked below it
   int32_t learned_reach;
+  // the largest union the other slots' bucket sorts reach in this call (0: kJsUMax —
+  // the 1,024-thread configuration not launched); the fallback pass takes a pair
+  // above it, or marked below it
+  int32_t fast_reach;
   // qf_fuse_qpp_micro: the join also writes the .qpp "%.6f" micro-units of all 13
   // normalised columns of its query's lists ([Q*R][13], qf_qpp_normalize's micro_out)
   int64_t* qpp_micro;

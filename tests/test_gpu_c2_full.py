@@ -110,8 +110,8 @@ def test_c2_qpp_file_values(c2):
 
 
 def test_c2_large_query_path_identical(c2):
-    """max_entries 7,680: join_kernel<JoinL> + bsort_fast_kernel (the path of queries of
-    5,121-10,240 entries) gives the same outputs as join_sort_kernel."""
+    """max_entries 7,680: the 768-thread join (JoinL, the path of queries of 5,121-7,680
+    entries) with the same sorts gives the same outputs as the headline's JoinM."""
     from qppfuse import engine as e
     b = e.fuse(c2.off, c2.docid, c2.micro, R, METHODS, 60, max_entries=7680,
                qpp=(c2.qraw, c2.mm, "minmax", 5))

@@ -875,17 +875,14 @@ def test_join_leaves_the_sort_key_constants(gpu, methods):
     key constants at fused[slot][base + U .. + 4) when the query has 4 spare slots:
     [min, max, c, top | cform << 31 | scale << 32] — exactly the values' extremes (-0.0
     folded) and bs_key2's constants; a run-time method set (no compile-time slots)
-    leaves w3 = 0 (the sort computes them).  The fused outputs are checked elsewhere.
-    Round 6: that is the join_kernel + bsort_fast_kernel path of max_entries above
-    5,120 (here 7,680: JoinL); join_sort_kernel (max_entries <= 5,120) keeps the same
-    constants in LDS for its own sorts."""
+    leaves w3 = 0 (the sort computes them).  The fused outputs are checked elsewhere."""
     from qppfuse import engine
     Q, R, K = 48, 5, 1000
     off, docid, raw, norm, micro = _synthetic(Q, R, K, seed=5)
     rng = np.random.default_rng(3)
     w = torch.from_numpy(rng.random(Q * R).round(6)).to(gpu)
     w[:R] = 0.0  # query 0: zero weights, outside the sums' division-free fast path
-    out = engine.fuse(off, docid, micro, R, methods, rrf_k=60, weights=w, max_entries=7680)
+    out = engine.fuse(off, docid, micro, R, methods, rrf_k=60, weights=w, max_entries=R * K)
     torch.cuda.synchronize()
     off_h = off.cpu().numpy()
     uc = out.union_count.cpu().numpy()
@@ -914,3 +911,37 @@ def test_join_leaves_the_sort_key_constants(gpu, methods):
                 assert w3 == k[1], (q, m, hex(w3), hex(k[1]))
             checked += 1
     assert checked >= (Q - 1) * len(methods) if compile_time else True
+
+
+@pytest.mark.parametrize("max_entries", [2048, 3072])
+def test_understated_max_entries_still_sorted(gpu, max_entries):
+    """the LDS join holds queries of up to 5,120 entries whatever
+    max_entries says, so a caller whose max_entries (1,025-3,072) understates a query
+    gets a union above 3,072 that the 512-thread bucket sort leaves and the 1,024-thread
+    configuration (launched only for max_entries > 3,072) never sees.  The fallback
+    pass now takes any such pair (FuseParams.fast_reach): every query bit-exact vs the
+    C oracle, none left with an uninitialised perm."""
+    import bench
+    from qppfuse import engine
+    Q, R, K = 16, 5, 900  # N = 4,500 entries per query, unions ~3,600 (SURVEY 8(d) data)
+    qo, qd = bench.nq_qrels()
+    off, docid, raw = engine.synth_runs_nq(0, Q, R, K, qo, qd)
+    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+    w = torch.from_numpy(np.random.default_rng(5).random(Q * R).round(6)).to(gpu)
+    out = engine.fuse(off, docid, micro, R, ALL, rrf_k=60, weights=w, max_entries=max_entries)
+    torch.cuda.synchronize()
+    off_h = off.cpu().numpy()
+    doc_h = docid.cpu().numpy().view(np.uint32)
+    sc_h = micro.cpu().numpy().astype(np.float64) / 1e6
+    uc = out.union_count.cpu().numpy()
+    assert (uc > 3072).all(), uc
+    perm = _perm_np(out)
+    fused = out.ranked_fused().cpu().numpy()
+    for m, name in enumerate(ALL):
+        _, o_uc, o_perm, o_fused = coracle.fuse(off_h, doc_h, sc_h, R, name, 60,
+                                                weights=w.cpu().numpy())
+        assert np.array_equal(uc, o_uc), name
+        for q in range(Q):
+            b, n = off_h[q * R], uc[q]
+            assert np.array_equal(perm[m, b:b + n], o_perm[b:b + n]), (name, q)
+            assert fused[m, b:b + n].tobytes() == o_fused[b:b + n].tobytes(), (name, q)

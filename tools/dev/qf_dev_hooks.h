@@ -18,3 +18,12 @@
       __VA_ARGS__                            \
     }                                        \
   } while (0)
+
+// QF_CF_SCATTER: bsort_fast_kernel's scatter stores item u at position u (consecutive
+// lanes, consecutive LDS addresses: no bank conflicts) instead of its bucket position —
+// the same instruction stream, wrong results; timed at stop point 24 against the
+// library's scatter (round 4's conflict probe, re-run in round 6 on the 1,024-thread,
+// 2^13-bucket configuration).
+#ifdef QF_CF_SCATTER
+#define QF_DEV_SCATTER_POS(pos, lin) (lin)
+#endif
