@@ -221,21 +221,23 @@ class Pipeline:
         self.args, self.world, self.rank, self.dev = args, world, rank, dev
         R, K = args.retrievers, args.k
         wl = args.wl
+        self.plan = None
         if args.queries is not None:
             Q, self.q_begin = args.queries, rank * args.queries
-        elif wl["total"]:  # strong scaling: the workload's total split across ranks
-            from qppfuse.dist import shard_range
-            b, e = shard_range(wl["queries"], world, rank)
-            Q, self.q_begin = e - b, b
+        elif wl["total"]:  # strong scaling: the workload's total split across ranks,
+            # balanced by Σ entries; every rank derives the same plan from
+            # the run set's list offsets (the synthetic lists are K long each)
+            from qppfuse.dist import shard_by_entries
+            n = wl["queries"] * R
+            self.plan = shard_by_entries(np.arange(n + 1, dtype=np.int64) * K, R, world)
+            Q, self.q_begin = int(self.plan[rank + 1] - self.plan[rank]), int(self.plan[rank])
         else:
             Q, self.q_begin = wl["queries"], rank * wl["queries"]
         self.Q, self.R, self.K = Q, R, K
-        if args.queries is not None or not wl["total"]:
+        if self.plan is None:
             self.shard_sizes = [Q] * world
         else:
-            from qppfuse.dist import shard_range
-            self.shard_sizes = [e - b for b, e in (shard_range(wl["queries"], world, r)
-                                                   for r in range(world))]
+            self.shard_sizes = [int(x) for x in np.diff(self.plan)]
         self.methods = args.methods
         self.off, self.docid, self.raw = gen_runs(args, self.q_begin, Q, R, K)
         self.qids = None
@@ -277,10 +279,9 @@ class Pipeline:
 
     def shard_begin(self, r: int) -> int:
         """First global query of rank r's shard (as __init__ computes its own)."""
-        if self.args.queries is not None or not self.args.wl["total"]:
+        if self.plan is None:
             return r * self.shard_sizes[r]
-        from qppfuse.dist import shard_range
-        return shard_range(self.args.wl["queries"], self.world, r)[0]
+        return int(self.plan[r])
 
     def text_arrays(self, q_begin: int, Q: int):
         """numTerms / text-feature columns of the shard [q_begin, q_begin + Q)."""
@@ -951,6 +952,11 @@ def main():
                        "queries_per_gpu": p.Q, "retrievers": args.retrievers,
                        "k": args.k, "qpp_top_k": args.qpp_top_k, "methods": p.methods,
                        "parallelism": f"query-sharded x{world}", "mean_union": round(mean_u, 1),
+                       "sharding": ("contiguous query ranges balanced by the entry count "
+                                    "(qppfuse.dist.shard_by_entries over the run set's list "
+                                    "offsets): shard sizes " + str(p.shard_sizes)
+                                    if p.plan is not None else
+                                    f"weak scaling: {p.Q} queries per rank, rank r at r x {p.Q}"),
                        "generator": args.generator,
                        "gather_topk_to_rank0": args.gather_topk,
                        "qids": (None if p.qids is None else

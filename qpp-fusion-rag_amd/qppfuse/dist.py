@@ -28,11 +28,17 @@ def shard_range(n_queries: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def shard_by_entries(list_off: np.ndarray, n_retrievers: int, world: int) -> np.ndarray:
-    """Query boundaries [world+1] balancing Σ entries (ragged lists) across ranks."""
-    qoff = np.asarray(list_off)[:: n_retrievers]
+    """Query boundaries [world+1] balancing Σ entries (ragged lists) across ranks
+    (shards balanced by Σ_r K_qr): boundary r is the query boundary
+    nearest to r/world of the entries, so each lies within half a query of its
+    target.  Contiguous query ranges, in query order."""
+    qoff = np.asarray(list_off, dtype=np.int64)[:: n_retrievers]
+    qoff = qoff - qoff[0]  # (a slice of a larger run set: offsets relative to its start)
     total = int(qoff[-1])
-    targets = [total * r // world for r in range(world + 1)]
-    b = np.searchsorted(qoff, targets, side="left")
+    targets = np.array([total * r // world for r in range(world + 1)], dtype=np.int64)
+    hi = np.clip(np.searchsorted(qoff, targets, side="left"), 0, len(qoff) - 1)
+    lo = np.clip(hi - 1, 0, len(qoff) - 1)
+    b = np.where(targets - qoff[lo] < qoff[hi] - targets, lo, hi)
     b[0], b[-1] = 0, len(qoff) - 1
     return np.maximum.accumulate(b)
 

@@ -188,3 +188,72 @@ def test_topk_gather_preallocated_unequal_shards(world, total):
                 + 100000 * r + 10 * step
             np.testing.assert_array_equal(d, want)
             assert s.tobytes() == (want.astype(np.float64) / 3).tobytes()
+
+
+def _topk_rows(off, R, k, methods, docid, score):
+    """[Q, M, k] top-k (docid, score) rows of every query of a run set through the C
+    oracle (what engine.fused_topk packs on device): rank i's docid and score, padded
+    with docid -1 / NaN past the union."""
+    from oracle import _loader as coracle
+    Q = (len(off) - 1) // R
+    d = np.full((Q, len(methods), k), -1, np.int32)
+    s = np.full((Q, len(methods), k), np.nan)
+    for m, name in enumerate(methods):
+        ud, uc, perm, fz = coracle.fuse(off, docid, score, R, name, 60)
+        for q in range(Q):
+            b, n = int(off[q * R]), min(int(uc[q]), k)
+            d[q, m, :n] = ud[b + perm[b:b + n].astype(np.int64)].view(np.int32)
+            s[q, m, :n] = fz[b:b + n]
+    return d, s
+
+
+def _entries_shard_worker(rank, world, port, off, docid, score, R, k, methods, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qppfuse.dist import TopkGather, shard_by_entries
+    plan = shard_by_entries(off, R, world)  # every rank derives the same boundaries
+    b, e = int(plan[rank]), int(plan[rank + 1])
+    sizes = np.diff(plan).tolist()
+    g = TopkGather(sizes, len(methods), k, "cpu", dst=0)
+    dd, ss = g.buffers(0)
+    d, s = _topk_rows(off[b * R:e * R + 1], R, k, methods, docid, score)  # this rank's shard
+    dd[:e - b].copy_(torch.from_numpy(d))
+    ss[:e - b].copy_(torch.from_numpy(s))
+    res = g.start(0).wait()
+    out[rank] = None if res is None else [(x.numpy().copy(), y.numpy().copy()) for x, y in res]
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shard_by_entries_ragged_gather_equals_single_process(world):
+    """bench.py's total-split workloads (C3, C4) shard by Σ entries (SURVEY §8(e):
+    "balanced by Σ_r K_qr"), not by query count: on ragged lists (0-1,500 entries per
+    list, some queries 10x heavier) each rank fuses its dist.shard_by_entries shard,
+    packs its top-k rows and TopkGather collects them on rank 0 (gloo) — the gathered
+    rows, concatenated in rank order, equal a single process's rows for every query,
+    and the shards' entry totals are balanced to within one query."""
+    rng = np.random.default_rng(11)
+    R, Q, k, methods = 3, 60, 20, ["combsum", "rrf"]
+    lens = rng.integers(0, 150, Q * R)
+    lens[rng.integers(0, Q * R, 12)] = rng.integers(900, 1500, 12)  # heavy queries
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    docid = np.concatenate([rng.choice(5000, n, replace=False) for n in lens]).astype(np.uint32)
+    score = np.concatenate([np.sort(rng.random(n))[::-1] for n in lens])
+    from qppfuse.dist import shard_by_entries
+    plan = shard_by_entries(off, R, world)
+    per = np.array([int(off[plan[i + 1] * R] - off[plan[i] * R]) for i in range(world)])
+    qtot = off[R::R] - off[:-1:R]
+    # every boundary within half a query of its target: each shard within one query
+    assert np.abs(per - off[-1] / world).max() <= qtot.max()
+    want_d, want_s = _topk_rows(off, R, k, methods, docid, score)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_entries_shard_worker,
+             args=(world, _free_port(), off, docid, score, R, k, methods, out),
+             nprocs=world, join=True)
+    got = out[0]
+    assert len(got) == world
+    d = np.concatenate([x for x, _ in got])
+    s = np.concatenate([y for _, y in got])
+    np.testing.assert_array_equal(d, want_d)
+    assert s.tobytes() == want_s.tobytes()
