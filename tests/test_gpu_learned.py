@@ -19,11 +19,15 @@ pytestmark = pytest.mark.gpu
 
 GOLD = Path(__file__).resolve().parent / "golden" / "lgbm"
 NAMES = ["fusion_multioutput", "fusion_per_retriever"]
+# every LightGBM model the reference holds (data/{nq,hotpotqa,scifact}/models): corpus_name
+MODELS = [f"{c}_{n}" for c in ("nq", "hotpotqa", "scifact") for n in NAMES]
 
 
 def _model(name):
     from qppfuse import lgbm
-    return lgbm.load_fusion_model(GOLD / f"nq_{name}.json.gz")
+    if not name.startswith(("nq_", "hotpotqa_", "scifact_")):
+        name = f"nq_{name}"
+    return lgbm.load_fusion_model(GOLD / f"{name}.json.gz")
 
 
 def _X(rng, n, f):
@@ -34,7 +38,7 @@ def _X(rng, n, f):
     return X
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", MODELS)
 def test_gbdt_predict_matches_restatement(gpu, name):
     from qppfuse import engine, lgbm
     m = _model(name)
@@ -84,7 +88,7 @@ def test_gbdt_model_beyond_lds_walks_global_arrays(gpu):
     assert got2.tobytes() == want2.tobytes()
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", MODELS)
 def test_learned_gbdt_weights_one_launch_equals_three(gpu, name):
     """qf_learned_gbdt_weights (features from the QPP micro-units, the walk and the
     weight normalisation in one launch) == qf_qpp_features + qf_gbdt_predict +
@@ -174,7 +178,7 @@ def _runs(rng, qids, rankers, k, overlap=0.6, ties=False):
     return frames
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", MODELS)
 @pytest.mark.parametrize("ties", [False, True])
 def test_learned_fusion_matches_reference_pandas(gpu, name, ties, tmp_path, capsys):
     from qppfuse import fusion
@@ -185,7 +189,7 @@ def test_learned_fusion_matches_reference_pandas(gpu, name, ties, tmp_path, caps
     runs = _runs(rng, qids, rankers, 40, ties=ties)
     qpp = {q: {r: [float(np.round(v, 6)) for v in rng.uniform(0, 1, 13)]
                for r in model.retrievers if rng.random() < 0.9} for q in qids[:-3]}
-    got = fusion.learned_fusion(runs, qpp, str(GOLD / f"nq_{name}.json.gz"))
+    got = fusion.learned_fusion(runs, qpp, str(GOLD / f"{name}.json.gz"))
     wd = lgbm_oracle.weights_dict(runs, qpp, model)
     want = ref_port.learned_fusion_from_weights(runs, wd, len(model.retrievers))
     assert list(got.keys()) == sorted(want.keys())

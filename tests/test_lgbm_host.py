@@ -94,10 +94,11 @@ def test_weight_normalisation_is_the_references_numpy():
     np.testing.assert_array_equal(w[50:], ok / np.where(sums == 0, 1.0, sums))
 
 
+@pytest.mark.parametrize("corpus", ["nq", "hotpotqa", "scifact"])
 @pytest.mark.parametrize("name", ["fusion_multioutput", "fusion_per_retriever"])
-def test_fixtures_load_and_pack(name):
+def test_fixtures_load_and_pack(name, corpus):
     from qppfuse import lgbm
-    m = lgbm.load_fusion_model(GOLD / f"nq_{name}.json.gz")
+    m = lgbm.load_fusion_model(GOLD / f"{corpus}_{name}.json.gz")
     assert m.retrievers == ["BGE", "BM25", "BM25_MonoT5", "BM25_TCT", "Splade"]
     assert m.n_qpp == 13 and len(m.boosters) == 5
     p = lgbm.pack_model(m)
@@ -106,13 +107,14 @@ def test_fixtures_load_and_pack(name):
 
 
 @pytest.mark.skipif(not REF_MODELS.exists(), reason="reference checkout not present")
+@pytest.mark.parametrize("corpus", ["nq", "hotpotqa", "scifact"])
 @pytest.mark.parametrize("name", ["fusion_multioutput", "fusion_per_retriever"])
-def test_static_pickle_reader_matches_fixture(name):
+def test_static_pickle_reader_matches_fixture(name, corpus):
     """The committed fixture is exactly what the static decoder reads from the pickle."""
     from qppfuse import lgbm
-    pkl = REF_MODELS / f"{name}.pkl"
+    pkl = REF_MODELS.parent.parent / corpus / "models" / f"{name}.pkl"
     m = lgbm.load_fusion_model(pkl)
-    with gzip.open(GOLD / f"nq_{name}.json.gz", "rt") as fh:
+    with gzip.open(GOLD / f"{corpus}_{name}.json.gz", "rt") as fh:
         fx = json.load(fh)
     assert lgbm.model_to_fixture(m, lgbm.booster_texts(pkl)) == fx
 
