@@ -3331,6 +3331,13 @@ hipError_t fuse_launch(const FuseParams& p0, int kind, int max_entries, hipStrea
     // ranked by bsort_core in the join's dead LDS: 349-352 us against join 126 +
     // bsort 202-204 us; the six sorts in turn at 3 workgroups per CU lose more than
     // the HBM re-read they save.)
+    // (Measured, not kept, round 6 — profiles/r06_ab_list_join.txt: for one- and
+    // two-method calls a "list-phased" join — after the insert and numbering, each
+    // method's sums accumulated over u in LDS list by list (barrier-ordered, retriever
+    // order, bit-identical), no contribution groups: W-CombSUM 120 vs 115 us, CombSUM
+    // + RRF 154-175 vs 134 us on SURVEY 8(d)'s C2 — the groups it removes cost less
+    // than its per-list passes; the method-independent cost is the hash insert and
+    // the loads, which it keeps.)
     // (Measured, not kept, round 6 — profiles/r06_ab_join_sort_and_chunks.txt: the join
     // and every slot's sort in one 1,024-thread workgroup per query, each slot re-read
     // by the thread that stored it, 500-561 us against this pair's 485-503; and
