@@ -1821,9 +1821,16 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
   // ---- exclusive scan of the counters -> u16 starts in bk ----------------------------
   {
     constexpr int kPer = NB / BLOCK;  // counters per thread
-    static_assert(kPer == 8, "two uint4 counter loads per thread");
-    const uint4 c0 = ((const uint4*)cnt)[tid * 2], c1 = ((const uint4*)cnt)[tid * 2 + 1];
-    uint32_t c[kPer] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    static_assert(kPer == 8 || kPer == 4, "one or two uint4 counter loads per thread");
+    uint32_t c[kPer];
+    if constexpr (kPer == 8) {
+      const uint4 c0 = ((const uint4*)cnt)[tid * 2], c1 = ((const uint4*)cnt)[tid * 2 + 1];
+      c[0] = c0.x; c[1] = c0.y; c[2] = c0.z; c[3] = c0.w;
+      c[4] = c1.x; c[5] = c1.y; c[6] = c1.z; c[7] = c1.w;
+    } else {  // (1,024 threads: join_learned_kernel)
+      const uint4 c0 = ((const uint4*)cnt)[tid];
+      c[0] = c0.x; c[1] = c0.y; c[2] = c0.z; c[3] = c0.w;
+    }
     uint32_t tot = 0u;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -1837,10 +1844,14 @@ __device__ __forceinline__ bool bsort_core(const FuseParams& p, unsigned char* l
     uint32_t pre = incl - tot;
 #pragma unroll
     for (int w = 0; w < WAVES - 1; ++w) pre += w < wid ? sm.wtot[w] : 0u;
-    ((uint4*)bk)[tid] = make_uint4((pre + c[0]) | ((pre + c[1]) << 16),
-                                   (pre + c[2]) | ((pre + c[3]) << 16),
-                                   (pre + c[4]) | ((pre + c[5]) << 16),
-                                   (pre + c[6]) | ((pre + c[7]) << 16));
+    if constexpr (kPer == 8)
+      ((uint4*)bk)[tid] = make_uint4((pre + c[0]) | ((pre + c[1]) << 16),
+                                     (pre + c[2]) | ((pre + c[3]) << 16),
+                                     (pre + c[4]) | ((pre + c[5]) << 16),
+                                     (pre + c[6]) | ((pre + c[7]) << 16));
+    else
+      ((uint2*)bk)[tid] = make_uint2((pre + c[0]) | ((pre + c[1]) << 16),
+                                     (pre + c[2]) | ((pre + c[3]) << 16));
     if (tid == 0) bk[NB] = (uint16_t)U;
   }
   __syncthreads();
@@ -2397,8 +2408,8 @@ constexpr int kLearnedUMax = 4608;
 template <class C>
 __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(FuseParams p) {
   constexpr int BLOCK = C::kBlock, ROWS = (kLearnedUMax + BLOCK - 1) / BLOCK;
-  static_assert(BLOCK == 512, "bsort_core is instantiated for 512 threads");
-  constexpr int kSortLds = BsLds<12, true, kLearnedUMax>::kBytes;
+  static_assert(BLOCK == 512 || BLOCK == 1024, "bsort_core's configurations");
+  constexpr int kSortLds = BsLds<12, true, kLearnedUMax, BLOCK>::kBytes;
   __shared__ JoinShared<C, 1, kSortLds> sh;
   __shared__ BsShared<BLOCK / 64> sm;
   const int64_t q = block_id();
@@ -2440,6 +2451,8 @@ __global__ __launch_bounds__(C::kBlock, C::kMinWaves) void join_learned_kernel(F
     }
   }
   if (tid == 0) p.union_count[q] = U;
+  QF_STOP(40, [&] { uint32_t a = 0u; for (int j = 0; j < ROWS; ++j) a += d[j] + (uint32_t)__double2loint(v[j]); return a; },
+          if (_qf_acc == 12345u) p.union_count[q] = 0; return;);
   __syncthreads();  // the groups are dead: their LDS is the sort's
   bsort_core<BLOCK, 12, true, kLearnedUMax>(p, sh.smem, sm, v, d, U, wid * 64, BLOCK, base);
 }
@@ -3213,7 +3226,11 @@ __global__ __launch_bounds__(kXlBlock, 8) void join_sort_xl_kernel(FuseParams p,
 using JoinT = JoinCfg<64, 5, 10, 6>;  // N <= 320: one wave per query (C1)
 using JoinS = JoinCfg<256, 4, 11>;    // N <= 1024
 using JoinM = JoinCfg<512, 10, 13, 6>;  // N <= 5120 (3 per CU with micro-unit scores)
+#ifdef QF_LEARNED_512  // (A/B builds: round 5's 512-thread form)
 using JoinML = JoinCfg<512, 10, 13, 4>;  // join_learned_kernel: 2 per CU (its sort's LDS)
+#else
+using JoinML = JoinCfg<1024, 5, 13, 8>;  // join_learned_kernel: 2 per CU, 32 waves per CU
+#endif
 using JoinL = JoinCfg<768, 10, 14>;   // N <= 7680
 using JoinXL = JoinCfg<1024, 10, 14>; // N <= 10240 (e.g. 10 runs x top-1000; 143 KB LDS)
 using SortT = SortCfg<64, 5, 8>;      // U <= 320: one wave per (query, method) (C1)
@@ -3350,7 +3367,7 @@ hipError_t fuse_launch(const FuseParams& p0, int kind, int max_entries, hipStrea
     // was left unsorted)
     p.fast_reach = max_entries > kJsUMax ? kFastUMaxL : kJsUMax;
     if (learned_only) {  // join + sort in one kernel (C5)
-      hipLaunchKernelGGL((join_learned_kernel<JoinML>), grid_for(p.n_queries), dim3(512), 0, st,
+      hipLaunchKernelGGL((join_learned_kernel<JoinML>), grid_for(p.n_queries), dim3(JoinML::kBlock), 0, st,
                          p);
     } else {
       if (max_entries <= JoinM::kNMax) launch_join<JoinM>(p, kind, st);
