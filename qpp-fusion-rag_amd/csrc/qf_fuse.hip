@@ -618,11 +618,13 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
   __syncthreads();
   const int64_t base = sh.off[0];
   const int64_t N64 = sh.off[R] - base;
-  if (p.qpp_micro) {  // uniform (qf_fuse_qpp_micro): the .qpp values of this query's lists
-    // every column of every list, src/qpp.py:356-372 + the "%.6f" of :333 —
-    // qpp_normalize_kernel's micro_out, one value per thread past wave 0 (whose
-    // per-list threads compute the weights below); before the size check, so a query
-    // the workspace join takes still gets its values
+  // qf_fuse_qpp_micro: the .qpp values of this query's lists — every column of every
+  // list, src/qpp.py:356-372 + the "%.6f" of :333, qpp_normalize_kernel's micro_out —
+  // one value per thread past wave 0 (whose per-list threads compute the weights),
+  // issued after the entries' loads (its loads' wait then overlaps theirs: issued
+  // before them, it cost the join ~8 us on C2); a query the workspace join takes
+  // gets its values before the early return
+  auto qpp_micro = [&]() __attribute__((always_inline)) {
     const int t2 = BLOCK > 64 ? (tid + BLOCK - 64) % BLOCK : tid;
     for (int i = t2; i < R * kQppCols; i += BLOCK) {
       const int r = i / kQppCols, c = i - r * kQppCols;
@@ -634,8 +636,9 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
       p.qpp_micro[l * kQppCols + c] =
           round6(qpp_norm_value(p.qpp_raw[l * kQppCols + c], m0, m1, mode, present));
     }
-  }
+  };
   if (N64 > NMAX) {  // uniform
+    if (p.qpp_micro) qpp_micro();
     if (tid == 0) p.union_count[q] = QF_QSTATUS_TOOBIG;
     return -1;
   }
@@ -674,6 +677,7 @@ __device__ __forceinline__ int join_groups(const FuseParams& p, JoinShared<C, KI
                      ((aw > 0x1p-900 && aw < 0x1p900) ? 0 : 2);
     if (slow) atomicOr(&sh.slow, slow);
   }
+  if (p.qpp_micro) qpp_micro();  // uniform
   for (int i = tid * 4; i < TS; i += BLOCK * 4)
     *(uint4*)&tkey[i] = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
   for (int i = tid * 4; i < TS / 2; i += BLOCK * 4)
