@@ -919,6 +919,9 @@ def main():
             c = cpu_baseline_port(p, per_worker, workers)
             cpu = {"value": c["value"], "unit": "fused queries/s", "cores": c["workers"],
                    "kind": "port",
+                   # "state nproc" — the host's CPUs and this process's share
+                   "host_nproc": os.cpu_count(),
+                   "host_cpus_allowed": len(os.sched_getaffinity(0)),
                    "sample": f"{c['sample_queries']} queries x {args.retrievers} x top-{args.k}"
                              f"{' + 13 QPP predictors' if args.wl['qpp'] else ''} + "
                              f"{len(p.methods)} fusion(s) through oracle/ref_port.py (the "
