@@ -95,7 +95,8 @@ def parse():
     ap.add_argument("--qpp-index", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="queries per CPU-baseline process timed through the Python port of "
-                         "the reference (0 = skip; default: the workload's, ~10 s each)")
+                         "the reference (0 = skip; default: the workload's — C2's 125 x 16 "
+                         "processes are SURVEY §8(d)'s 2,000-query sample, ~50 s)")
     ap.add_argument("--cpu-workers", type=int, default=None,
                     help="processes the CPU baseline runs on (default min(16, cpu_count))")
     ap.add_argument("--native-sample", type=int, default=400,
