@@ -844,6 +844,52 @@ def test_fuse_qpp_weights_in_kernel_equal_normalize_then_fuse(gpu, mode, qidx, R
         s, u = int(lo[q * R]), int(uc[q])
         assert fa[:, s:s + u].tobytes() == fb[:, s:s + u].tobytes(), q
         assert np.array_equal(pa[:, s:s + u], pb[:, s:s + u]), q
+    # qf_fuse_qpp_micro: the same fusion plus every list's 13 ".qpp" micro-units,
+    # written by the join (each join configuration) — qpp_normalize's, bit for bit
+    qm = torch.full((Q * R * 13,), -7, dtype=torch.int64, device=gpu)
+    if R > 16:  # the workspace join (more runs than the LDS join's masks) writes none
+        with pytest.raises(Exception):
+            engine.fuse(off2, docid2, micro, R, M, 60, max_entries=R * K,
+                        qpp=(qraw, stats, mode, qidx), qpp_micro_out=qm)
+        return
+    c = engine.fuse(off2, docid2, micro, R, M, 60, max_entries=R * K,
+                    qpp=(qraw, stats, mode, qidx), qpp_micro_out=qm)
+    want = engine.qpp_normalize(qraw, stats, off2, R, mode, qidx)["micro"]
+    assert torch.equal(qm, want.reshape(-1).to(torch.int64))
+    assert torch.equal(c.union_count, b.union_count)
+    fc, pc = c.fused.cpu().numpy(), c.perm.cpu().numpy()
+    for q in range(Q):
+        s, u = int(lo[q * R]), int(uc[q])
+        assert fc[:, s:s + u].tobytes() == fb[:, s:s + u].tobytes(), q
+        assert np.array_equal(pc[:, s:s + u], pb[:, s:s + u]), q
+
+
+@pytest.mark.parametrize("max_entries", [2000, 12000])
+def test_fuse_qpp_micro_for_queries_past_the_lds_join(gpu, max_entries):
+    """qf_fuse_qpp_micro writes the .qpp micro-units of a query the LDS join does not
+    take: reported QF_QSTATUS_TOOBIG (max_entries 2,000 below its 2,400 x 5 entries) or
+    joined by the workspace kernel (max_entries 12,000 > 10,240) — the values come from
+    the LDS join's early exit either way."""
+    from qppfuse import engine
+    Q, R, K = 24, 5, 2400
+    off, docid, raw = engine.synth_runs(5, Q, R, K)
+    _, micro = engine.minmax_per_query(raw, off, want_norm=False)
+    nt = torch.full((Q,), 4, dtype=torch.int32, device=gpu)
+    tf = torch.rand((Q, 2), dtype=torch.float64, device=gpu,
+                    generator=torch.Generator(gpu).manual_seed(3))
+    qraw = engine.qpp_raw(raw, off, R, 100, nt, tf)
+    stats = engine.qpp_colminmax(qraw, off, R)
+    qm = torch.full((Q * R * 13,), -7, dtype=torch.int64, device=gpu)
+    out = engine.fuse(off, docid, micro, R, ["wcombsum", "rrf"], 60, max_entries=max_entries,
+                      qpp=(qraw, stats, "minmax", 5), qpp_micro_out=qm)
+    want = engine.qpp_normalize(qraw, stats, off, R, "minmax", 5)["micro"]
+    assert torch.equal(qm, want.reshape(-1).to(torch.int64))
+    from qppfuse import _lib
+    uc = out.union_count.cpu().numpy()
+    if max_entries < R * K:
+        assert (uc == _lib.QF_QSTATUS_TOOBIG).all()
+    else:
+        assert (uc > 0).all()
 
 
 def _bs_key2(smin, smax, shift=8, minbase=3840):
