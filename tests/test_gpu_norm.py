@@ -30,14 +30,17 @@ def test_minmax_bit_exact_and_micro_is_python_format(gpu):
 
 @pytest.mark.parametrize("n_lists", [1, 7, 32768, 32769])
 def test_minmax_batch_sizes_and_list_lengths(gpu, n_lists):
-    """One to 32,769 lists of 0-1,100 entries (the register path up to 1,024, the
-    loop beyond), odd counts: bit-exact, and the micro-units are "%.6f"."""
+    """One to 32,769 lists of 0-1,100 entries (the 4-row register body up to 256, the
+    16-row one up to 1,024, the loop beyond, and each boundary), odd counts:
+    bit-exact, and the micro-units are "%.6f"."""
     from qppfuse import engine
     rng = np.random.default_rng(n_lists)
     lens = rng.integers(0, 80, n_lists)
     lens[rng.random(n_lists) < 0.05] = 512
     lens[rng.random(n_lists) < 0.02] = 513
     lens[rng.random(n_lists) < 0.01] = 1100
+    edge = [256, 257, 255, 1024, 1025, 100, 64, 65]
+    lens[:min(len(edge), n_lists)] = edge[:n_lists]
     off = np.cumsum(np.concatenate([[0], lens])).astype(np.int64)
     flat = np.repeat(rng.normal(0, 5, n_lists), lens) + rng.random(int(off[-1]))
     norm, micro = engine.minmax_per_query(torch.from_numpy(flat).to(gpu),
